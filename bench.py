@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 3-D isotropic-elastic CubicGrid stage loop, 512^3, fp64.
+
+One step = one full time step of cubic::Engine::nextTimeStep (all three stages,
+engine/cubic/Engine.cpp:90-121) over the whole grid, inputs resident in HBM.
+`python bench.py --gpus N --steps K --warmup W`; for N > 1 the driver launches
+one rank per GPU (torch.distributed.run) and the 512^3 grid is split into
+N X-slabs with an RCCL halo exchange of the X ghost planes every step
+(strong scaling: the total work is fixed).
+
+Prints ONE JSON line on rank 0 (see README/DESIGN for the fields).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+BYTES_PER_NODE_STAGE = 2 * 9 * 8  # read + write the 9-component fp64 state
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n", type=int, default=512, help="global grid edge (nodes)")
+    p.add_argument("--path", default="auto", choices=["auto", "generic", "split", "fused"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-profile", action="store_true",
+                   help="skip the per-kernel event timing pass")
+    return p.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """Oracle (C restatement, OpenMP over x) on a bounded 3-D sample of the same
+    workload: 96^3 parity-random field, (4,2,1), bs 2, tau 0.9."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    N = 96
+    t = O.Task(D=3, border_size=2, h=[1, 1, 1], cubics={0: ([N] * 3, [0] * 3)}, courant=0.9,
+               default_material=O.Material(4, 2, 1), number_of_snaps=1)
+    b = O.Engine(t).bodies[0]
+    O.fill_random(b, [N, N, N], 0x5EED)
+    b.stage(0, 0.9, threads)  # warm
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        for s in range(3):
+            b.stage(s, 0.9, threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 200:
+            break
+    rate = N ** 3 * steps / el / 1e6
+    return {"value": rate, "unit": "Mnode-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle C restatement, 96^3 parity-random, {steps} steps in {el:.1f} s "
+                      f"({threads} OpenMP threads)"}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gcm_amd
+    from gcm_amd import gcmx
+    paths = {"auto": gcmx.PATH_AUTO, "generic": gcmx.PATH_GENERIC, "split": gcmx.PATH_SPLIT,
+             "fused": gcmx.PATH_FUSED}
+
+    N = a.n
+    if N % world:
+        raise SystemExit("grid edge must be divisible by the number of ranks")
+    X = N // world
+    x0 = rank * X
+    device = local if torch.cuda.device_count() > 1 else 0
+    # material (4,2,1): ElasticModel<3> matrices built by the host mirror
+    from gcm_amd.host import isotropic_elastic_matrices
+    U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
+    tau = 0.9 * 1.0 / 1.0  # Courant * h / max|lambda| (Engine.cpp:124-140)
+
+    t_setup = time.perf_counter()
+    ctx = gcm_amd.Context(3, 2, [X, N, N], start=[x0, 0, 0], device=device)
+    ctx.set_materials(U[None], U1[None], L[None])
+    ctx.set_path(paths[a.path])
+    ctx.fill_random([N, N, N], 0x5EED)
+    if world > 1:
+        uid = gcm_amd.unique_id() if rank == 0 else None
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(obj[0], world, rank, rank - 1 if rank > 0 else -1,
+                      rank + 1 if rank < world - 1 else -1)
+    ctx.sync()
+    log(f"[rank {rank}] slab x[{x0},{x0 + X}) of {N}^3, {ctx.device_bytes / 1e9:.1f} GB, "
+        f"path {ctx.effective_path}, setup {time.perf_counter() - t_setup:.1f}s")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        ctx.step(tau)
+    ctx.sync()
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.step(tau)
+    ctx.sync()
+    barrier()
+    t1 = time.perf_counter()
+    el = t1 - t0
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    # Per-kernel live timing: the same steps again with hipEvents around every
+    # launch on the context stream (kept out of the headline timed region).
+    kernels = {}
+    if not a.no_profile:
+        ctx.profile(True)
+        ctx.profile_reset()
+        barrier()
+        for _ in range(a.steps):
+            ctx.step(tau)
+        ctx.sync()
+        kernels = ctx.profile_read()
+        ctx.profile(False)
+        barrier()
+
+    total_nodes = N ** 3
+    value = total_nodes * a.steps / el / 1e6
+    roof = None
+    if kernels:
+        dom_name, dom = max(kernels.items(), key=lambda kv: kv[1]["total_ms"])
+        avg_ms = dom["total_ms"] / max(1, dom["launches"])
+        achieved = dom["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                rec = json.load(open(pmc))
+                k = rec.get("kernels", {}).get(dom_name)
+                if k and rec.get("n") == N and rec.get("ranks", 1) == world:
+                    traffic = k.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": dom_name, "kernel_avg_ms": round(avg_ms, 4),
+                "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
+                "kernels": {k: {"avg_ms": round(v["total_ms"] / max(1, v["launches"]), 4),
+                                "GBps": round(v["bytes_per_launch"] /
+                                              (v["total_ms"] / max(1, v["launches"]) * 1e-3) /
+                                              1e9, 1)}
+                            for k, v in kernels.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(a.cpu_seconds)
+        except Exception as e:  # the baseline is reported, never required
+            log(f"cpu baseline failed: {e}")
+
+    if rank == 0:
+        step_bytes = 3 * BYTES_PER_NODE_STAGE * total_nodes  # per-stage algorithmic model
+        out = {
+            "metric": "Mnode-steps/sec + achieved HBM GB/s, 3D isotropic elastic 512³ CubicGrid",
+            "value": round(value, 1),
+            "unit": "Mnode-steps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic parity-random field (SplitMix64 seed 0x5EED), material (4,2,1)",
+            "config": {"workload": f"3-D isotropic elastic CubicGrid {N}^3, borderSize 2, "
+                                   f"Courant 0.9, tau 0.9, one full time step (3 stages)",
+                       "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,
+                       "parallelism": f"x-slab{world}" if world > 1 else "single"},
+            "effective_GBps_per_stage_model": round(step_bytes * a.steps / el / 1e9, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,12 @@
+"""gcm_amd -- MI355X-native grid-characteristic elastic-wave stepper.
+
+The hot path (libgcm's cubic stage loop) lives in ``lib/libgcmx.so``: hand-written
+gfx950 HIP kernels behind the C-ABI declared in ``include/gcmx.h``.  This package
+holds the Python side of that boundary (``gcm_amd.gcmx``) and the host mirror of
+the reference's Engine / Task / factory surface (``gcm_amd.engine``).
+"""
+from .gcmx import (Context, GcmxError, LIB_PATH, PATH_AUTO, PATH_FUSED, PATH_GENERIC,
+                   PATH_SPLIT, lib, pde_size, unique_id)
+
+__all__ = ["Context", "GcmxError", "LIB_PATH", "PATH_AUTO", "PATH_FUSED", "PATH_GENERIC",
+           "PATH_SPLIT", "lib", "pde_size", "unique_id"]

@@ -1,0 +1,87 @@
+// common.hpp -- device layout, per-axis stage tables and the Newton/min-max
+// interpolation shared by every gcmx kernel.
+//
+// Layout: one time layer = M component planes (SoA).  A
+// plane is the ghost-padded grid with the reference's axis order (X slowest,
+// last axis fastest, CubicGrid.hpp:202-225).  The fastest axis is padded so
+// that its first INNER node sits at a 128-byte boundary and every row is a
+// multiple of 16 doubles: a wavefront reading 64 consecutive inner nodes of one
+// component touches exactly four whole 128-byte lines.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gcmx {
+
+constexpr int kMaxM = 9;
+constexpr int kMaxBs = 8;
+constexpr int kRowAlign = 16;  // doubles (128 B)
+
+__host__ __device__ constexpr int pde_size(int D) { return D + D * (D + 1) / 2; }
+
+// Geometry of one context's device layers.
+struct Geo {
+	int D, M, bs;
+	int sizes[3];          // inner nodes (1 for axes >= D)
+	long long stride[3];   // element strides (0 for axes >= D)
+	long long origin;      // element offset of inner node (0,0,0)
+	long long cs;          // component (plane) stride in elements
+	long long n_inner;
+	int lead;              // padding in front of the first ghost of a row
+	long long row;         // padded length of the fastest axis
+};
+
+// Per (material, axis) table: the matrices plus everything the stage derives
+// from L and tau on the host (crossingPoints, GridCharacteristicMethod.hpp:56-59;
+// q = |dx|/h and the Newton coefficients ((q - i) + 1) / i,
+// EqualDistanceLineInterpolator.hpp:58-69), computed once per tau in IEEE double
+// exactly as the reference does per node.
+struct AxisTable {
+	double U[kMaxM * kMaxM];
+	double U1[kMaxM * kMaxM];
+	double coef[kMaxM][kMaxBs];
+	int shift[kMaxM];   // +1 / -1: side the characteristic foot lies on
+	int kf[kMaxM];      // floor(q): interval holding the foot
+	int zero_q[kMaxM];  // q == 0 exactly: interpolation returns the node value
+	int pad_[kMaxM];
+};
+
+// EqualDistanceLineInterpolator::minMaxInterpolate for ONE component
+// (EqualDistanceLineInterpolator.hpp:18-43 + 56-71).  s[0..BS] are the values
+// at the node and its BS neighbours on the foot side.  The Newton recurrence
+// is unrolled in the reference's order; the limiter bounds come from the
+// original values s[kf], s[kf+1].
+template <int BS>
+__device__ __forceinline__ double newton_minmax(const double (&s)[BS + 1], int kf,
+                                                const double* __restrict__ coef) {
+	double lo = s[0], hi = s[1];
+#pragma unroll
+	for (int i = 1; i < BS; i++)
+		if (kf == i) { lo = s[i]; hi = s[i + 1]; }
+	const double mx = fmax(lo, hi);
+	const double mn = fmin(lo, hi);
+	double d[BS + 1];
+#pragma unroll
+	for (int i = 0; i <= BS; i++) d[i] = s[i];
+	double ans = d[0];
+#pragma unroll
+	for (int i = 1; i <= BS; i++) {
+		const double c = coef[i - 1];
+#pragma unroll
+		for (int j = 0; j <= BS - i; j++) d[j] = (d[j + 1] - d[j]) * c;
+		ans += d[0];
+	}
+	if (ans > mx) ans = mx;
+	else if (ans < mn) ans = mn;
+	return ans;
+}
+
+// Same with compile-time coefficients held in registers by the caller.
+template <int BS>
+__device__ __forceinline__ double newton_minmax_r(const double (&s)[BS + 1], int kf,
+                                                  const double (&coef)[BS]) {
+	return newton_minmax<BS>(s, kf, coef);
+}
+
+}  // namespace gcmx

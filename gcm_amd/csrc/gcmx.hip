@@ -1,0 +1,826 @@
+// gcmx.hip -- the C-ABI (include/gcmx.h): device contexts, layout transforms,
+// per-tau stage tables, kernel-path selection, RCCL X-slab halo exchange and
+// per-kernel event timing.
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gcmx.h"
+#include "common.hpp"
+#include "launch.hpp"
+
+using namespace gcmx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+gcmx_status fail(gcmx_status s, const std::string& msg) {
+	g_last_error = msg;
+	return s;
+}
+
+#define HIP_TRY(expr)                                                                   \
+	do {                                                                                \
+		hipError_t e_ = (expr);                                                         \
+		if (e_ != hipSuccess)                                                           \
+			return fail(GCMX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+	} while (0)
+
+struct PendingTiming {
+	int bucket;
+	hipEvent_t a, b;
+};
+
+struct Bucket {
+	std::string name;
+	double total_ms = 0;
+	long long launches = 0;
+	double bytes = 0;  // algorithmic bytes per launch (last launch)
+};
+
+}  // namespace
+
+struct gcmx_ctx {
+	int device = 0;
+	hipStream_t stream = nullptr;
+	hipStream_t comm_stream = nullptr;
+	hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+	gcmx_grid_desc desc{};
+	Geo geo{};
+	int D = 0, M = 0, bs = 0;
+	long long n_all = 0;         // reference all-nodes count
+	long long all_shape[3] = {1, 1, 1};
+	size_t layer_elems = 0;      // M * cs
+	double* cur = nullptr;
+	double* nxt = nullptr;
+	// materials
+	int n_mat = 0;
+	std::vector<double> U, U1, L;  // [mat][D][M*M], [mat][D][M]
+	uint8_t* mat_d = nullptr;      // inner nodes, linear inner order; null = homogeneous
+	AxisTable* tabs_d = nullptr;   // [mat][D]
+	double tabs_tau = NAN;
+	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso pattern)
+	bool ghosts_touched = false;   // border fills / contact copies happened
+	gcmx_path path = GCMX_PATH_AUTO;
+	// halo exchange
+	ncclComm_t comm = nullptr;
+	int nranks = 1, rank = 0, left = -1, right = -1;
+	std::vector<int> halo_comps;
+	// profiling
+	bool prof = false;
+	std::vector<Bucket> buckets;
+	std::vector<PendingTiming> pending;
+	// scratch for border fills
+	int* nodes_d = nullptr;
+	size_t nodes_cap = 0;
+	int* qs_d = nullptr;
+	double* vals_d = nullptr;
+};
+
+namespace {
+
+int bucket_id(gcmx_ctx* c, const char* name) {
+	for (size_t i = 0; i < c->buckets.size(); i++)
+		if (c->buckets[i].name == name) return (int)i;
+	c->buckets.push_back(Bucket{name});
+	return (int)c->buckets.size() - 1;
+}
+
+// Bracket one launch with events when profiling.
+struct Timed {
+	gcmx_ctx* c;
+	int b;
+	hipEvent_t a = nullptr, e = nullptr;
+	hipStream_t st;
+	Timed(gcmx_ctx* c_, const char* name, double bytes, hipStream_t s) : c(c_), b(-1), st(s) {
+		if (!c->prof) return;
+		b = bucket_id(c, name);
+		c->buckets[b].bytes = bytes;
+		hipEventCreate(&a);
+		hipEventCreate(&e);
+		hipEventRecord(a, st);
+	}
+	~Timed() {
+		if (b < 0) return;
+		hipEventRecord(e, st);
+		c->pending.push_back({b, a, e});
+	}
+};
+
+void drain_timings(gcmx_ctx* c) {
+	for (auto& p : c->pending) {
+		float ms = 0;
+		hipEventSynchronize(p.b);
+		hipEventElapsedTime(&ms, p.a, p.b);
+		c->buckets[p.bucket].total_ms += ms;
+		c->buckets[p.bucket].launches += 1;
+		hipEventDestroy(p.a);
+		hipEventDestroy(p.b);
+	}
+	c->pending.clear();
+}
+
+long long round_up(long long v, long long m) { return (v + m - 1) / m * m; }
+
+// Element offset (device layout) of node `it` (multi-index incl. ghosts).
+long long dev_offset(const Geo& g, const int it[3]) {
+	long long o = g.origin;
+	for (int d = 0; d < g.D; d++) o += (long long)it[d] * g.stride[d];
+	return o;
+}
+
+gcmx_status check_ctx(gcmx_ctx* c) {
+	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");
+	if (hipSetDevice(c->device) != hipSuccess) return fail(GCMX_ERR_HIP, "hipSetDevice failed");
+	return GCMX_OK;
+}
+
+// Per-tau tables: crossingPoints (GridCharacteristicMethod.hpp:56-59), q = |dx|/h
+// (:84), k = floor(q) with the reference's interpolation assertions
+// (EqualDistanceLineInterpolator.hpp:20-23) and the Newton coefficients (:58-66).
+gcmx_status build_tables(gcmx_ctx* c, double tau) {
+	if (c->n_mat <= 0) return fail(GCMX_ERR_STATE, "materials not set");
+	if (std::memcmp(&tau, &c->tabs_tau, sizeof(double)) == 0) return GCMX_OK;
+	const int D = c->D, M = c->M, bs = c->bs;
+	std::vector<AxisTable> h((size_t)c->n_mat * D);
+	for (int m = 0; m < c->n_mat; m++)
+		for (int s = 0; s < D; s++) {
+			AxisTable& t = h[(size_t)m * D + s];
+			std::memset(&t, 0, sizeof(t));
+			const double* Um = &c->U[((size_t)m * D + s) * M * M];
+			const double* U1m = &c->U1[((size_t)m * D + s) * M * M];
+			const double* Lm = &c->L[((size_t)m * D + s) * M];
+			for (int i = 0; i < M * M; i++) {
+				t.U[i] = Um[i];
+				t.U1[i] = U1m[i];
+			}
+			for (int k = 0; k < M; k++) {
+				const double dx = Lm[k] * (-tau);
+				const double q = std::fabs(dx) / c->desc.h[s];
+				if (!(q >= 0))
+					return fail(GCMX_ERR_CFL, "interpolation point q < 0 (reference assert_ge)");
+				const double kf = std::floor(q);
+				if (!(kf < bs)) {
+					char buf[256];
+					std::snprintf(buf, sizeof buf,
+					              "Courant too large: q = %.17g >= borderSize %d on axis %d "
+					              "(reference assert in minMaxInterpolate)", q, bs, s);
+					return fail(GCMX_ERR_CFL, buf);
+				}
+				t.shift[k] = (dx > 0) ? 1 : -1;
+				t.kf[k] = (int)kf;
+				t.zero_q[k] = (q == 0) ? 1 : 0;
+				for (int i = 1; i <= bs; i++) t.coef[k][i - 1] = ((q - i) + 1) / i;
+			}
+		}
+	HIP_TRY(hipMemcpyAsync(c->tabs_d, h.data(), h.size() * sizeof(AxisTable),
+	                       hipMemcpyHostToDevice, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	c->tabs_tau = tau;
+	return GCMX_OK;
+}
+
+// Components the X stage reads at the neighbours (those to put in the halo).
+void compute_halo_comps(gcmx_ctx* c) {
+	const int D = c->D, M = c->M;
+	c->halo_comps.clear();
+	for (int j = 0; j < M; j++) {
+		bool need = false;
+		for (int m = 0; m < c->n_mat && !need; m++)
+			for (int k = 0; k < M && !need; k++) {
+				const double Lk = c->L[((size_t)m * D + 0) * M + k];
+				if (Lk != 0.0 && c->U[(((size_t)m * D + 0) * M + k) * M + j] != 0.0) need = true;
+			}
+		if (need) c->halo_comps.push_back(j);
+	}
+}
+
+gcmx_status halo_exchange_impl(gcmx_ctx* c) {
+	if (!c->comm || (c->left < 0 && c->right < 0)) return GCMX_OK;
+	if (c->D < 2) return fail(GCMX_ERR_UNSUPPORTED, "X-slab halo needs dim >= 2");
+	if (c->halo_comps.empty()) return fail(GCMX_ERR_STATE, "materials not set");
+	const Geo& g = c->geo;
+	const long long plane = g.stride[0];
+	const size_t n = (size_t)(c->bs * plane);
+	const int X = g.sizes[0];
+	// ghost planes [-bs, 0) and [X, X+bs); inner planes [0, bs) and [X-bs, X).
+	// For D >= 2 the x-plane x (all y/z rows including ghosts and row padding)
+	// is the contiguous range [(x + bs) * stride0, (x + bs + 1) * stride0).
+	auto plane_ptr = [&](int comp, int x) {
+		return c->cur + (size_t)comp * g.cs + (size_t)((long long)(x + c->bs) * plane);
+	};
+	HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+	HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+	if (ncclGroupStart() != ncclSuccess) return fail(GCMX_ERR_COMM, "ncclGroupStart");
+	for (int comp : c->halo_comps) {
+		if (c->left >= 0) {
+			if (ncclSend(plane_ptr(comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream) != ncclSuccess ||
+			    ncclRecv(plane_ptr(comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream) != ncclSuccess)
+				return fail(GCMX_ERR_COMM, "ncclSend/Recv left");
+		}
+		if (c->right >= 0) {
+			if (ncclSend(plane_ptr(comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream) != ncclSuccess ||
+			    ncclRecv(plane_ptr(comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream) != ncclSuccess)
+				return fail(GCMX_ERR_COMM, "ncclSend/Recv right");
+		}
+	}
+	if (ncclGroupEnd() != ncclSuccess) return fail(GCMX_ERR_COMM, "ncclGroupEnd");
+	HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+	HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+	return GCMX_OK;
+}
+
+// Fast kernels: 3-D, one material, no per-node ids, isotropic zero pattern.
+void refresh_fast(gcmx_ctx* c) {
+	const int D = c->D, M = c->M;
+	bool fits = (D == 3) && (c->mat_d == nullptr) && (c->n_mat == 1);
+	for (int sx = 0; fits && sx < D; sx++)
+		fits = iso_pattern_fits(sx, &c->U[(size_t)sx * M * M], &c->U1[(size_t)sx * M * M],
+		                        &c->L[(size_t)sx * M]);
+	c->iso_fast = fits;
+}
+
+gcmx_path effective_path(gcmx_ctx* c) {
+	if (c->D != 3 || !c->iso_fast || c->bs > 3) return GCMX_PATH_GENERIC;
+	if (c->path == GCMX_PATH_GENERIC) return GCMX_PATH_GENERIC;
+	if (c->path == GCMX_PATH_SPLIT) return GCMX_PATH_SPLIT;
+	if (c->ghosts_touched || !fused_yz_supported(c->geo)) return GCMX_PATH_SPLIT;
+	return GCMX_PATH_FUSED;
+}
+
+double node_stage_bytes(const gcmx_ctx* c) { return 2.0 * c->M * sizeof(double); }
+
+gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
+	gcmx_status s = build_tables(c, tau);
+	if (s != GCMX_OK) return s;
+	if (axis == 0 && c->comm) {
+		s = halo_exchange_impl(c);
+		if (s != GCMX_OK) return s;
+	}
+	const Geo& g = c->geo;
+	const double bytes = node_stage_bytes(c) * (double)g.n_inner;
+	const AxisTable* tab = c->tabs_d + axis;  // material 0
+	const gcmx_path p = effective_path(c);
+	bool ok;
+	if (p == GCMX_PATH_GENERIC) {
+		Timed t(c, "stage_generic", bytes, c->stream);
+		ok = launch_stage_generic(c->cur, c->nxt, g, axis, c->tabs_d, c->mat_d, c->stream);
+	} else if (axis < 2) {
+		Timed t(c, axis == 0 ? "march_x" : "march_y", bytes, c->stream);
+		ok = launch_march(c->cur, c->nxt, g, axis, tab, 0, g.sizes[0], c->stream);
+	} else {
+		Timed t(c, "line_z", bytes, c->stream);
+		ok = launch_line_z(c->cur, c->nxt, g, tab, 0, g.sizes[0], c->stream);
+	}
+	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "no kernel variant for this configuration");
+	HIP_TRY(hipGetLastError());
+	std::swap(c->cur, c->nxt);
+	return GCMX_OK;
+}
+
+}  // namespace
+
+// =================================================================== ABI ==
+
+extern "C" {
+
+int gcmx_abi_version(void) { return GCMX_ABI_VERSION; }
+const char* gcmx_last_error(void) { return g_last_error.c_str(); }
+int gcmx_pde_size(int dim) { return (dim >= 1 && dim <= 3) ? pde_size(dim) : -1; }
+
+const char* gcmx_status_string(gcmx_status s) {
+	switch (s) {
+	case GCMX_OK: return "ok";
+	case GCMX_ERR_INVALID_ARG: return "invalid argument";
+	case GCMX_ERR_CFL: return "Courant condition violated";
+	case GCMX_ERR_HIP: return "HIP error";
+	case GCMX_ERR_OOM: return "out of device memory";
+	case GCMX_ERR_STATE: return "invalid call order";
+	case GCMX_ERR_UNSUPPORTED: return "unsupported configuration";
+	case GCMX_ERR_COMM: return "communication error";
+	}
+	return "unknown";
+}
+
+gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
+	if (!d || !out) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	*out = nullptr;
+	if (d->dim < 1 || d->dim > 3) return fail(GCMX_ERR_INVALID_ARG, "dim must be 1..3");
+	// CubicGrid ctor: assert_gt(borderSize, 0), sizes >= borderSize, h > 0 (CubicGrid.hpp:193-199)
+	if (d->border_size <= 0 || d->border_size > kMaxBs)
+		return fail(GCMX_ERR_INVALID_ARG, "border_size must be 1..8");
+	for (int i = 0; i < d->dim; i++) {
+		if (d->sizes[i] < d->border_size)
+			return fail(GCMX_ERR_INVALID_ARG, "sizes[i] must be >= border_size");
+		if (!(d->h[i] > 0)) return fail(GCMX_ERR_INVALID_ARG, "h[i] must be > 0");
+	}
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+		return fail(GCMX_ERR_HIP, "no HIP device available");
+	if (device < 0 || device >= ndev) return fail(GCMX_ERR_INVALID_ARG, "bad device index");
+	HIP_TRY(hipSetDevice(device));
+
+	auto* c = new gcmx_ctx();
+	c->device = device;
+	c->desc = *d;
+	c->D = d->dim;
+	c->M = pde_size(d->dim);
+	c->bs = d->border_size;
+	Geo& g = c->geo;
+	g.D = c->D;
+	g.M = c->M;
+	g.bs = c->bs;
+	const int D = c->D, bs = c->bs;
+	for (int i = 0; i < 3; i++) g.sizes[i] = (i < D) ? d->sizes[i] : 1;
+	// fastest axis: `lead` unused elements, bs ghosts, inner, bs ghosts, padding
+	const int last = D - 1;
+	g.lead = (int)round_up(bs, kRowAlign) - bs;
+	g.row = round_up(g.lead + bs + d->sizes[last] + bs, kRowAlign);
+	long long n_all_d[3] = {1, 1, 1};
+	for (int i = 0; i < D; i++) n_all_d[i] = d->sizes[i] + 2LL * bs;
+	for (int i = 0; i < 3; i++) g.stride[i] = 0;
+	g.stride[last] = 1;
+	long long st = g.row;
+	for (int i = last - 1; i >= 0; i--) {
+		g.stride[i] = st;
+		st *= n_all_d[i];
+	}
+	long long total = g.row;
+	for (int i = 0; i < last; i++) total *= n_all_d[i];
+	g.cs = round_up(total, 64);
+	g.origin = (long long)(g.lead + bs);  // fastest-axis offset of inner index 0
+	for (int i = 0; i < last; i++) g.origin += (long long)bs * g.stride[i];
+	g.n_inner = (long long)g.sizes[0] * g.sizes[1] * g.sizes[2];
+	c->n_all = 1;
+	for (int i = 0; i < D; i++) {
+		c->all_shape[i] = n_all_d[i];
+		c->n_all *= n_all_d[i];
+	}
+	c->layer_elems = (size_t)c->M * (size_t)g.cs;
+
+	const size_t bytes = c->layer_elems * sizeof(double);
+	if (hipMalloc(&c->cur, bytes) != hipSuccess || hipMalloc(&c->nxt, bytes) != hipSuccess ||
+	    hipMalloc(&c->tabs_d, sizeof(AxisTable) * 255 * 3) != hipSuccess) {
+		gcmx_destroy(c);
+		return fail(GCMX_ERR_OOM, "device allocation failed");
+	}
+	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
+	    hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming) != hipSuccess) {
+		gcmx_destroy(c);
+		return fail(GCMX_ERR_HIP, "stream/event creation failed");
+	}
+	if (hipMemsetAsync(c->cur, 0, bytes, c->stream) != hipSuccess ||
+	    hipMemsetAsync(c->nxt, 0, bytes, c->stream) != hipSuccess ||
+	    hipStreamSynchronize(c->stream) != hipSuccess) {
+		gcmx_destroy(c);
+		return fail(GCMX_ERR_HIP, "zero fill failed");
+	}
+	*out = c;
+	return GCMX_OK;
+}
+
+void gcmx_destroy(gcmx_ctx* c) {
+	if (!c) return;
+	hipSetDevice(c->device);
+	if (c->stream) hipStreamSynchronize(c->stream);
+	if (c->comm_stream) hipStreamSynchronize(c->comm_stream);
+	drain_timings(c);
+	if (c->comm) ncclCommDestroy(c->comm);
+	hipFree(c->cur);
+	hipFree(c->nxt);
+	hipFree(c->tabs_d);
+	hipFree(c->mat_d);
+	hipFree(c->nodes_d);
+	hipFree(c->qs_d);
+	hipFree(c->vals_d);
+	if (c->ev_ready) hipEventDestroy(c->ev_ready);
+	if (c->ev_halo) hipEventDestroy(c->ev_halo);
+	if (c->stream) hipStreamDestroy(c->stream);
+	if (c->comm_stream) hipStreamDestroy(c->comm_stream);
+	delete c;
+}
+
+gcmx_status gcmx_set_materials(gcmx_ctx* c, int n_mat, const double* U, const double* U1,
+                               const double* L) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (n_mat < 1 || n_mat > 255 || !U || !U1 || !L)
+		return fail(GCMX_ERR_INVALID_ARG, "n_mat must be 1..255 with non-null tables");
+	const int D = c->D, M = c->M;
+	const size_t nm = (size_t)n_mat * D * M * M, nl = (size_t)n_mat * D * M;
+	for (size_t i = 0; i < nm; i++)
+		if (!std::isfinite(U[i]) || !std::isfinite(U1[i]))
+			return fail(GCMX_ERR_INVALID_ARG, "non-finite matrix entry");
+	for (size_t i = 0; i < nl; i++)
+		if (!std::isfinite(L[i])) return fail(GCMX_ERR_INVALID_ARG, "non-finite eigenvalue");
+	c->n_mat = n_mat;
+	c->U.assign(U, U + nm);
+	c->U1.assign(U1, U1 + nm);
+	c->L.assign(L, L + nl);
+	c->tabs_tau = NAN;
+	refresh_fast(c);
+	compute_halo_comps(c);
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_set_material_ids(gcmx_ctx* c, const uint8_t* ids) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!ids) {
+		hipFree(c->mat_d);
+		c->mat_d = nullptr;
+	} else {
+		const Geo& g = c->geo;
+		std::vector<uint8_t> inner((size_t)g.n_inner);
+		long long i = 0;
+		for (int x = 0; x < g.sizes[0]; x++)
+			for (int y = 0; y < g.sizes[1]; y++)
+				for (int z = 0; z < g.sizes[2]; z++, i++) {
+					const int it[3] = {x, y, z};
+					long long ref = 0, mul = 1;
+					for (int d = c->D - 1; d >= 0; d--) {
+						ref += (it[d] + c->bs) * mul;
+						mul *= c->all_shape[d];
+					}
+					const uint8_t m = ids[ref];
+					if (c->n_mat > 0 && m >= c->n_mat)
+						return fail(GCMX_ERR_INVALID_ARG, "material id out of range");
+					inner[(size_t)i] = m;
+				}
+		if (!c->mat_d) HIP_TRY(hipMalloc(&c->mat_d, inner.size()));
+		HIP_TRY(hipMemcpy(c->mat_d, inner.data(), inner.size(), hipMemcpyHostToDevice));
+	}
+	refresh_fast(c);
+	return GCMX_OK;
+}
+
+// Host AoS (reference order, all nodes) <-> device SoA layer.
+static void aos_to_soa(const gcmx_ctx* c, const double* aos, double* soa) {
+	const Geo& g = c->geo;
+	const int D = c->D, M = c->M;
+	const long long n0 = c->all_shape[0], n1 = c->all_shape[1], n2 = c->all_shape[2];
+	const long long first = g.origin - c->bs * (g.stride[0] + (D > 1 ? g.stride[1] : 0) +
+	                                            (D > 2 ? g.stride[2] : 0));
+	auto work = [&](long long a0, long long a1) {
+		for (long long i0 = a0; i0 < a1; i0++)
+			for (long long i1 = 0; i1 < n1; i1++)
+				for (long long i2 = 0; i2 < n2; i2++) {
+					const long long ref = (i0 * n1 + i1) * n2 + i2;
+					const long long dev = first + i0 * g.stride[0] + (D > 1 ? i1 * g.stride[1] : 0) +
+					                      (D > 2 ? i2 * g.stride[2] : 0);
+					for (int m = 0; m < M; m++) soa[m * g.cs + dev] = aos[ref * M + m];
+				}
+	};
+	const int nt = (int)std::min<long long>(16, std::max<long long>(1, n0 / 8));
+	std::vector<std::thread> th;
+	for (int t = 0; t < nt; t++) th.emplace_back(work, n0 * t / nt, n0 * (t + 1) / nt);
+	for (auto& t : th) t.join();
+}
+
+static void soa_to_aos(const gcmx_ctx* c, const double* soa, double* aos) {
+	const Geo& g = c->geo;
+	const int D = c->D, M = c->M;
+	const long long n0 = c->all_shape[0], n1 = c->all_shape[1], n2 = c->all_shape[2];
+	const long long first = g.origin - c->bs * (g.stride[0] + (D > 1 ? g.stride[1] : 0) +
+	                                            (D > 2 ? g.stride[2] : 0));
+	auto work = [&](long long a0, long long a1) {
+		for (long long i0 = a0; i0 < a1; i0++)
+			for (long long i1 = 0; i1 < n1; i1++)
+				for (long long i2 = 0; i2 < n2; i2++) {
+					const long long ref = (i0 * n1 + i1) * n2 + i2;
+					const long long dev = first + i0 * g.stride[0] + (D > 1 ? i1 * g.stride[1] : 0) +
+					                      (D > 2 ? i2 * g.stride[2] : 0);
+					for (int m = 0; m < M; m++) aos[ref * M + m] = soa[m * g.cs + dev];
+				}
+	};
+	const int nt = (int)std::min<long long>(16, std::max<long long>(1, n0 / 8));
+	std::vector<std::thread> th;
+	for (int t = 0; t < nt; t++) th.emplace_back(work, n0 * t / nt, n0 * (t + 1) / nt);
+	for (auto& t : th) t.join();
+}
+
+gcmx_status gcmx_upload(gcmx_ctx* c, const double* aos) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!aos) return fail(GCMX_ERR_INVALID_ARG, "null host array");
+	std::vector<double> soa(c->layer_elems, 0.0);
+	aos_to_soa(c, aos, soa.data());
+	// Ghost values that are not zero make the two time layers differ in their
+	// ghosts, which the fused step (it leaves the state in the other layer)
+	// must not assume away: fall back to the per-stage path.
+	{
+		const Geo& g = c->geo;
+		const long long n0 = c->all_shape[0], n1 = c->all_shape[1], n2 = c->all_shape[2];
+		bool nz = false;
+		for (long long i0 = 0; i0 < n0 && !nz; i0++)
+			for (long long i1 = 0; i1 < n1 && !nz; i1++)
+				for (long long i2 = 0; i2 < n2 && !nz; i2++) {
+					const bool ghost = (i0 < c->bs || i0 >= n0 - c->bs) ||
+					                   (c->D > 1 && (i1 < c->bs || i1 >= n1 - c->bs)) ||
+					                   (c->D > 2 && (i2 < c->bs || i2 >= n2 - c->bs));
+					if (!ghost) continue;
+					const long long ref = (i0 * n1 + i1) * n2 + i2;
+					for (int m = 0; m < c->M; m++) nz |= aos[ref * c->M + m] != 0.0;
+				}
+		(void)g;
+		if (nz) c->ghosts_touched = true;
+	}
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(hipMemcpy(c->cur, soa.data(), c->layer_elems * sizeof(double), hipMemcpyHostToDevice));
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_download(gcmx_ctx* c, double* aos) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!aos) return fail(GCMX_ERR_INVALID_ARG, "null host array");
+	std::vector<double> soa(c->layer_elems);
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(hipMemcpy(soa.data(), c->cur, c->layer_elems * sizeof(double), hipMemcpyDeviceToHost));
+	soa_to_aos(c, soa.data(), aos);
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_fill_random(gcmx_ctx* c, const int gs[3], uint64_t seed) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!gs) return fail(GCMX_ERR_INVALID_ARG, "null sizes");
+	const int D = c->D;
+	int st[3] = {0, 0, 0};
+	for (int i = 0; i < D; i++) {
+		st[i] = c->desc.start[i];
+		if (st[i] < 0 || st[i] + c->desc.sizes[i] > gs[i])
+			return fail(GCMX_ERR_INVALID_ARG, "local box outside the global box");
+	}
+	launch_fill_random(c->cur, c->geo, st, D > 1 ? gs[1] : 1, D > 2 ? gs[2] : 1, seed, c->stream);
+	HIP_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_stage(gcmx_ctx* c, int axis, double tau) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (axis < 0 || axis >= c->D) return fail(GCMX_ERR_INVALID_ARG, "axis out of range");
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	return stage_impl(c, axis, tau);
+}
+
+gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	s = build_tables(c, tau);
+	if (s) return s;
+	if (effective_path(c) != GCMX_PATH_FUSED) {
+		for (int a = 0; a < c->D; a++) {
+			s = stage_impl(c, a, tau);
+			if (s) return s;
+		}
+		return GCMX_OK;
+	}
+	if (c->comm) {
+		s = halo_exchange_impl(c);
+		if (s) return s;
+	}
+	const Geo& g = c->geo;
+	const double bytes = node_stage_bytes(c) * (double)g.n_inner;
+	bool ok;
+	{
+		Timed t(c, "march_x", bytes, c->stream);
+		ok = launch_march(c->cur, c->nxt, g, 0, c->tabs_d + 0, 0, g.sizes[0], c->stream);
+	}
+	if (ok) {
+		Timed t(c, "fused_yz", bytes, c->stream);
+		ok = launch_fused_yz(c->nxt, c->cur, g, c->tabs_d + 1, c->tabs_d + 2, 0, g.sizes[0],
+		                     c->stream);
+	}
+	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
+	HIP_TRY(hipGetLastError());
+	// X: cur -> nxt; fused Y/Z: nxt -> cur.  The state stays in `cur`.
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_set_kernel_path(gcmx_ctx* c, gcmx_path p) {
+	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");
+	if (p < GCMX_PATH_AUTO || p > GCMX_PATH_FUSED) return fail(GCMX_ERR_INVALID_ARG, "bad path");
+	c->path = p;
+	return GCMX_OK;
+}
+
+gcmx_path gcmx_effective_path(gcmx_ctx* c) { return c ? effective_path(c) : GCMX_PATH_GENERIC; }
+
+gcmx_status gcmx_border_fill(gcmx_ctx* c, int axis, int side, int n_nodes, const int* nodes,
+                             int n_q, const int* qs, const double* vals) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (axis < 0 || axis >= c->D || (side != 1 && side != -1) || n_nodes < 0 || n_q < 0 ||
+	    n_q > 32 || (n_nodes > 0 && !nodes) || (n_q > 0 && (!qs || !vals)))
+		return fail(GCMX_ERR_INVALID_ARG, "bad border-fill arguments");
+	const int D = c->D;
+	for (int i = 0; i < n_nodes; i++) {
+		for (int d = 0; d < D; d++) {
+			const int v = nodes[i * D + d];
+			if (v < 0 || v >= c->geo.sizes[d]) return fail(GCMX_ERR_INVALID_ARG, "face node out of range");
+		}
+		const int want = side > 0 ? c->geo.sizes[axis] - 1 : 0;
+		if (nodes[i * D + axis] != want) return fail(GCMX_ERR_INVALID_ARG, "node not on the face");
+	}
+	for (int k = 0; k < n_q; k++) {
+		const int q = qs[k];
+		const bool ok = (q == 12) || (q >= 2 && q <= 4 && q - 2 < D) ||
+		                (q >= 5 && q <= 10 && (D == 3 || (D == 2 && (q == 5 || q == 6 || q == 8)) ||
+		                                      (D == 1 && q == 5)));
+		if (!ok) return fail(GCMX_ERR_INVALID_ARG, "quantity not in this PDE vector");
+	}
+	c->ghosts_touched = true;
+	if (n_nodes == 0) return GCMX_OK;
+	const size_t need = (size_t)n_nodes * D;
+	HIP_TRY(hipStreamSynchronize(c->stream));  // scratch reuse
+	if (need > c->nodes_cap) {
+		hipFree(c->nodes_d);
+		HIP_TRY(hipMalloc(&c->nodes_d, need * sizeof(int)));
+		c->nodes_cap = need;
+	}
+	if (!c->qs_d) {
+		HIP_TRY(hipMalloc(&c->qs_d, 32 * sizeof(int)));
+		HIP_TRY(hipMalloc(&c->vals_d, 32 * sizeof(double)));
+	}
+	HIP_TRY(hipMemcpy(c->nodes_d, nodes, need * sizeof(int), hipMemcpyHostToDevice));
+	if (n_q) {
+		HIP_TRY(hipMemcpy(c->qs_d, qs, n_q * sizeof(int), hipMemcpyHostToDevice));
+		HIP_TRY(hipMemcpy(c->vals_d, vals, n_q * sizeof(double), hipMemcpyHostToDevice));
+	}
+	launch_border_fill(c->cur, c->geo, axis, side > 0 ? -1 : 1, n_nodes, c->nodes_d, n_q, c->qs_d,
+	                   c->vals_d, c->stream);
+	HIP_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dmin[3], const int dmax[3], gcmx_ctx* src,
+                          const int smin[3]) {
+	gcmx_status s = check_ctx(dst);
+	if (s) return s;
+	if (!src || !dmin || !dmax || !smin || src->D != dst->D || src->M != dst->M ||
+	    src->device != dst->device)
+		return fail(GCMX_ERR_INVALID_ARG, "bad copy-box arguments");
+	const int D = dst->D;
+	int ext[3] = {1, 1, 1}, dm[3] = {0, 0, 0}, sm[3] = {0, 0, 0};
+	for (int d = 0; d < D; d++) {
+		ext[d] = dmax[d] - dmin[d];
+		dm[d] = dmin[d];
+		sm[d] = smin[d];
+		if (ext[d] <= 0) return fail(GCMX_ERR_INVALID_ARG, "empty box");
+		if (dmin[d] < -dst->bs || dmax[d] > dst->geo.sizes[d] + dst->bs || smin[d] < -src->bs ||
+		    smin[d] + ext[d] > src->geo.sizes[d] + src->bs)
+			return fail(GCMX_ERR_INVALID_ARG, "box outside the grid");
+	}
+	dst->ghosts_touched = true;
+	// order the copy after the source's pending work
+	HIP_TRY(hipEventRecord(src->ev_ready, src->stream));
+	HIP_TRY(hipStreamWaitEvent(dst->stream, src->ev_ready, 0));
+	launch_copy_box(dst->cur, dst->geo, src->cur, src->geo, dm, sm, ext, dst->stream);
+	HIP_TRY(hipGetLastError());
+	HIP_TRY(hipEventRecord(dst->ev_ready, dst->stream));
+	HIP_TRY(hipStreamWaitEvent(src->stream, dst->ev_ready, 0));
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]) {
+	static_assert(sizeof(ncclUniqueId) <= GCMX_UNIQUE_ID_BYTES, "unique id size");
+	if (!id) return fail(GCMX_ERR_INVALID_ARG, "null id");
+	ncclUniqueId u;
+	if (ncclGetUniqueId(&u) != ncclSuccess) return fail(GCMX_ERR_COMM, "ncclGetUniqueId failed");
+	std::memset(id, 0, GCMX_UNIQUE_ID_BYTES);
+	std::memcpy(id, &u, sizeof(u));
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], int nranks,
+                           int rank, int left, int right) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!id || nranks < 1 || rank < 0 || rank >= nranks || left >= nranks || right >= nranks ||
+	    left == rank || right == rank)
+		return fail(GCMX_ERR_INVALID_ARG, "bad communicator arguments");
+	if (c->comm) return fail(GCMX_ERR_STATE, "communicator already initialised");
+	ncclUniqueId u;
+	std::memcpy(&u, id, sizeof(u));
+	ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+	if (r != ncclSuccess) {
+		c->comm = nullptr;
+		return fail(GCMX_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+	}
+	c->nranks = nranks;
+	c->rank = rank;
+	c->left = left;
+	c->right = right;
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_halo_exchange(gcmx_ctx* c) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	return halo_exchange_impl(c);
+}
+
+gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n) {
+	if (!slabs || n < 1) return fail(GCMX_ERR_INVALID_ARG, "bad slab list");
+	for (int i = 0; i < n; i++) {
+		gcmx_ctx* c = slabs[i];
+		if (!c || c->D < 2 || c->n_mat <= 0) return fail(GCMX_ERR_INVALID_ARG, "bad slab");
+		if (i > 0) {
+			const gcmx_ctx* p = slabs[i - 1];
+			bool ok = p->D == c->D && p->bs == c->bs && p->desc.start[0] + p->geo.sizes[0] == c->desc.start[0];
+			for (int d = 1; d < c->D; d++) ok = ok && p->geo.sizes[d] == c->geo.sizes[d] && p->desc.start[d] == c->desc.start[d];
+			if (!ok) return fail(GCMX_ERR_INVALID_ARG, "slabs are not X-adjacent");
+		}
+	}
+	if (n == 1) return GCMX_OK;
+	gcmx_ctx* lead = slabs[0];
+	HIP_TRY(hipSetDevice(lead->device));
+	for (int i = 0; i < n; i++) {
+		HIP_TRY(hipSetDevice(slabs[i]->device));
+		HIP_TRY(hipEventRecord(slabs[i]->ev_ready, slabs[i]->stream));
+		HIP_TRY(hipSetDevice(lead->device));
+		HIP_TRY(hipStreamWaitEvent(lead->comm_stream, slabs[i]->ev_ready, 0));
+	}
+	for (int i = 0; i + 1 < n; i++) {
+		gcmx_ctx* a = slabs[i];
+		gcmx_ctx* b = slabs[i + 1];
+		const long long pa = a->geo.stride[0], pb = b->geo.stride[0];
+		if (pa != pb) return fail(GCMX_ERR_INVALID_ARG, "slab planes differ");
+		const size_t bytes = (size_t)(a->bs * pa) * sizeof(double);
+		const int Xa = a->geo.sizes[0];
+		for (int comp : a->halo_comps) {
+			double* a_plane = a->cur + (size_t)comp * a->geo.cs;
+			double* b_plane = b->cur + (size_t)comp * b->geo.cs;
+			// a's right ghosts [Xa, Xa+bs) <- b's inner [0, bs)
+			HIP_TRY(hipMemcpyPeerAsync(a_plane + (size_t)((Xa + a->bs) * pa), a->device,
+			                           b_plane + (size_t)(b->bs * pb), b->device, bytes,
+			                           lead->comm_stream));
+			// b's left ghosts [-bs, 0) <- a's inner [Xa-bs, Xa)
+			HIP_TRY(hipMemcpyPeerAsync(b_plane, b->device, a_plane + (size_t)(Xa * pa), a->device,
+			                           bytes, lead->comm_stream));
+		}
+	}
+	HIP_TRY(hipEventRecord(lead->ev_halo, lead->comm_stream));
+	for (int i = 0; i < n; i++) {
+		HIP_TRY(hipSetDevice(slabs[i]->device));
+		HIP_TRY(hipStreamWaitEvent(slabs[i]->stream, lead->ev_halo, 0));
+	}
+	HIP_TRY(hipSetDevice(lead->device));
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_sync(gcmx_ctx* c) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	HIP_TRY(hipStreamSynchronize(c->comm_stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	drain_timings(c);
+	return GCMX_OK;
+}
+
+void* gcmx_stream(gcmx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+gcmx_status gcmx_profile_enable(gcmx_ctx* c, int enable) {
+	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");
+	c->prof = enable != 0;
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_profile_reset(gcmx_ctx* c) {
+	gcmx_status s = gcmx_sync(c);
+	if (s) return s;
+	c->buckets.clear();
+	return GCMX_OK;
+}
+
+int gcmx_profile_read(gcmx_ctx* c, int index, const char** name, double* total_ms,
+                      long long* launches, double* bytes) {
+	if (!c) return 0;
+	drain_timings(c);
+	const int n = (int)c->buckets.size();
+	if (index >= 0 && index < n) {
+		if (name) *name = c->buckets[index].name.c_str();
+		if (total_ms) *total_ms = c->buckets[index].total_ms;
+		if (launches) *launches = c->buckets[index].launches;
+		if (bytes) *bytes = c->buckets[index].bytes;
+	}
+	return n;
+}
+
+long long gcmx_inner_nodes(gcmx_ctx* c) { return c ? c->geo.n_inner : 0; }
+long long gcmx_all_nodes(gcmx_ctx* c) { return c ? c->n_all : 0; }
+size_t gcmx_device_bytes(gcmx_ctx* c) { return c ? 2 * c->layer_elems * sizeof(double) : 0; }
+
+}  // extern "C"

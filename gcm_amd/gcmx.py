@@ -1,0 +1,280 @@
+"""ctypes binding of the gcmx C-ABI (``include/gcmx.h``).
+
+This is the Python side of the drop-in boundary: a thin, typed wrapper around
+``gcm_amd/lib/libgcmx.so``.  There is no fallback: if the HIP library is
+missing or no GPU is present, construction fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgcmx.so")
+
+# include/gcmx.h
+GCMX_OK = 0
+STATUS_NAMES = {0: "GCMX_OK", 1: "GCMX_ERR_INVALID_ARG", 2: "GCMX_ERR_CFL", 3: "GCMX_ERR_HIP",
+                4: "GCMX_ERR_OOM", 5: "GCMX_ERR_STATE", 6: "GCMX_ERR_UNSUPPORTED",
+                7: "GCMX_ERR_COMM"}
+PATH_AUTO, PATH_GENERIC, PATH_SPLIT, PATH_FUSED = 0, 1, 2, 3
+PATH_NAMES = {0: "auto", 1: "generic", 2: "split", 3: "fused"}
+UNIQUE_ID_BYTES = 128
+
+# Exported symbols, in header order (checked by tests/test_abi.py).
+SYMBOLS = [
+    "gcmx_abi_version", "gcmx_last_error", "gcmx_pde_size", "gcmx_status_string",
+    "gcmx_create", "gcmx_destroy", "gcmx_set_materials", "gcmx_set_material_ids",
+    "gcmx_upload", "gcmx_download", "gcmx_fill_random", "gcmx_stage", "gcmx_step",
+    "gcmx_set_kernel_path", "gcmx_effective_path", "gcmx_border_fill", "gcmx_copy_box",
+    "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
+    "gcmx_sync", "gcmx_stream",
+    "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_inner_nodes",
+    "gcmx_all_nodes", "gcmx_device_bytes",
+]
+
+
+class GcmxError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class GridDesc(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int), ("border_size", ctypes.c_int),
+                ("sizes", ctypes.c_int * 3), ("start", ctypes.c_int * 3),
+                ("h", ctypes.c_double * 3)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libgcmx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() "
+                          "(make -C gcm_amd/csrc)")
+    L = ctypes.CDLL(LIB_PATH)
+    dp = ctypes.POINTER(ctypes.c_double)
+    ip = ctypes.POINTER(ctypes.c_int)
+    vp = ctypes.c_void_p
+    st = ctypes.c_int
+    L.gcmx_abi_version.restype = ctypes.c_int
+    L.gcmx_last_error.restype = ctypes.c_char_p
+    L.gcmx_pde_size.argtypes = [ctypes.c_int]
+    L.gcmx_status_string.argtypes = [st]
+    L.gcmx_status_string.restype = ctypes.c_char_p
+    L.gcmx_create.argtypes = [ctypes.POINTER(GridDesc), ctypes.c_int, ctypes.POINTER(vp)]
+    L.gcmx_create.restype = st
+    L.gcmx_destroy.argtypes = [vp]
+    L.gcmx_destroy.restype = None
+    L.gcmx_set_materials.argtypes = [vp, ctypes.c_int, dp, dp, dp]
+    L.gcmx_set_material_ids.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8)]
+    L.gcmx_upload.argtypes = [vp, dp]
+    L.gcmx_download.argtypes = [vp, dp]
+    L.gcmx_fill_random.argtypes = [vp, ip, ctypes.c_uint64]
+    L.gcmx_stage.argtypes = [vp, ctypes.c_int, ctypes.c_double]
+    L.gcmx_step.argtypes = [vp, ctypes.c_double]
+    L.gcmx_set_kernel_path.argtypes = [vp, ctypes.c_int]
+    L.gcmx_effective_path.argtypes = [vp]
+    L.gcmx_border_fill.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int,
+                                   ip, dp]
+    L.gcmx_copy_box.argtypes = [vp, ip, ip, vp, ip]
+    L.gcmx_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
+    L.gcmx_comm_init.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int]
+    L.gcmx_halo_exchange.argtypes = [vp]
+    L.gcmx_halo_exchange_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.gcmx_sync.argtypes = [vp]
+    L.gcmx_stream.argtypes = [vp]
+    L.gcmx_stream.restype = vp
+    L.gcmx_profile_enable.argtypes = [vp, ctypes.c_int]
+    L.gcmx_profile_reset.argtypes = [vp]
+    L.gcmx_profile_read.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), dp,
+                                    ctypes.POINTER(ctypes.c_longlong), dp]
+    L.gcmx_profile_read.restype = ctypes.c_int
+    L.gcmx_inner_nodes.argtypes = [vp]
+    L.gcmx_inner_nodes.restype = ctypes.c_longlong
+    L.gcmx_all_nodes.argtypes = [vp]
+    L.gcmx_all_nodes.restype = ctypes.c_longlong
+    L.gcmx_device_bytes.argtypes = [vp]
+    L.gcmx_device_bytes.restype = ctypes.c_size_t
+    _lib = L
+    return L
+
+
+def _check(status: int):
+    if status != GCMX_OK:
+        raise GcmxError(status, lib().gcmx_last_error().decode())
+
+
+def _dp(a: np.ndarray):
+    if a.dtype != np.float64 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError("expected a C-contiguous float64 array")
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _ip(seq) -> ctypes.Array:
+    seq = list(seq)
+    return (ctypes.c_int * max(1, len(seq)))(*seq)
+
+
+def pde_size(dim: int) -> int:
+    return dim + dim * (dim + 1) // 2
+
+
+class Context:
+    """One body (or one X-slab of a body) resident on one GPU."""
+
+    def __init__(self, dim: int, border_size: int, sizes: Sequence[int],
+                 start: Optional[Sequence[int]] = None, h: Optional[Sequence[float]] = None,
+                 device: int = 0):
+        start = list(start) if start is not None else [0] * dim
+        h = list(h) if h is not None else [1.0] * dim
+        self.dim, self.bs, self.M = dim, border_size, pde_size(dim)
+        self.sizes = list(sizes)[:dim]
+        self.start = start[:dim]
+        self.h = h[:dim]
+        d = GridDesc(dim, border_size, (ctypes.c_int * 3)(*(self.sizes + [1] * (3 - dim))),
+                     (ctypes.c_int * 3)(*(self.start + [0] * (3 - dim))),
+                     (ctypes.c_double * 3)(*(list(self.h) + [0.0] * (3 - dim))))
+        self._ptr = ctypes.c_void_p()
+        _check(lib().gcmx_create(ctypes.byref(d), device, ctypes.byref(self._ptr)))
+        self.shape_all = tuple(s + 2 * border_size for s in self.sizes)
+        self.n_all = int(np.prod(self.shape_all))
+
+    def close(self):
+        if getattr(self, "_ptr", None) and self._ptr.value:
+            lib().gcmx_destroy(self._ptr)
+            self._ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ptr(self):
+        return self._ptr
+
+    # -- set-up -----------------------------------------------------------
+    def set_materials(self, U: np.ndarray, U1: np.ndarray, L: np.ndarray):
+        """U/U1: [n_mat, dim, M, M], L: [n_mat, dim, M] (GcmMatrices per material)."""
+        U = np.ascontiguousarray(U, dtype=np.float64)
+        U1 = np.ascontiguousarray(U1, dtype=np.float64)
+        L = np.ascontiguousarray(L, dtype=np.float64)
+        n = U.shape[0]
+        assert U.shape == (n, self.dim, self.M, self.M) and U1.shape == U.shape
+        assert L.shape == (n, self.dim, self.M)
+        _check(lib().gcmx_set_materials(self._ptr, n, _dp(U), _dp(U1), _dp(L)))
+
+    def set_material_ids(self, ids_all: Optional[np.ndarray]):
+        if ids_all is None:
+            _check(lib().gcmx_set_material_ids(self._ptr, None))
+            return
+        ids = np.ascontiguousarray(ids_all, dtype=np.uint8).reshape(-1)
+        assert ids.size == self.n_all
+        _check(lib().gcmx_set_material_ids(self._ptr, ids.ctypes.data_as(
+            ctypes.POINTER(ctypes.c_uint8))))
+
+    def upload(self, aos: np.ndarray):
+        a = np.ascontiguousarray(aos, dtype=np.float64).reshape(-1)
+        assert a.size == self.n_all * self.M
+        _check(lib().gcmx_upload(self._ptr, _dp(a)))
+
+    def download(self) -> np.ndarray:
+        out = np.empty((self.n_all, self.M))
+        _check(lib().gcmx_download(self._ptr, _dp(out)))
+        return out
+
+    def fill_random(self, global_sizes: Sequence[int], seed: int):
+        gs = list(global_sizes) + [1] * (3 - len(global_sizes))
+        _check(lib().gcmx_fill_random(self._ptr, _ip(gs), seed))
+
+    # -- hot path ---------------------------------------------------------
+    def stage(self, axis: int, tau: float):
+        _check(lib().gcmx_stage(self._ptr, axis, tau))
+
+    def step(self, tau: float):
+        _check(lib().gcmx_step(self._ptr, tau))
+
+    def set_path(self, path: int):
+        _check(lib().gcmx_set_kernel_path(self._ptr, path))
+
+    @property
+    def effective_path(self) -> str:
+        return PATH_NAMES[lib().gcmx_effective_path(self._ptr)]
+
+    def border_fill(self, axis: int, side: int, nodes: np.ndarray, quantities: Sequence[int],
+                    values: Sequence[float]):
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32).reshape(-1, self.dim)
+        q = _ip(quantities)
+        v = (ctypes.c_double * max(1, len(values)))(*values)
+        _check(lib().gcmx_border_fill(self._ptr, axis, side, nodes.shape[0],
+                                      nodes.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                      len(quantities), q, v))
+
+    def copy_box(self, dst_min, dst_max, src: "Context", src_min):
+        pad = lambda s: list(s) + [0] * (3 - len(s))
+        _check(lib().gcmx_copy_box(self._ptr, _ip(pad(dst_min)), _ip(pad(dst_max)), src._ptr,
+                                   _ip(pad(src_min))))
+
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int, left: int, right: int):
+        buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)(*unique_id)
+        _check(lib().gcmx_comm_init(self._ptr, buf, nranks, rank, left, right))
+
+    def halo_exchange(self):
+        _check(lib().gcmx_halo_exchange(self._ptr))
+
+    def sync(self):
+        _check(lib().gcmx_sync(self._ptr))
+
+    @property
+    def stream(self) -> int:
+        return lib().gcmx_stream(self._ptr) or 0
+
+    # -- timing -----------------------------------------------------------
+    def profile(self, enable: bool = True):
+        _check(lib().gcmx_profile_enable(self._ptr, 1 if enable else 0))
+
+    def profile_reset(self):
+        _check(lib().gcmx_profile_reset(self._ptr))
+
+    def profile_read(self) -> dict:
+        n = lib().gcmx_profile_read(self._ptr, -1, None, None, None, None)
+        out = {}
+        for i in range(n):
+            name = ctypes.c_char_p(); tot = ctypes.c_double(); cnt = ctypes.c_longlong()
+            byt = ctypes.c_double()
+            lib().gcmx_profile_read(self._ptr, i, ctypes.byref(name), ctypes.byref(tot),
+                                    ctypes.byref(cnt), ctypes.byref(byt))
+            out[name.value.decode()] = {"total_ms": tot.value, "launches": cnt.value,
+                                        "bytes_per_launch": byt.value}
+        return out
+
+    @property
+    def inner_nodes(self) -> int:
+        return lib().gcmx_inner_nodes(self._ptr)
+
+    @property
+    def device_bytes(self) -> int:
+        return lib().gcmx_device_bytes(self._ptr)
+
+
+def halo_exchange_group(slabs: Sequence["Context"]):
+    """Refresh X ghosts of in-process X slabs (ordered by increasing X)."""
+    arr = (ctypes.c_void_p * len(slabs))(*[c.ptr.value for c in slabs])
+    _check(lib().gcmx_halo_exchange_group(arr, len(slabs)))
+
+
+def unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)()
+    _check(lib().gcmx_comm_unique_id(buf))
+    return bytes(buf)

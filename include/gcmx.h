@@ -1,0 +1,181 @@
+/*
+ * gcmx.h -- C-ABI of the MI355X grid-characteristic stage path.
+ *
+ * This is the drop-in boundary for libgcm's cubic stage loop.  Each entry point
+ * names the reference interface it replaces (paths relative to
+ * /root/reference/src/libgcm).  Plain C: no exceptions cross the ABI, every call
+ * returns a gcmx_status and gcmx_last_error() holds the message of the last
+ * failure on the calling thread (the reference throws gcm::Exception from
+ * assert_* / THROW_* instead: util/infrastructure/Assertion.hpp).
+ *
+ * Ownership: a gcmx_ctx owns every device buffer of one body (one CubicGrid
+ * mesh, or one X-slab of it on one GPU).  Threading: one host thread drives one
+ * context at a time; all work of a context is issued on its own HIP stream.
+ *
+ * Host-side arrays passed through this ABI use the reference's DefaultMesh
+ * storage order: M doubles per node, over ALL nodes including borderSize ghost
+ * layers, indexed by CubicGrid::getIndex (grid/cubic/CubicGrid.hpp:141-147;
+ * X slowest, last axis fastest).  On the device the context keeps its own
+ * ghost-padded SoA layout.
+ */
+#ifndef GCMX_H
+#define GCMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCMX_ABI_VERSION 1
+
+typedef enum gcmx_status {
+	GCMX_OK = 0,
+	GCMX_ERR_INVALID_ARG = 1, /* reference: assert_* on arguments                     */
+	GCMX_ERR_CFL = 2,         /* reference: assert_le(k, src.size()-1) in minMaxInterpolate
+	                             (interpolation/EqualDistanceLineInterpolator.hpp:22-23) */
+	GCMX_ERR_HIP = 3,         /* a HIP runtime call failed                            */
+	GCMX_ERR_OOM = 4,         /* device allocation failed                             */
+	GCMX_ERR_STATE = 5,       /* call order violated (e.g. stage before materials)    */
+	GCMX_ERR_UNSUPPORTED = 6, /* configuration outside what this build implements     */
+	GCMX_ERR_COMM = 7         /* RCCL error in the halo exchange                      */
+} gcmx_status;
+
+typedef struct gcmx_ctx gcmx_ctx;
+
+/* CubicGrid<D>::ConstructionPack (grid/cubic/CubicGrid.hpp:96-101). */
+typedef struct gcmx_grid_desc {
+	int dim;          /* 1, 2 or 3 (Task::globalSettings.dimensionality)            */
+	int border_size;  /* ghost layers, 1..8 (Task::CubicGrid::borderSize)          */
+	int sizes[3];     /* inner nodes per axis; entries >= dim are ignored          */
+	int start[3];     /* global index of the first inner node (CubicGrid::start)   */
+	double h[3];      /* spatial steps (CubicGrid::h)                              */
+} gcmx_grid_desc;
+
+/* Which kernels gcmx_step may use (gcmx_set_kernel_path). */
+typedef enum gcmx_path {
+	GCMX_PATH_AUTO = 0,    /* fastest path the configuration admits                */
+	GCMX_PATH_GENERIC = 1, /* one thread per node, any D / borderSize / materials  */
+	GCMX_PATH_SPLIT = 2,   /* per-axis tuned kernels (march / LDS line), 3-D only  */
+	GCMX_PATH_FUSED = 3    /* X march + fused Y/Z pass, 3-D only                   */
+} gcmx_path;
+
+/* ---- library ------------------------------------------------------------ */
+int         gcmx_abi_version(void);
+const char* gcmx_last_error(void);
+int         gcmx_pde_size(int dim); /* VelocitySigmaVariables<D>: D + D(D+1)/2 */
+const char* gcmx_status_string(gcmx_status s);
+
+/* ---- lifetime --------------------------------------------------------------
+ * Replaces: AbstractFactory::createMesh + DefaultMesh ctor/allocate
+ * (engine/cubic/AbstractFactory.hpp:74-79, engine/cubic/DefaultMesh.hpp:159-167)
+ * and CubicGrid ctor assertions (grid/cubic/CubicGrid.hpp:184-199).
+ * Allocates two zero-filled time layers on `device`. */
+gcmx_status gcmx_create(const gcmx_grid_desc* desc, int device, gcmx_ctx** out);
+void        gcmx_destroy(gcmx_ctx* ctx);
+
+/* ---- set-up ----------------------------------------------------------------
+ * Replaces the per-node GcmMatrices shared_ptr table DefaultMesh::gcmMatrices
+ * (DefaultMesh.hpp:144) filled by MaterialsCondition::apply
+ * (util/task/MaterialsCondition.hpp:23-36).  U/U1: [n_mat][dim][M*M] row-major,
+ * L: [n_mat][dim][M] (GcmMatrices<M,D>::GcmMatrix {U, U1, L},
+ * util/math/GridCharacteristicMethod.hpp:40-52).  n_mat in 1..255. */
+gcmx_status gcmx_set_materials(gcmx_ctx* ctx, int n_mat, const double* U,
+                               const double* U1, const double* L);
+/* One byte per node of the all-nodes array (getIndex order); NULL means every
+ * node uses material 0.  Ghost entries are ignored. */
+gcmx_status gcmx_set_material_ids(gcmx_ctx* ctx, const uint8_t* ids_all_nodes);
+
+/* Whole current time layer, host <-> device (DefaultMesh::pdeVariables). */
+gcmx_status gcmx_upload(gcmx_ctx* ctx, const double* aos_all_nodes);
+gcmx_status gcmx_download(gcmx_ctx* ctx, double* aos_all_nodes);
+/* "parity-random" field: every inner component uniform in
+ * [-1,1) from SplitMix64(seed), indexed in global (x,y,z,c) order of a global
+ * box of `global_sizes` nodes; ghosts untouched.  Generated on the device. */
+gcmx_status gcmx_fill_random(gcmx_ctx* ctx, const int global_sizes[3], uint64_t seed);
+
+/* ---- the hot path ------------------------------------------------------------
+ * gcmx_stage replaces GridCharacteristicMethodBase::stage(s, timeStep, mesh)
+ * (engine/cubic/GridCharacteristicMethod.hpp:13-17, impl :42-52) followed by
+ * AbstractMesh::swapCurrAndNextPdeTimeLayer(0) (engine/cubic/DefaultMesh.hpp:134-137),
+ * i.e. one iteration of the stage loop body in cubic::Engine::nextTimeStep
+ * (engine/cubic/Engine.cpp:108-112).  Validates Courant (floor(q) < borderSize
+ * for every material/eigenvalue) where the reference would assert.
+ * Asynchronous on the context stream. */
+gcmx_status gcmx_stage(gcmx_ctx* ctx, int axis, double tau);
+/* All `dim` stages of one time step with no border or contact work between
+ * them (cubic::Engine::nextTimeStep, Engine.cpp:90-121, for a body without
+ * border conditions, contacts or ODEs).  May run fused kernels; results are
+ * identical to dim consecutive gcmx_stage calls. */
+gcmx_status gcmx_step(gcmx_ctx* ctx, double tau);
+gcmx_status gcmx_set_kernel_path(gcmx_ctx* ctx, gcmx_path path);
+/* Which path gcmx_step would take now (after materials are set). */
+gcmx_path   gcmx_effective_path(gcmx_ctx* ctx);
+
+/* ---- sibling plugin points ----------------------------------------------------
+ * Replaces cubic::BorderConditions::handleBorderPoint
+ * (engine/cubic/BorderConditions.hpp:94-114) for one condition on one face:
+ * for each listed face node and a = 1..borderSize,
+ *   ghost(-a) = inner(+a); then for each quantity q in order,
+ *   q(ghost) = -q(inner) + 2 * value_q.
+ * `face_nodes`: n_nodes inner multi-indices (dim ints each) on the face
+ * sizes[axis]-1 (side = +1, innerSign -1) or 0 (side = -1, innerSign +1).
+ * `quantities`: codes of PhysicalQuantities::T (util/Enum.hpp:27-50):
+ *   2..4 = Vx..Vz, 5..10 = Sxx,Sxy,Sxz,Syy,Syz,Szz, 12 = PRESSURE.
+ * `values`: the time dependency already evaluated at Clock::Time(). */
+gcmx_status gcmx_border_fill(gcmx_ctx* ctx, int axis, int side, int n_nodes,
+                             const int* face_nodes, int n_quantities,
+                             const int* quantities, const double* values);
+/* Replaces ContactCopier::apply (engine/cubic/ContactConditions.hpp:56-68):
+ * copy a box of `dst`'s current layer from a same-sized box of `src`'s current
+ * layer (boxes as local multi-indices [min, max), may include ghosts).  Both
+ * contexts must live on the same device. */
+gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dst_min[3], const int dst_max[3],
+                          gcmx_ctx* src, const int src_min[3]);
+
+/* ---- multi-GPU X-slab halo (replaces the dead MPI slab design,
+ * src/test/TestMPI.cpp:33-50, 92-155, and the in-process ContactCopier for
+ * bodies split along X) ---------------------------------------------------------*/
+#define GCMX_UNIQUE_ID_BYTES 128
+gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]);
+/* left/right: ranks owning the slabs at lower/higher X, or -1 at a physical
+ * boundary.  Collective over `nranks` processes (one context per process). */
+gcmx_status gcmx_comm_init(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES],
+                           int nranks, int rank, int left, int right);
+/* Fill the X ghost layers of the current layer from the neighbours' boundary
+ * inner planes (only the components the X stage reads), on the comm stream.
+ * gcmx_step/gcmx_stage(axis 0) on a comm-enabled context call it themselves. */
+gcmx_status gcmx_halo_exchange(gcmx_ctx* ctx);
+
+/* In-process X slabs (one or several devices, one host thread): refresh the X
+ * ghost layers of every slab's current layer from its neighbours in `slabs`
+ * (ordered by increasing X; slabs[i] and slabs[i+1] must be adjacent).  Orders
+ * itself after all pending work of every slab and before any later work of
+ * any slab.  Call it before each time step, like the RCCL exchange. */
+gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n);
+
+/* ---- synchronisation and timing ------------------------------------------- */
+gcmx_status gcmx_sync(gcmx_ctx* ctx);
+/* The context's compute stream as a hipStream_t (for event timing by callers). */
+void*       gcmx_stream(gcmx_ctx* ctx);
+/* Per-kernel event timing on the stream each kernel is launched on: when
+ * enabled, every launch is bracketed by hipEvents and its duration added to
+ * the kernel's bucket once the events complete (read after gcmx_sync). */
+gcmx_status gcmx_profile_enable(gcmx_ctx* ctx, int enable);
+gcmx_status gcmx_profile_reset(gcmx_ctx* ctx);
+/* Returns the number of kernel buckets; fills name/total_ms/launches of
+ * bucket `index` when index < count. */
+int         gcmx_profile_read(gcmx_ctx* ctx, int index, const char** name,
+                              double* total_ms, long long* launches,
+                              double* bytes_per_launch);
+
+/* Device-side layout facts (for DESIGN.md-style reporting and tests). */
+long long   gcmx_inner_nodes(gcmx_ctx* ctx);
+long long   gcmx_all_nodes(gcmx_ctx* ctx);
+size_t      gcmx_device_bytes(gcmx_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GCMX_H */

@@ -1,0 +1,70 @@
+"""Shared test helpers: build matching oracle bodies and gcmx contexts."""
+import numpy as np
+
+from oracle import oracle as O
+
+
+def oracle_body(D, bs, sizes, start=None, h=None, materials=((4.0, 2.0, 1.0),), courant=0.9):
+    """An oracle Body with zero state (no initial conditions)."""
+    start = list(start) if start is not None else [0] * D
+    h = list(h) if h is not None else [1.0] * D
+    mats = [O.Material(*m) for m in materials]
+    inh = [(("infinite",), m) for m in mats[1:]]
+    t = O.Task(D=D, border_size=bs, h=h, cubics={0: (list(sizes), start)}, courant=courant,
+               default_material=mats[0], inhomogeneities=inh, number_of_snaps=1)
+    return O.Engine(t).bodies[0]
+
+
+def random_state(body, seed, ghosts=True):
+    rng = np.random.default_rng(seed)
+    if ghosts:
+        body.pde[:] = rng.uniform(-1, 1, body.pde.shape)
+    else:
+        body.pde[:] = 0.0
+        body.inner_view()[...] = rng.uniform(-1, 1, body.inner_view().shape)
+
+
+def random_materials(body, seed):
+    """Random per-node material ids over the inner nodes (ghosts keep 0)."""
+    rng = np.random.default_rng(seed)
+    its = body.inner_indices()
+    body.mat_id[body.flat_index(its)] = rng.integers(0, len(body.tables), len(its)).astype(np.uint8)
+
+
+def tables(body):
+    U = np.stack([t[0] for t in body.tables]); U1 = np.stack([t[1] for t in body.tables])
+    L = np.stack([t[2] for t in body.tables])
+    return U, U1, L
+
+
+def context_for(body, path=None, device=0):
+    import gcm_amd
+    ctx = gcm_amd.Context(body.D, body.bs, body.sizes[:body.D], start=body.start[:body.D],
+                          h=body.h[:body.D], device=device)
+    U, U1, L = tables(body)
+    ctx.set_materials(U, U1, L)
+    if len(body.tables) > 1:
+        ctx.set_material_ids(body.mat_id)
+    ctx.upload(body.pde)
+    if path is not None:
+        ctx.set_path(path)
+    return ctx
+
+
+def assert_same(ctx, body, what=""):
+    got = ctx.download()
+    want = body.pde
+    if not np.array_equal(got, want):
+        diff = got != want
+        idx = np.argwhere(diff)
+        n = int(diff.sum())
+        i0 = tuple(idx[0])
+        raise AssertionError(f"{what}: {n} values differ; first at {i0}: "
+                             f"got {got[i0]!r} want {want[i0]!r}")
+
+
+def seq_sum(a):
+    s = 0.0
+    for x in np.asarray(a).reshape(-1).tolist():
+        s += x
+    return s

@@ -1,0 +1,255 @@
+"""GPU parity: libgcmx.so (through its C-ABI) against the oracle, bitwise.
+
+Bit-exact is the bar (integer-exact arithmetic order, no FMA contraction): the
+comparison is IEEE equality, which identifies +0 and -0 (the skipped exact-zero
+matrix terms can only change the sign of an exact zero).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import (assert_same, context_for, oracle_body, random_materials, random_state,
+                           seq_sum)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def G():
+    import gcm_amd
+    gcm_amd.lib()
+    return gcm_amd
+
+
+CASES = [
+    (1, 1, [37]), (1, 2, [300]), (1, 3, [65]),
+    (2, 1, [9, 13]), (2, 2, [21, 70]), (2, 3, [17, 5]), (2, 5, [20, 40]),
+    (3, 1, [7, 9, 11]), (3, 2, [12, 10, 70]), (3, 3, [6, 8, 19]),
+]
+
+
+@pytest.mark.parametrize("D,bs,sizes", CASES)
+def test_generic_stages_random_with_ghosts(G, D, bs, sizes):
+    """Every stage of two time steps, random state including ghost layers."""
+    b = oracle_body(D, bs, sizes, h=[1.0, 0.5, 2.0][:D])
+    random_state(b, seed=D * 10 + bs, ghosts=True)
+    ctx = context_for(b, path=G.PATH_GENERIC)
+    tau = 0.9 * 0.5 / 1.0  # Courant 0.9 on the smallest h
+    for step in range(2):
+        for s in range(D):
+            b.stage(s, tau)
+            ctx.stage(s, tau)
+            assert_same(ctx, b, f"D={D} bs={bs} step {step} stage {s}")
+
+
+@pytest.mark.parametrize("bs,sizes", [(1, [5, 6, 7]), (2, [13, 17, 70]), (2, [9, 4, 300]),
+                                      (3, [10, 11, 64]), (2, [140, 3, 5])])
+def test_split_stages_3d(G, bs, sizes):
+    b = oracle_body(3, bs, sizes)
+    random_state(b, seed=bs + sizes[2], ghosts=True)
+    ctx = context_for(b, path=G.PATH_SPLIT)
+    assert ctx.effective_path == "split"
+    for step in range(2):
+        for s in range(3):
+            b.stage(s, 0.9)
+            ctx.stage(s, 0.9)
+            assert_same(ctx, b, f"split bs={bs} sizes={sizes} step {step} stage {s}")
+
+
+@pytest.mark.parametrize("bs,sizes", [(2, [12, 10, 70]), (2, [9, 150, 300]), (1, [4, 3, 64]),
+                                      (3, [130, 7, 100]), (2, [5, 66, 520])])
+def test_fused_step_3d(G, bs, sizes):
+    """gcmx_step on the fused path (X march + fused Y/Z) == three oracle stages."""
+    b = oracle_body(3, bs, sizes)
+    random_state(b, seed=sum(sizes), ghosts=False)
+    ctx = context_for(b, path=G.PATH_AUTO)
+    assert ctx.effective_path == "fused"
+    for step in range(3):
+        for s in range(3):
+            b.stage(s, 0.9)
+        ctx.step(0.9)
+        assert_same(ctx, b, f"fused bs={bs} sizes={sizes} step {step}")
+
+
+def test_fused_disabled_by_nonzero_ghosts(G):
+    b = oracle_body(3, 2, [6, 6, 6])
+    random_state(b, seed=1, ghosts=True)
+    ctx = context_for(b)
+    assert ctx.effective_path == "split"
+    for s in range(3):
+        b.stage(s, 0.9)
+    ctx.step(0.9)
+    assert_same(ctx, b, "auto path with ghosts")
+
+
+@pytest.mark.parametrize("D,bs,sizes", [(2, 2, [23, 31]), (3, 2, [9, 10, 11]), (3, 3, [7, 6, 40])])
+def test_heterogeneous_materials(G, D, bs, sizes):
+    mats = ((4.0, 2.0, 1.0), (1.0, 2.0, 0.8), (2.5, 0.0, 3.0))
+    b = oracle_body(D, bs, sizes, materials=mats, courant=0.9)
+    random_materials(b, seed=5)
+    random_state(b, seed=6, ghosts=True)
+    ctx = context_for(b)
+    assert ctx.effective_path == "generic"
+    tau = 0.9 / np.sqrt((3.0 + 6.0) / 2.5)  # Courant 0.9 on the fastest material
+    for step in range(2):
+        for s in range(D):
+            b.stage(s, tau)
+            ctx.stage(s, tau)
+            assert_same(ctx, b, f"hetero D={D} step {step} stage {s}")
+
+
+@pytest.mark.parametrize("path", ["generic", "split", "fused"])
+def test_large_courant_multi_cell(G, path):
+    """Courant 2.5 with borderSize 3: feet two cells away (k = floor(q) = 2)."""
+    p = {"generic": G.PATH_GENERIC, "split": G.PATH_SPLIT, "fused": G.PATH_FUSED}[path]
+    b = oracle_body(3, 3, [8, 9, 70])
+    random_state(b, seed=11, ghosts=False)
+    ctx = context_for(b, path=p)
+    tau = 2.5
+    for step in range(2):
+        for s in range(3):
+            b.stage(s, tau)
+        if path == "fused":
+            ctx.step(tau)
+        else:
+            for s in range(3):
+                ctx.stage(s, tau)
+        assert_same(ctx, b, f"{path} courant 2.5 step {step}")
+
+
+def test_cfl_violation_is_an_error(G):
+    b = oracle_body(3, 2, [6, 6, 6])
+    ctx = context_for(b)
+    with pytest.raises(G.GcmxError) as e:
+        ctx.stage(0, 2.0)  # q = 2 = borderSize: the reference asserts / reads out of range
+    assert e.value.status == 2
+    with pytest.raises(ValueError):
+        b.stage(0, 2.0)
+
+
+def test_anchor_pressure_sphere_on_gpu(G):
+    """SURVEY.md §8c anchor reproduced on the GPU through gcmx_step (fused) and
+    gcmx_stage (generic): bitwise the reference's sums."""
+    N = 32
+    t = O.Task(D=3, border_size=2, h=[1, 1, 1], cubics={0: ([N] * 3, [0] * 3)}, courant=0.9,
+               default_material=O.Material(4, 2, 1), number_of_snaps=5,
+               ic_quantities=[(("sphere", N / 4, (N / 2,) * 3), "PRESSURE", 10.0)])
+    for path in (G.PATH_AUTO, G.PATH_GENERIC):
+        b = O.Engine(t).bodies[0]
+        ctx = context_for(b, path=path)
+        for _ in range(5):
+            ctx.step(0.9)
+        got = ctx.download()
+        s = seq_sum(b.inner_view(got))
+        assert s == -63401.220461788325, (path, s)
+
+
+def test_fill_random_matches_oracle(G):
+    b = oracle_body(3, 2, [5, 7, 9], start=[3, 0, 0])
+    b.pde[:] = 0
+    O.fill_random(b, [20, 7, 9], 0x5EED)
+    ctx = context_for(oracle_body(3, 2, [5, 7, 9], start=[3, 0, 0]))
+    ctx.fill_random([20, 7, 9], 0x5EED)
+    assert_same(ctx, b, "fill_random")
+
+
+def test_border_fill_matches_oracle(G):
+    """cubic BorderConditions (BorderConditions.hpp:81-114) on the device."""
+    D, bs = 2, 2
+    t = O.Task(D=D, border_size=bs, h=[1, 1], cubics={0: ([8, 7], [0, 0])}, courant=0.9,
+               default_material=O.Material(4, 2, 1), number_of_snaps=1,
+               border_conditions={0: [
+                   O.BorderCondition(0, ("box", (-1, 1.5, -1), (100, 4.5, 1)),
+                                     {"Sxx": lambda t: 0.5, "Sxy": lambda t: -0.25}),
+                   O.BorderCondition(1, ("infinite",), {"PRESSURE": lambda t: 0.125}),
+               ]})
+    b = O.Engine(t).bodies[0]
+    random_state(b, seed=3, ghosts=True)
+    ctx = context_for(b)
+    qcode = {"Vx": 2, "Vy": 3, "Vz": 4, "Sxx": 5, "Sxy": 6, "Sxz": 7, "Syy": 8, "Syz": 9,
+             "Szz": 10, "PRESSURE": 12}
+    for direction in (0, 1):
+        b.apply_border(direction, 0.0)
+        for d, left, right, vals in b.border:
+            if d != direction:
+                continue
+            qs = [qcode[q] for q, _ in vals]
+            vs = [f(0.0) for _, f in vals]
+            ctx.border_fill(d, -1, left, qs, vs)
+            ctx.border_fill(d, +1, right, qs, vs)
+        assert_same(ctx, b, f"border fill direction {direction}")
+
+
+def test_adhesion_contact_two_contexts_bitwise(G):
+    """Engine.AdhesionContact (TestEngine.cpp:27-87) on the device: two bodies
+    joined by contact copies == one body, bitwise, and == the oracle."""
+    from tests.test_oracle import adhesion_task
+    two = O.Engine(adhesion_task(True))
+    one = O.Engine(adhesion_task(False))
+    tau = two.time_step
+    nsteps = O.step_count(tau, two.required_time)
+    b0, b1 = two.bodies
+    c0, c1 = context_for(b0), context_for(b1)
+    call = context_for(one.bodies[0])
+    Y, bs = 41, 2
+    for _ in range(nsteps):
+        for s in range(2):
+            if s == 1:  # contact direction: body0's top ghosts <- body1 rows 0..1, and back
+                c0.copy_box([0, Y], [21, Y + bs], c1, [0, 0])
+                c1.copy_box([0, -bs], [21, 0], c0, [0, Y - bs])
+            c0.stage(s, tau); c1.stage(s, tau); call.stage(s, tau)
+    two.run(); one.run()
+    g0, g1, ga = c0.download(), c1.download(), call.download()
+    i0, i1, ia = b0.inner_view(g0), b1.inner_view(g1), one.bodies[0].inner_view(ga)
+    assert np.array_equal(ia[:, :Y], i0) and np.array_equal(ia[:, Y:], i1)
+    assert np.array_equal(ia, one.bodies[0].inner_view())
+
+
+def test_x_slabs_with_copy_halo_equal_single(G):
+    """Slab decomposition along X (the multi-GPU layout) on one device: two
+    slabs whose X ghosts are refreshed from the neighbour before every step
+    (gcmx_halo_exchange_group) == one context, bitwise, on the fused path."""
+    N, bs, seed = 40, 2, 0x5EED
+    import gcm_amd
+    from gcm_amd.host import isotropic_elastic_matrices
+    U, U1, L = isotropic_elastic_matrices(3, 4, 2, 1)
+    full = gcm_amd.Context(3, bs, [N, N, N])
+    full.set_materials(U[None], U1[None], L[None]); full.fill_random([N, N, N], seed)
+    halves = []
+    for r, (x0, X) in enumerate(((0, 17), (17, N - 17))):
+        c = gcm_amd.Context(3, bs, [X, N, N], start=[x0, 0, 0])
+        c.set_materials(U[None], U1[None], L[None]); c.fill_random([N, N, N], seed)
+        halves.append(c)
+    a, b = halves
+    from gcm_amd.gcmx import halo_exchange_group
+    for _ in range(3):
+        halo_exchange_group([a, b])
+        full.step(0.9); a.step(0.9); b.step(0.9)
+    assert a.effective_path == "fused" and b.effective_path == "fused"
+    fa, ga, gb = full.download(), a.download(), b.download()
+    sh = lambda c, arr: arr.reshape(tuple(s + 2 * bs for s in c.sizes) + (9,))[bs:-bs, bs:-bs, bs:-bs]
+    F = sh(full, fa)
+    assert np.array_equal(F[:17], sh(a, ga)) and np.array_equal(F[17:], sh(b, gb))
+
+
+@pytest.mark.slow
+def test_full_size_256_paths_agree_and_match_oracle(G):
+    """256^3 (BASELINE config 2): one step on the fused path == split == oracle."""
+    import gcm_amd
+    from gcm_amd.host import isotropic_elastic_matrices
+    N, seed = 256, 0x5EED
+    U, U1, L = isotropic_elastic_matrices(3, 4, 2, 1)
+    outs = {}
+    for path in (G.PATH_FUSED, G.PATH_SPLIT):
+        c = gcm_amd.Context(3, 2, [N, N, N])
+        c.set_materials(U[None], U1[None], L[None]); c.set_path(path)
+        c.fill_random([N, N, N], seed)
+        c.step(0.9)
+        outs[path] = c.download()
+        c.close()
+    assert np.array_equal(outs[G.PATH_FUSED], outs[G.PATH_SPLIT])
+    b = oracle_body(3, 2, [N, N, N])
+    O.fill_random(b, [N, N, N], seed)
+    for s in range(3):
+        b.stage(s, 0.9, 16)
+    assert np.array_equal(b.inner_view(outs[G.PATH_FUSED]), b.inner_view())
