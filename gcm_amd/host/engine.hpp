@@ -1,0 +1,277 @@
+// engine.hpp -- host mirror of libgcm's cubic engine surface over the gcmx C-ABI.
+//
+// Same class roles and call order as the reference:
+//   AbstractEngine (engine/AbstractEngine.{hpp,cpp})        -> gcm::AbstractEngine
+//   Clock (engine/GlobalVariables.hpp:16-41)                 -> gcm::Clock
+//   cubic::Engine<D> (engine/cubic/Engine.{hpp,cpp})         -> gcm::cubic::Engine<D>
+//   cubic::AbstractFactoryBase / AbstractFactory             -> cubic::AbstractFactoryBase / HipFactory
+//   cubic::AbstractMesh / DefaultMesh                        -> cubic::AbstractMesh / HipMesh
+//   cubic::GridCharacteristicMethodBase / ...Method<Mesh>    -> same base / HipGridCharacteristicMethod
+//   cubic::AbstractBorderConditions / BorderConditions       -> same base / HipBorderConditions
+//   cubic::AbstractContactCopier / ContactCopier             -> same base / HipContactCopier
+// The per-node work of stage(), border fills and contact copies runs on the GPU
+// through include/gcmx.h; the host keeps set-up and the time loop.
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "../../include/gcmx.h"
+#include "task.hpp"
+
+namespace gcm {
+
+/// engine/GlobalVariables.hpp:16-41 -- physical time and time step.
+struct Clock {
+	static real Time() { return time; }
+	static real TimeStep() { return timeStep; }
+
+private:
+	static real time;
+	static real timeStep;
+	static void setZero() { time = timeStep = 0; }
+	static void tickTack() { time += timeStep; }
+	friend class AbstractEngine;
+};
+
+/// Throw gcm::Exception for a failed gcmx call.
+void gcmxCheck(gcmx_status s, const char* what);
+
+/// engine/AbstractEngine.hpp:29-55
+class AbstractEngine {
+public:
+	explicit AbstractEngine(const Task& task);
+	virtual ~AbstractEngine() = default;
+	AbstractEngine(const AbstractEngine&) = delete;
+	AbstractEngine& operator=(const AbstractEngine&) = delete;
+	/// AbstractEngine::run (AbstractEngine.cpp:30-46)
+	void run();
+	int stepsDone() const { return steps; }
+	real getRequiredTime() const { return requiredTime; }
+
+protected:
+	const real CourantNumber = 0;
+	real requiredTime = 0;
+	int steps = 0;
+	void afterConstruction(const Task& task);
+	virtual void nextTimeStep() = 0;
+	virtual real estimateTimeStep() = 0;
+};
+
+/// grid/AbstractGrid.hpp -- what stage()/apply() receive and downcast.
+class AbstractGrid {
+public:
+	virtual ~AbstractGrid() = default;
+};
+
+namespace cubic {
+
+/// CubicGrid<D> (grid/cubic/CubicGrid.hpp) -- index arithmetic of the reference
+/// storage order (X slowest); `it` are local indices, ghosts at -bs..-1 / size..
+template <int D>
+struct CubicGrid : public AbstractGrid {
+	typedef std::array<int, D> IntD;
+	typedef std::array<real, D> RealD;
+	struct ConstructionPack {
+		int borderSize = 0;
+		IntD sizes{};
+		IntD start{};
+		RealD h{};
+	};
+	CubicGrid(size_t id_, const ConstructionPack& cp);
+	size_t id;
+	int borderSize;
+	IntD sizes, start;
+	RealD h;
+	long long indexMaker[D];
+	long long sizeOfAllNodes() const { return indexMaker[0] * (2LL * borderSize + sizes[0]); }
+	long long getIndex(const IntD& it) const {
+		long long a = 0;
+		for (int i = 0; i < D; i++) a += indexMaker[i] * (long long)(it[i] + borderSize);
+		return a;
+	}
+	/// coords (CubicGrid.hpp:114-126): startR + it * h, padded to 3-D
+	Real3 coords(const IntD& it) const {
+		Real3 c = {0, 0, 0};
+		for (int i = 0; i < D; i++) c[i] = (real)start[i] * h[i] + (real)it[i] * h[i];
+		return c;
+	}
+	real getMinimalSpatialStep() const;
+	/// AABB in global indices {start, start + sizes - 1}
+	std::pair<IntD, IntD> aabb() const;
+};
+
+/// engine/cubic/AbstractMesh.hpp:17-51
+template <int D>
+class AbstractMesh : public CubicGrid<D> {
+public:
+	using CubicGrid<D>::CubicGrid;
+	virtual ~AbstractMesh() = default;
+	virtual void setUpPde(const Task& task) = 0;
+	virtual real getMaximalEigenvalue() const = 0;
+	virtual void swapCurrAndNextPdeTimeLayer(int indexOfNextPde) = 0;
+};
+
+/// DefaultMesh's role with GPU-resident storage: the context owns both time
+/// layers on the device; the host holds only set-up data.
+template <int D>
+class HipMesh : public AbstractMesh<D> {
+public:
+	static constexpr int M = pdeSize(D);
+	typedef typename CubicGrid<D>::IntD IntD;
+	HipMesh(const Task& task, size_t id, const typename CubicGrid<D>::ConstructionPack& cp,
+	        int device);
+	~HipMesh() override;
+	/// DefaultMesh::setUpPde (DefaultMesh.hpp:60-66): allocate, MaterialsCondition,
+	/// InitialCondition, then upload.
+	void setUpPde(const Task& task) override;
+	real getMaximalEigenvalue() const override { return maximalEigenvalue; }
+	/// The device swap happens inside gcmx_stage; nothing to do here.
+	void swapCurrAndNextPdeTimeLayer(int) override {}
+	gcmx_ctx* ctx() const { return ctx_; }
+	/// Current layer in the reference AoS all-nodes order (downloads).
+	std::vector<real> pdeAll() const;
+	/// One node's PDE vector (downloads the layer; for tests and snapshots).
+	std::array<real, M> pde(const IntD& it) const;
+	int numberOfMaterials() const { return (int)matrices.size(); }
+
+private:
+	gcmx_ctx* ctx_ = nullptr;
+	int device;
+	real maximalEigenvalue = 0;
+	std::vector<GcmMatrices<D>> matrices;  // one per material condition
+	bool pdeIsSetUp = false;
+};
+
+/// engine/cubic/GridCharacteristicMethod.hpp:13-17
+class GridCharacteristicMethodBase {
+public:
+	virtual ~GridCharacteristicMethodBase() = default;
+	virtual void stage(const int s, const real& timeStep, AbstractGrid& mesh) const = 0;
+};
+
+/// GridCharacteristicMethod<Mesh>::stage on the device (gcmx_stage).
+template <int D>
+class HipGridCharacteristicMethod : public GridCharacteristicMethodBase {
+public:
+	explicit HipGridCharacteristicMethod(const Task&) {}
+	void stage(const int s, const real& timeStep, AbstractGrid& mesh) const override;
+	/// All D stages at once (gcmx_step; fused kernels where admissible).
+	void step(const real& timeStep, HipMesh<D>& mesh) const;
+};
+
+/// engine/cubic/BorderConditions.hpp:17-20
+class AbstractBorderConditions {
+public:
+	virtual ~AbstractBorderConditions() = default;
+	virtual void apply(AbstractGrid& mesh, const int direction) const = 0;
+	virtual bool empty() const = 0;
+};
+
+/// BorderConditions<Mesh> (BorderConditions.hpp:23-121): node lists found on the
+/// host at construction, ghost fills on the device per stage.
+template <int D>
+class HipBorderConditions : public AbstractBorderConditions {
+public:
+	HipBorderConditions(const Task& task, const HipMesh<D>& mesh);
+	void apply(AbstractGrid& mesh, const int direction) const override;
+	bool empty() const override { return conditions.empty(); }
+
+private:
+	struct Condition {
+		int direction;
+		std::vector<int> leftNodes, rightNodes;  // D ints per node
+		std::vector<std::pair<PhysicalQuantities::T, Task::TimeDependency>> values;
+	};
+	std::vector<Condition> conditions;
+};
+
+/// engine/cubic/ContactConditions.hpp:20-68 (adhesion: plain copy)
+template <int D>
+class HipContactCopier {
+public:
+	HipContactCopier(const std::array<int, 3>& dstMin, const std::array<int, 3>& dstMax,
+	                 const std::array<int, 3>& srcMin)
+	    : dmin(dstMin), dmax(dstMax), smin(srcMin) {}
+	void apply(HipMesh<D>& a, const HipMesh<D>& b) const;
+
+private:
+	std::array<int, 3> dmin, dmax, smin;
+};
+
+/// engine/cubic/AbstractFactory.hpp:22-54
+template <int D>
+class AbstractFactoryBase {
+public:
+	virtual ~AbstractFactoryBase() = default;
+	virtual std::shared_ptr<AbstractMesh<D>> createMesh(
+	    const Task& task, size_t gridId, const typename CubicGrid<D>::ConstructionPack& cp,
+	    size_t numberOfNextPdeTimeLayers) = 0;
+	virtual std::shared_ptr<GridCharacteristicMethodBase> createGcm(const Task& task) = 0;
+	virtual std::shared_ptr<AbstractBorderConditions> createBorder(
+	    const Task& task, std::shared_ptr<AbstractMesh<D>> mesh) = 0;
+};
+
+/// AbstractFactory<ElasticModel<D>, CubicGrid<D>, IsotropicMaterial, HipMesh>
+template <int D>
+class HipFactory : public AbstractFactoryBase<D> {
+public:
+	explicit HipFactory(int device_) : device(device_) {}
+	std::shared_ptr<AbstractMesh<D>> createMesh(const Task& task, size_t gridId,
+	                                            const typename CubicGrid<D>::ConstructionPack& cp,
+	                                            size_t) override {
+		return std::make_shared<HipMesh<D>>(task, gridId, cp, device);
+	}
+	std::shared_ptr<GridCharacteristicMethodBase> createGcm(const Task& task) override {
+		return std::make_shared<HipGridCharacteristicMethod<D>>(task);
+	}
+	std::shared_ptr<AbstractBorderConditions> createBorder(
+	    const Task& task, std::shared_ptr<AbstractMesh<D>> mesh) override {
+		return std::make_shared<HipBorderConditions<D>>(
+		    task, dynamic_cast<const HipMesh<D>&>(*mesh));
+	}
+
+private:
+	int device;
+};
+
+/// cubic::Engine<D> (engine/cubic/Engine.{hpp,cpp})
+template <int D>
+class Engine : public AbstractEngine {
+public:
+	typedef CubicGrid<D> Grid;
+	explicit Engine(const Task& task, int device = 0);
+	std::shared_ptr<const HipMesh<D>> getMesh(size_t gridId) const;
+	/// Run `n` more time steps regardless of the required time (benchmarks).
+	void runSteps(int n);
+
+protected:
+	void nextTimeStep() override;
+	real estimateTimeStep() override;
+
+private:
+	struct Body {
+		std::shared_ptr<AbstractFactoryBase<D>> factory;
+		std::shared_ptr<AbstractMesh<D>> mesh;
+		std::shared_ptr<GridCharacteristicMethodBase> gcm;
+		std::shared_ptr<AbstractBorderConditions> border;
+		struct Contact {
+			size_t neighborId;
+			int direction;
+			std::shared_ptr<HipContactCopier<D>> copier;
+		};
+		std::vector<Contact> contacts;
+	};
+	std::vector<Body> bodies;
+	int device;
+	Body& getBody(size_t id);
+	const Body& getBody(size_t id) const;
+	void createGridsAndContacts(const Task& task);
+};
+
+}  // namespace cubic
+
+/// engine/EngineFactory.hpp:11-38 (cubic only on this path)
+std::shared_ptr<AbstractEngine> createEngine(const Task& task, int device = 0);
+
+}  // namespace gcm
