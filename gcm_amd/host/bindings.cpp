@@ -1,0 +1,174 @@
+// bindings.cpp -- pybind11 module gcm_amd._gcm_host: the C++ host mirror
+// (Task / createEngine / cubic::Engine<D>) for Python tests and tools.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "engine.hpp"
+
+namespace py = pybind11;
+using namespace gcm;
+
+namespace {
+
+Real3 r3(const py::sequence& s) {
+	Real3 r = {0, 0, 0};
+	for (size_t i = 0; i < 3 && i < (size_t)py::len(s); i++) r[i] = s[i].cast<real>();
+	return r;
+}
+
+/// ("infinite",) | ("box", min3, max3) | ("sphere", r, c3) | ("cylinder", r, b3, e3)
+std::shared_ptr<Area> makeArea(const py::tuple& t) {
+	const std::string kind = t[0].cast<std::string>();
+	if (kind == "infinite") return std::make_shared<InfiniteArea>();
+	if (kind == "box") return std::make_shared<AxisAlignedBoxArea>(r3(t[1]), r3(t[2]));
+	if (kind == "sphere") return std::make_shared<SphereArea>(t[1].cast<real>(), r3(t[2]));
+	if (kind == "cylinder")
+		return std::make_shared<StraightBoundedCylinderArea>(t[1].cast<real>(), r3(t[2]), r3(t[3]));
+	throw Exception("unknown area kind " + kind);
+}
+
+PhysicalQuantities::T quantity(const std::string& q) {
+	static const std::map<std::string, PhysicalQuantities::T> m = {
+	    {"Vx", PhysicalQuantities::T::Vx},   {"Vy", PhysicalQuantities::T::Vy},
+	    {"Vz", PhysicalQuantities::T::Vz},   {"Sxx", PhysicalQuantities::T::Sxx},
+	    {"Sxy", PhysicalQuantities::T::Sxy}, {"Sxz", PhysicalQuantities::T::Sxz},
+	    {"Syy", PhysicalQuantities::T::Syy}, {"Syz", PhysicalQuantities::T::Syz},
+	    {"Szz", PhysicalQuantities::T::Szz}, {"PRESSURE", PhysicalQuantities::T::PRESSURE}};
+	auto it = m.find(q);
+	if (it == m.end()) throw Exception("unknown quantity " + q);
+	return it->second;
+}
+
+Waves::T wave(const std::string& w) {
+	static const std::map<std::string, Waves::T> m = {
+	    {"P_FORWARD", Waves::T::P_FORWARD},   {"P_BACKWARD", Waves::T::P_BACKWARD},
+	    {"S1_FORWARD", Waves::T::S1_FORWARD}, {"S1_BACKWARD", Waves::T::S1_BACKWARD},
+	    {"S2_FORWARD", Waves::T::S2_FORWARD}, {"S2_BACKWARD", Waves::T::S2_BACKWARD}};
+	auto it = m.find(w);
+	if (it == m.end()) throw Exception("unknown wave " + w);
+	return it->second;
+}
+
+/// Dimension-erased handle on cubic::Engine<D>.
+struct PyEngine {
+	std::shared_ptr<AbstractEngine> e;
+	int D;
+	template <int DD>
+	cubic::Engine<DD>& as() { return dynamic_cast<cubic::Engine<DD>&>(*e); }
+
+	py::array_t<real> pde(size_t id) {
+		std::vector<real> v;
+		std::vector<ssize_t> shape;
+		auto grab = [&](auto& eng) {
+			auto mesh = eng.getMesh(id);
+			v = mesh->pdeAll();
+			for (int i = 0; i < (int)mesh->sizes.size(); i++) shape.push_back(mesh->sizes[i] + 2 * mesh->borderSize);
+			shape.push_back((ssize_t)(v.size() / (size_t)mesh->sizeOfAllNodes()));
+		};
+		if (D == 1) grab(as<1>());
+		else if (D == 2) grab(as<2>());
+		else grab(as<3>());
+		py::array_t<real> out(shape);
+		std::copy(v.begin(), v.end(), out.mutable_data());
+		return out;
+	}
+	void runSteps(int n) { e->runSteps(n); }
+	std::string path(size_t id) {
+		gcmx_ctx* c = nullptr;
+		if (D == 1) c = as<1>().getMesh(id)->ctx();
+		else if (D == 2) c = as<2>().getMesh(id)->ctx();
+		else c = as<3>().getMesh(id)->ctx();
+		static const char* names[] = {"auto", "generic", "split", "fused"};
+		return names[gcmx_effective_path(c)];
+	}
+	real maximalEigenvalue(size_t id) {
+		if (D == 1) return as<1>().getMesh(id)->getMaximalEigenvalue();
+		if (D == 2) return as<2>().getMesh(id)->getMaximalEigenvalue();
+		return as<3>().getMesh(id)->getMaximalEigenvalue();
+	}
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_gcm_host, m) {
+	m.doc() = "C++ host mirror of libgcm's cubic Engine/Task surface over the gcmx C-ABI";
+	py::register_exception<Exception>(m, "GcmException");
+
+	py::class_<Task>(m, "Task")
+	    .def(py::init<>())
+	    .def_property("dimensionality", [](Task& t) { return t.globalSettings.dimensionality; },
+	                  [](Task& t, int d) { t.globalSettings.dimensionality = d; })
+	    .def_property("courant", [](Task& t) { return t.globalSettings.CourantNumber; },
+	                  [](Task& t, real c) { t.globalSettings.CourantNumber = c; })
+	    .def_property("number_of_snaps", [](Task& t) { return t.globalSettings.numberOfSnaps; },
+	                  [](Task& t, int n) { t.globalSettings.numberOfSnaps = n; })
+	    .def_property("steps_per_snap", [](Task& t) { return t.globalSettings.stepsPerSnap; },
+	                  [](Task& t, int n) { t.globalSettings.stepsPerSnap = n; })
+	    .def_property("required_time", [](Task& t) { return t.globalSettings.requiredTime; },
+	                  [](Task& t, real r) { t.globalSettings.requiredTime = r; })
+	    .def_property("border_size", [](Task& t) { return t.cubicGrid.borderSize; },
+	                  [](Task& t, int b) { t.cubicGrid.borderSize = b; })
+	    .def_property("h", [](Task& t) { return t.cubicGrid.h; },
+	                  [](Task& t, std::vector<real> h) { t.cubicGrid.h = h; })
+	    .def("add_body",
+	         [](Task& t, size_t id, std::vector<int> sizes, std::vector<int> start) {
+		         t.bodies[id] = Task::Body();
+		         t.cubicGrid.cubics[id] = {sizes, start};
+	         })
+	    .def("set_default_material",
+	         [](Task& t, real rho, real lam, real mu) {
+		         t.materialConditions.type = Task::MaterialCondition::Type::BY_AREAS;
+		         t.materialConditions.byAreas.defaultMaterial = std::make_shared<IsotropicMaterial>(rho, lam, mu);
+	         })
+	    .def("add_material",
+	         [](Task& t, py::tuple area, real rho, real lam, real mu) {
+		         t.materialConditions.byAreas.materials.push_back(
+		             {makeArea(area), std::make_shared<IsotropicMaterial>(rho, lam, mu)});
+	         })
+	    .def("set_body_material",
+	         [](Task& t, size_t id, real rho, real lam, real mu) {
+		         t.materialConditions.type = Task::MaterialCondition::Type::BY_BODIES;
+		         t.materialConditions.byBodies.bodyMaterialMap[id] = std::make_shared<IsotropicMaterial>(rho, lam, mu);
+	         })
+	    .def("add_initial_vector",
+	         [](Task& t, py::tuple area, std::vector<real> v) {
+		         t.initialCondition.vectors.push_back({makeArea(area), v});
+	         })
+	    .def("add_initial_wave",
+	         [](Task& t, py::tuple area, const std::string& w, int direction, const std::string& q, real value) {
+		         t.initialCondition.waves.push_back({makeArea(area), wave(w), direction, quantity(q), value});
+	         })
+	    .def("add_initial_quantity",
+	         [](Task& t, py::tuple area, const std::string& q, real value) {
+		         t.initialCondition.quantities.push_back({makeArea(area), quantity(q), value});
+	         })
+	    .def("add_border_condition",
+	         [](Task& t, size_t body, int direction, py::tuple area,
+	            std::map<std::string, std::function<real(real)>> values) {
+		         Task::CubicBorderCondition bc;
+		         bc.direction = direction;
+		         bc.area = makeArea(area);
+		         for (auto& kv : values) bc.values[quantity(kv.first)] = kv.second;
+		         t.cubicBorderConditions[body].push_back(bc);
+	         });
+
+	py::class_<PyEngine>(m, "Engine")
+	    .def(py::init([](const Task& t, int device) {
+		         PyEngine p;
+		         p.e = createEngine(t, device);
+		         p.D = t.globalSettings.dimensionality;
+		         return p;
+	         }),
+	         py::arg("task"), py::arg("device") = 0)
+	    .def("run", [](PyEngine& p) { p.e->run(); })
+	    .def("run_steps", &PyEngine::runSteps)
+	    .def("pde", &PyEngine::pde, "current layer of a body, all nodes incl. ghosts [..., M]")
+	    .def("path", &PyEngine::path)
+	    .def("maximal_eigenvalue", &PyEngine::maximalEigenvalue)
+	    .def_property_readonly("steps", [](PyEngine& p) { return p.e->stepsDone(); })
+	    .def_property_readonly("required_time", [](PyEngine& p) { return p.e->getRequiredTime(); })
+	    .def_property_readonly("time", [](PyEngine&) { return Clock::Time(); })
+	    .def_property_readonly("time_step", [](PyEngine&) { return Clock::TimeStep(); });
+}

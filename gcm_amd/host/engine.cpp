@@ -1,0 +1,486 @@
+// engine.cpp -- host mirror of the cubic engine (see engine.hpp for the map).
+#include "engine.hpp"
+
+#include <algorithm>
+#include <limits>
+#include <string>
+
+namespace gcm {
+
+real Clock::time = 0;
+real Clock::timeStep = 0;
+
+void gcmxCheck(gcmx_status s, const char* what) {
+	if (s != GCMX_OK)
+		throw Exception(std::string(what) + ": " + gcmx_status_string(s) + ": " + gcmx_last_error());
+}
+
+// ------------------------------------------------------------ AbstractEngine --
+
+AbstractEngine::AbstractEngine(const Task& task)
+    : CourantNumber(task.globalSettings.CourantNumber) {
+	Clock::setZero();
+}
+
+// AbstractEngine.cpp:18-27
+void AbstractEngine::afterConstruction(const Task& task) {
+	Clock::timeStep = estimateTimeStep();
+	requiredTime = Clock::TimeStep() * task.globalSettings.numberOfSnaps *
+	               task.globalSettings.stepsPerSnap;
+	if (task.globalSettings.numberOfSnaps <= 0) requiredTime = task.globalSettings.requiredTime;
+	if (!(requiredTime > 0)) throw Exception("requiredTime must be > 0");
+}
+
+// AbstractEngine.cpp:30-46 (snapshots are out of scope on this path)
+void AbstractEngine::run() {
+	while (Clock::Time() < requiredTime) {
+		Clock::timeStep = estimateTimeStep();
+		nextTimeStep();
+		steps++;
+		Clock::tickTack();
+	}
+}
+
+void AbstractEngine::runSteps(int n) {
+	for (int i = 0; i < n; i++) {
+		Clock::timeStep = estimateTimeStep();
+		nextTimeStep();
+		steps++;
+		Clock::tickTack();
+	}
+}
+
+namespace cubic {
+
+// ------------------------------------------------------------------ CubicGrid --
+
+template <int D>
+CubicGrid<D>::CubicGrid(size_t id_, const ConstructionPack& cp)
+    : id(id_), borderSize(cp.borderSize), sizes(cp.sizes), start(cp.start), h(cp.h) {
+	// CubicGrid.hpp:184-199 and calculateIndexMaker :202-225
+	if (!(borderSize > 0)) throw Exception("CubicGrid: borderSize must be > 0");
+	for (int i = 0; i < D; i++) {
+		if (!(sizes[i] >= borderSize)) throw Exception("CubicGrid: sizes must be >= borderSize");
+		if (!(h[i] > 0)) throw Exception("CubicGrid: h must be > 0");
+	}
+	const long long b2 = 2LL * borderSize;
+	if (D == 1) {
+		indexMaker[0] = 1;
+	} else if (D == 2) {
+		indexMaker[0] = b2 + sizes[D - 1];
+		indexMaker[D - 1] = 1;
+	} else {
+		indexMaker[0] = (b2 + sizes[1 % D]) * (b2 + sizes[D - 1]);
+		indexMaker[1 % D] = b2 + sizes[D - 1];
+		indexMaker[D - 1] = 1;
+	}
+}
+
+template <int D>
+real CubicGrid<D>::getMinimalSpatialStep() const {
+	real ans = std::numeric_limits<real>::max();
+	for (int i = 0; i < D; i++)
+		if (ans > h[i]) ans = h[i];
+	return ans;
+}
+
+template <int D>
+std::pair<typename CubicGrid<D>::IntD, typename CubicGrid<D>::IntD> CubicGrid<D>::aabb() const {
+	IntD mx;
+	for (int i = 0; i < D; i++) mx[i] = start[i] + sizes[i] - 1;
+	return {start, mx};
+}
+
+/// Calls f(it) for every inner node in SlowXFastZ order (linal/Multiindex.hpp:99-118),
+/// optionally restricted to it[axis] == fixed.
+template <int D, class F>
+static void forEachInner(const std::array<int, D>& sizes, F f, int axis = -1, int fixed = 0) {
+	std::array<int, D> it{};
+	std::array<int, D> lo{}, hi = sizes;
+	if (axis >= 0) {
+		lo[axis] = fixed;
+		hi[axis] = fixed + 1;
+	}
+	it = lo;
+	while (true) {
+		f(it);
+		int d = D - 1;
+		for (; d >= 0; d--) {
+			if (++it[d] < hi[d]) break;
+			it[d] = lo[d];
+		}
+		if (d < 0) break;
+	}
+}
+
+// -------------------------------------------------------------------- HipMesh --
+
+template <int D>
+HipMesh<D>::HipMesh(const Task&, size_t id_, const typename CubicGrid<D>::ConstructionPack& cp,
+                    int device_)
+    : AbstractMesh<D>(id_, cp), device(device_) {
+	gcmx_grid_desc desc{};
+	desc.dim = D;
+	desc.border_size = cp.borderSize;
+	for (int i = 0; i < 3; i++) {
+		desc.sizes[i] = i < D ? cp.sizes[i] : 1;
+		desc.start[i] = i < D ? cp.start[i] : 0;
+		desc.h[i] = i < D ? cp.h[i] : 0;
+	}
+	gcmxCheck(gcmx_create(&desc, device, &ctx_), "gcmx_create");
+}
+
+template <int D>
+HipMesh<D>::~HipMesh() {
+	gcmx_destroy(ctx_);
+}
+
+template <int D>
+void HipMesh<D>::setUpPde(const Task& task) {
+	if (pdeIsSetUp) throw Exception("setUpPde called twice");
+	pdeIsSetUp = true;
+	const long long nAll = this->sizeOfAllNodes();
+	std::vector<real> pde((size_t)nAll * M, 0.0);
+	std::vector<uint8_t> matId((size_t)nAll, 0);
+
+	// ---- MaterialsCondition::apply (util/task/MaterialsCondition.hpp:23-36, 70-91)
+	std::vector<std::pair<std::shared_ptr<Area>, std::shared_ptr<IsotropicMaterial>>> conds;
+	const auto& mc = task.materialConditions;
+	if (mc.type == Task::MaterialCondition::Type::BY_AREAS) {
+		conds.push_back({std::make_shared<InfiniteArea>(), mc.byAreas.defaultMaterial});
+		for (const auto& m : mc.byAreas.materials) conds.push_back({m.area, m.material});
+	} else {
+		conds.push_back({std::make_shared<InfiniteArea>(), mc.byBodies.bodyMaterialMap.at(this->id)});
+	}
+	if (conds.size() > 255) throw Exception("at most 255 material conditions per body");
+	matrices.assign(conds.size(), GcmMatrices<D>());
+	for (size_t c = 0; c < conds.size(); c++) {
+		if (!conds[c].second) throw Exception("material condition without a material");
+		ElasticModel<D>::constructGcmMatrices(matrices[c], *conds[c].second);
+	}
+	forEachInner<D>(this->sizes, [&](const IntD& it) {
+		const Real3 x = this->coords(it);
+		for (size_t c = 0; c < conds.size(); c++)
+			if (conds[c].first->contains(x)) matId[(size_t)this->getIndex(it)] = (uint8_t)c;
+	});
+	maximalEigenvalue = 0;
+	for (const auto& m : matrices) maximalEigenvalue = std::fmax(maximalEigenvalue, m.getMaximalEigenvalue());
+
+	// ---- InitialCondition::apply (util/task/InitialCondition.hpp:23-88)
+	std::vector<std::pair<std::shared_ptr<Area>, std::array<real, M>>> ics;
+	for (const auto& v : task.initialCondition.vectors) {
+		if ((int)v.list.size() != M) throw Exception("initial vector has the wrong size");
+		std::array<real, M> a{};
+		std::copy(v.list.begin(), v.list.end(), a.begin());
+		ics.push_back({v.area, a});
+	}
+	{
+		GcmMatrices<D> front;  // mcConditions.front().material
+		ElasticModel<D>::constructGcmMatrices(front, *conds.front().second);
+		for (const auto& w : task.initialCondition.waves) {
+			if (!(w.direction >= 0 && w.direction < D)) throw Exception("wave direction out of range");
+			const int col = waveColumn(D, w.waveType);
+			std::array<real, M> tmp{};
+			for (int r = 0; r < M; r++) tmp[r] = front.m[w.direction].U1[r * M + col];
+			const real current = getQuantity(D, w.quantity, tmp.data());
+			if (current == 0) throw Exception("wave calibration quantity is zero");
+			const real f = w.quantityValue / current;
+			for (int r = 0; r < M; r++) tmp[r] *= f;
+			ics.push_back({w.area, tmp});
+		}
+	}
+	for (const auto& q : task.initialCondition.quantities) {
+		std::array<real, M> tmp{};
+		setQuantity(D, q.physicalQuantity, q.value, tmp.data());
+		ics.push_back({q.area, tmp});
+	}
+	forEachInner<D>(this->sizes, [&](const IntD& it) {
+		const Real3 x = this->coords(it);
+		real* v = &pde[(size_t)this->getIndex(it) * M];
+		for (int c = 0; c < M; c++) v[c] = 0;
+		for (const auto& ic : ics)
+			if (ic.first->contains(x))
+				for (int c = 0; c < M; c++) v[c] += ic.second[c];
+	});
+
+	// ---- device tables: only the materials the nodes actually use
+	std::vector<int> used(matrices.size(), 0);
+	forEachInner<D>(this->sizes, [&](const IntD& it) { used[matId[(size_t)this->getIndex(it)]] = 1; });
+	std::vector<int> remap(matrices.size(), -1);
+	int nUsed = 0;
+	for (size_t c = 0; c < matrices.size(); c++)
+		if (used[c]) remap[c] = nUsed++;
+	std::vector<real> U((size_t)nUsed * D * M * M), U1(U.size()), L((size_t)nUsed * D * M);
+	for (size_t c = 0; c < matrices.size(); c++) {
+		if (remap[c] < 0) continue;
+		for (int s = 0; s < D; s++) {
+			const size_t o = ((size_t)remap[c] * D + s);
+			std::copy(matrices[c].m[s].U.begin(), matrices[c].m[s].U.end(), U.begin() + o * M * M);
+			std::copy(matrices[c].m[s].U1.begin(), matrices[c].m[s].U1.end(), U1.begin() + o * M * M);
+			std::copy(matrices[c].m[s].L.begin(), matrices[c].m[s].L.end(), L.begin() + o * M);
+		}
+	}
+	gcmxCheck(gcmx_set_materials(ctx_, nUsed, U.data(), U1.data(), L.data()), "gcmx_set_materials");
+	if (nUsed > 1) {
+		for (auto& m : matId) m = (uint8_t)std::max(0, remap[m]);
+		gcmxCheck(gcmx_set_material_ids(ctx_, matId.data()), "gcmx_set_material_ids");
+	}
+	gcmxCheck(gcmx_upload(ctx_, pde.data()), "gcmx_upload");
+}
+
+template <int D>
+std::vector<real> HipMesh<D>::pdeAll() const {
+	std::vector<real> out((size_t)this->sizeOfAllNodes() * M);
+	gcmxCheck(gcmx_download(ctx_, out.data()), "gcmx_download");
+	return out;
+}
+
+template <int D>
+std::array<real, HipMesh<D>::M> HipMesh<D>::pde(const IntD& it) const {
+	const std::vector<real> all = pdeAll();
+	std::array<real, M> v;
+	const size_t i = (size_t)this->getIndex(it);
+	for (int c = 0; c < M; c++) v[c] = all[i * M + c];
+	return v;
+}
+
+// ----------------------------------------------------------------- the stage --
+
+template <int D>
+void HipGridCharacteristicMethod<D>::stage(const int s, const real& timeStep,
+                                           AbstractGrid& mesh_) const {
+	HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(mesh_);  // std::bad_cast like the reference
+	gcmxCheck(gcmx_stage(mesh.ctx(), s, timeStep), "gcmx_stage");
+}
+
+template <int D>
+void HipGridCharacteristicMethod<D>::step(const real& timeStep, HipMesh<D>& mesh) const {
+	gcmxCheck(gcmx_step(mesh.ctx(), timeStep), "gcmx_step");
+}
+
+// ------------------------------------------------------------ border conditions --
+
+static int quantityCode(PhysicalQuantities::T q) { return static_cast<int>(q); }
+
+template <int D>
+HipBorderConditions<D>::HipBorderConditions(const Task& task, const HipMesh<D>& mesh) {
+	const auto found = task.cubicBorderConditions.find(mesh.id);
+	if (found == task.cubicBorderConditions.end()) return;
+	for (const auto& bc : found->second) {
+		Condition c;
+		c.direction = bc.direction;
+		if (!(bc.direction >= 0 && bc.direction < D)) throw Exception("border direction out of range");
+		for (const auto& q : bc.values) {
+			if (!hasQuantity(D, q.first)) throw Exception("border quantity not in the PDE vector");
+			c.values.push_back({q.first, q.second});  // std::map order == reference order
+		}
+		auto collect = [&](int index, std::vector<int>& out) {
+			forEachInner<D>(mesh.sizes, [&](const std::array<int, D>& it) {
+				if (bc.area->contains(mesh.coords(it)))
+					for (int d = 0; d < D; d++) out.push_back(it[d]);
+			}, bc.direction, index);
+		};
+		collect(0, c.leftNodes);
+		collect(mesh.sizes[bc.direction] - 1, c.rightNodes);
+		conditions.push_back(std::move(c));
+	}
+}
+
+template <int D>
+void HipBorderConditions<D>::apply(AbstractGrid& mesh_, const int direction) const {
+	HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(mesh_);
+	for (const auto& c : conditions) {
+		if (c.direction != direction) continue;
+		std::vector<int> qs;
+		std::vector<real> vals;
+		for (const auto& v : c.values) {
+			qs.push_back(quantityCode(v.first));
+			vals.push_back(v.second(Clock::Time()));
+		}
+		gcmxCheck(gcmx_border_fill(mesh.ctx(), direction, -1, (int)(c.leftNodes.size() / D),
+		                           c.leftNodes.data(), (int)qs.size(), qs.data(), vals.data()),
+		          "gcmx_border_fill");
+		gcmxCheck(gcmx_border_fill(mesh.ctx(), direction, +1, (int)(c.rightNodes.size() / D),
+		                           c.rightNodes.data(), (int)qs.size(), qs.data(), vals.data()),
+		          "gcmx_border_fill");
+	}
+}
+
+template <int D>
+void HipContactCopier<D>::apply(HipMesh<D>& a, const HipMesh<D>& b) const {
+	gcmxCheck(gcmx_copy_box(a.ctx(), dmin.data(), dmax.data(), b.ctx(), smin.data()), "gcmx_copy_box");
+}
+
+// --------------------------------------------------------------------- Engine --
+
+template <int D>
+Engine<D>::Engine(const Task& task, int device_) : AbstractEngine(task), device(device_) {
+	if (task.globalSettings.dimensionality != D) throw Exception("dimensionality mismatch");
+	createGridsAndContacts(task);
+	for (const auto& tb : task.bodies) {
+		Body& body = getBody(tb.first);
+		if (!tb.second.odes.empty()) throw Exception("ODE correctors are not on this path");
+		body.mesh->setUpPde(task);
+		body.gcm = body.factory->createGcm(task);
+		body.border = body.factory->createBorder(task, body.mesh);
+	}
+	afterConstruction(task);
+}
+
+template <int D>
+typename Engine<D>::Body& Engine<D>::getBody(size_t id) {
+	for (Body& b : bodies)
+		if (b.mesh->id == id) return b;
+	throw Exception("There isn't a body with given id");
+}
+
+template <int D>
+const typename Engine<D>::Body& Engine<D>::getBody(size_t id) const {
+	for (const Body& b : bodies)
+		if (b.mesh->id == id) return b;
+	throw Exception("There isn't a body with given id");
+}
+
+template <int D>
+std::shared_ptr<const HipMesh<D>> Engine<D>::getMesh(size_t gridId) const {
+	return std::dynamic_pointer_cast<const HipMesh<D>>(getBody(gridId).mesh);
+}
+
+// Engine.cpp:38-87 (factory choice: Engine.cpp:155-189)
+template <int D>
+void Engine<D>::createGridsAndContacts(const Task& task) {
+	if (task.bodies.empty()) throw Exception("the task has no bodies");
+	if (task.bodies.size() != task.cubicGrid.cubics.size())
+		throw Exception("every body needs a cube");
+	for (const auto& tb : task.bodies) {
+		if (tb.second.materialId != Materials::T::ISOTROPIC || tb.second.modelId != Models::T::ELASTIC)
+			throw Exception("only isotropic elastic bodies are on this path");
+		Body body;
+		body.factory = std::make_shared<HipFactory<D>>(device);
+		typename Grid::ConstructionPack cp;
+		cp.borderSize = task.cubicGrid.borderSize;
+		if ((int)task.cubicGrid.h.size() != D) throw Exception("h has the wrong size");
+		const auto& cube = task.cubicGrid.cubics.at(tb.first);
+		if ((int)cube.sizes.size() != D || (int)cube.start.size() != D)
+			throw Exception("cube sizes/start have the wrong size");
+		for (int i = 0; i < D; i++) {
+			cp.h[i] = task.cubicGrid.h[i];
+			cp.sizes[i] = cube.sizes[i];
+			cp.start[i] = cube.start[i];
+		}
+		body.mesh = body.factory->createMesh(task, tb.first, cp, 1);
+		bodies.push_back(body);
+	}
+	for (Body& body : bodies) {
+		for (const Body& other : bodies) {
+			if (other.mesh->id == body.mesh->id) continue;
+			auto a = body.mesh->aabb(), b = other.mesh->aabb();
+			std::array<int, D> mn, mx, w;
+			bool valid = true;
+			for (int i = 0; i < D; i++) {
+				mn[i] = std::max(a.first[i], b.first[i]);
+				mx[i] = std::min(a.second[i], b.second[i]);
+				w[i] = mx[i] - mn[i];
+				if (w[i] < 0) valid = false;
+			}
+			if (valid) throw Exception("Bodies must not intersect");
+			int axis = 0;
+			int minW = w[0];
+			for (int i = 1; i < D; i++)
+				if (w[i] < minW) {
+					axis = i;
+					minW = w[i];
+				}
+			if (minW != -1) continue;  // no contact
+			std::array<int, D> bmin = mn, bmax = mx;
+			if (body.mesh->start[axis] > other.mesh->start[axis]) bmin[axis] -= body.mesh->borderSize;
+			else bmax[axis] += body.mesh->borderSize;
+			std::array<int, 3> dmin{0, 0, 0}, dmax{1, 1, 1}, smin{0, 0, 0};
+			for (int i = 0; i < D; i++) {
+				dmin[i] = bmin[i] - body.mesh->start[i];
+				dmax[i] = bmax[i] - body.mesh->start[i] + 1;
+				smin[i] = bmin[i] - other.mesh->start[i];
+			}
+			typename Body::Contact contact;
+			contact.neighborId = other.mesh->id;
+			contact.direction = axis;
+			contact.copier = std::make_shared<HipContactCopier<D>>(dmin, dmax, smin);
+			body.contacts.push_back(contact);
+		}
+	}
+}
+
+// Engine.cpp:90-121
+template <int D>
+void Engine<D>::nextTimeStep() {
+	bool plain = true;
+	for (const Body& b : bodies) plain = plain && b.border->empty() && b.contacts.empty();
+	if (plain) {
+		// No border or contact work between the stages: one gcmx_step per body
+		// (identical results; lets the library use its fused kernels).
+		for (Body& b : bodies)
+			std::static_pointer_cast<HipGridCharacteristicMethod<D>>(b.gcm)->step(
+			    Clock::TimeStep(), dynamic_cast<HipMesh<D>&>(*b.mesh));
+		return;
+	}
+	for (int stage = 0; stage < D; stage++) {
+		for (Body& body : bodies) body.border->apply(*body.mesh, stage);
+		for (Body& body : bodies)
+			for (auto& contact : body.contacts)
+				if (contact.direction == stage)
+					contact.copier->apply(dynamic_cast<HipMesh<D>&>(*body.mesh),
+					                      dynamic_cast<const HipMesh<D>&>(*getBody(contact.neighborId).mesh));
+		for (Body& body : bodies) {
+			body.gcm->stage(stage, Clock::TimeStep(), *body.mesh);
+			body.mesh->swapCurrAndNextPdeTimeLayer(0);
+		}
+	}
+}
+
+// Engine.cpp:124-140
+template <int D>
+real Engine<D>::estimateTimeStep() {
+	real maxEigenvalue = 0;
+	const auto h = bodies.front().mesh->h;
+	for (const Body& b : bodies) {
+		if (!(h == b.mesh->h)) throw Exception("all bodies must share h");
+		const real e = b.mesh->getMaximalEigenvalue();
+		if (e > maxEigenvalue) maxEigenvalue = e;
+	}
+	return CourantNumber * bodies.front().mesh->getMinimalSpatialStep() / maxEigenvalue;
+}
+
+template class CubicGrid<1>;
+template class CubicGrid<2>;
+template class CubicGrid<3>;
+template class HipMesh<1>;
+template class HipMesh<2>;
+template class HipMesh<3>;
+template class HipGridCharacteristicMethod<1>;
+template class HipGridCharacteristicMethod<2>;
+template class HipGridCharacteristicMethod<3>;
+template class HipBorderConditions<1>;
+template class HipBorderConditions<2>;
+template class HipBorderConditions<3>;
+template class HipContactCopier<1>;
+template class HipContactCopier<2>;
+template class HipContactCopier<3>;
+template class Engine<1>;
+template class Engine<2>;
+template class Engine<3>;
+
+}  // namespace cubic
+
+// engine/EngineFactory.hpp:11-38
+std::shared_ptr<AbstractEngine> createEngine(const Task& task, int device) {
+	if (task.globalSettings.gridId != Grids::T::CUBIC)
+		throw Exception("only the cubic engine is on this path");
+	switch (task.globalSettings.dimensionality) {
+	case 1: return std::make_shared<cubic::Engine<1>>(task, device);
+	case 2: return std::make_shared<cubic::Engine<2>>(task, device);
+	case 3: return std::make_shared<cubic::Engine<3>>(task, device);
+	default: throw Exception("Invalid dimensionality");
+	}
+}
+
+}  // namespace gcm

@@ -46,6 +46,8 @@ public:
 	AbstractEngine& operator=(const AbstractEngine&) = delete;
 	/// AbstractEngine::run (AbstractEngine.cpp:30-46)
 	void run();
+	/// `n` more time steps of the same loop body, ignoring requiredTime (benchmarks).
+	void runSteps(int n);
 	int stepsDone() const { return steps; }
 	real getRequiredTime() const { return requiredTime; }
 
@@ -242,8 +244,6 @@ public:
 	typedef CubicGrid<D> Grid;
 	explicit Engine(const Task& task, int device = 0);
 	std::shared_ptr<const HipMesh<D>> getMesh(size_t gridId) const;
-	/// Run `n` more time steps regardless of the required time (benchmarks).
-	void runSteps(int n);
 
 protected:
 	void nextTimeStep() override;

@@ -1,0 +1,183 @@
+"""The C++ host mirror (Task -> createEngine -> cubic::Engine<D>::run) on the GPU,
+restating the reference's engine tests (src/test/sequence/TestEngine.cpp) and
+checking every run bitwise against the oracle engine on the same Task."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import seq_sum
+from tests.taskspec import host_task, oracle_task, spec
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    from gcm_amd import _gcm_host
+    return _gcm_host
+
+
+def inner(arr, bs, D):
+    sl = tuple(slice(bs, -bs) for _ in range(D))
+    return arr[sl]
+
+
+def run_both(H, s, steps=None):
+    oe = O.Engine(oracle_task(s))
+    he = H.Engine(host_task(s))
+    if steps is None:
+        oe.run(); he.run()
+        assert he.steps == oe.steps_done
+    else:
+        oe.run(max_steps=steps); he.run_steps(steps)
+    return oe, he
+
+
+def assert_bodies_equal(oe, he, s):
+    for b in oe.bodies:
+        got = he.pde(b.id)
+        want = b.pde.reshape(got.shape)
+        assert np.array_equal(got, want), f"body {b.id}: {int((got != want).sum())} values differ"
+
+
+def sphere_spec(N=32, snaps=5):
+    return spec(3, 2, [1, 1, 1], {0: ([N] * 3, [0] * 3)}, 0.9, (4, 2, 1), snaps=snaps,
+                quantities=[(("sphere", N / 4, (N / 2,) * 3), "PRESSURE", 10.0)])
+
+
+def test_engine_anchor_3d(H):
+    """SURVEY.md §8c anchor through Task -> Engine::run (fused path)."""
+    s = sphere_spec()
+    he = H.Engine(host_task(s))
+    assert he.path(0) == "fused"
+    he.run()
+    assert he.steps == 5
+    got = he.pde(0)
+    total = seq_sum(inner(got, 2, 3))
+    assert total == -63401.220461788325
+
+
+def test_engine_anchor_1d(H):
+    s = spec(1, 2, [1], {0: ([10000], [0])}, 0.9, (4, 2, 1), snaps=1000,
+             waves=[(("box", (1000, -1, -1), (2000, 1, 1)), "P_FORWARD", 0, "Vx", 1.0)])
+    he = H.Engine(host_task(s))
+    he.run_steps(1000)
+    v = inner(he.pde(0), 2, 1)
+    tot = 0.0
+    tot2 = 0.0
+    for x in v.reshape(-1).tolist():
+        tot += x
+        tot2 += x * x
+    assert tot == -2997.0000000000014 and tot2 == 16914.932549439342
+    he2 = H.Engine(host_task(s))
+    he2.run()
+    assert he2.steps == 1001  # Clock semantics (AbstractEngine.cpp:35-43)
+
+
+def adhesion(two):
+    X, Y = 21, 41
+    cubics = {0: ([X, Y], [0, 0]), 1: ([X, Y], [0, Y])} if two else {0: ([X, 2 * Y], [0, 0])}
+    return spec(2, 2, [1, 0.25], cubics, 0.9, (4, 2, 0.5), snaps=70,
+                waves=[(("box", (-1000, 2.5, -1000), (1000, 7.5, 1000)), "P_FORWARD", 1,
+                        "PRESSURE", 1.0)])
+
+
+def test_engine_adhesion_contact(H):
+    """Engine.AdhesionContact (TestEngine.cpp:27-87): bitwise split == unsplit, and == oracle."""
+    two = H.Engine(host_task(adhesion(True)))
+    two.run()
+    one = H.Engine(host_task(adhesion(False)))
+    one.run()
+    a0, a1, aa = inner(two.pde(0), 2, 2), inner(two.pde(1), 2, 2), inner(one.pde(0), 2, 2)
+    assert np.array_equal(aa[:, :41], a0) and np.array_equal(aa[:, 41:], a1)
+    oe = O.Engine(oracle_task(adhesion(True)))
+    oe.run()
+    assert_bodies_equal(oe, two, adhesion(True))
+
+
+def test_engine_run_statement(H):
+    """Engine.runStatement (TestEngine.cpp:91-136): bs 5, Courant 4.5, exact translation."""
+    s = spec(2, 5, [7.0 / 19, 3.0 / 39], {0: ([20, 40], [0, 0])}, 4.5, (4, 2, 0.5), snaps=9,
+             required_time=100.0,
+             waves=[(("box", (-1, 0.1125, -1), (8, 0.6375, 1)), "S1_FORWARD", 1, "Vx", 1.0)])
+    he = H.Engine(host_task(s))
+    expected = inner(he.pde(0), 5, 2)[10, 3].copy()
+    he.run()
+    actual = inner(he.pde(0), 5, 2)[10, 22]
+    for a, b in zip(expected, actual):
+        assert 4 * (a - b) ** 2 / ((a + b) ** 2 + 1e-9) < 1e-18
+    oe, he2 = run_both(H, s)
+    assert_bodies_equal(oe, he2, s)
+
+
+@pytest.mark.parametrize("kind", ["rho", "E"])
+def test_engine_two_layers(H, kind):
+    """Engine.TwoLayersDifferentRho/E (TestEngine.cpp:139-296) on the GPU (per-node
+    materials: generic kernel), reflection within 1e-2 and bitwise == oracle."""
+    rho0, lam0, mu0 = 1, 2, 0.8
+    for i in range(5):
+        if kind == "rho":
+            rho, lam, mu = 0.25 * 2 ** i * rho0, lam0, mu0
+        else:
+            rho, lam, mu = rho0, 0.25 * 2 ** i * lam0, 0.25 * 2 ** i * mu0
+        s = spec(2, 3, [2.0 / 49, 1.0 / 99], {0: ([50, 100], [0, 0])}, 1.5, (rho0, lam0, mu0),
+                 inhomogeneities=[(("box", (-10, 0.5 - 1e-5, -10), (10, 10, 10)), (rho, lam, mu))],
+                 snaps=0, required_time=0.24,
+                 waves=[(("box", (-1, 0.015, -1), (4, 0.455, 1)), "P_FORWARD", 1, "Vy", -2.0)])
+        he = H.Engine(host_task(s))
+        assert he.path(0) == "generic"
+        init = inner(he.pde(0), 3, 2)[25, 25].copy()
+        he.run()
+        refl = inner(he.pde(0), 3, 2)[25, 25]
+        E0 = mu0 * (3 * lam0 + 2 * mu0) / (lam0 + mu0); Z0 = math.sqrt(E0 * rho0)
+        E = mu * (3 * lam + 2 * mu) / (lam + mu); Z = math.sqrt(E * rho)
+        assert abs(refl[4] / init[4] - (Z - Z0) / (Z + Z0)) < 1e-2
+        assert abs(refl[1] / init[1] - (Z0 - Z) / (Z + Z0)) < 1e-2
+        oe = O.Engine(oracle_task(s))
+        oe.run()
+        assert_bodies_equal(oe, he, s)
+
+
+def test_engine_border_conditions_time_dependent(H):
+    """Cubic border conditions with time dependencies, overlapping conditions and
+    PRESSURE (BorderConditions.hpp:46-114), 2-D and 3-D: bitwise == oracle."""
+    f = lambda t: 0.5 * math.sin(3 * t)
+    s2 = spec(2, 2, [0.5, 0.25], {0: ([30, 25], [0, 0])}, 0.8, (4, 2, 1), snaps=12,
+              waves=[(("box", (3, -1, -1), (8, 100, 1)), "P_FORWARD", 0, "PRESSURE", 1.0)],
+              borders={0: [(0, ("infinite",), {"Sxx": f, "Sxy": lambda t: 0.0}),
+                           (1, ("box", (-1, -1, -1), (7.2, 100, 1)), {"PRESSURE": lambda t: 0.1 * t}),
+                           (1, ("box", (4.1, -1, -1), (100, 100, 1)), {"Vy": lambda t: -0.2})]})
+    oe, he = run_both(H, s2)
+    assert_bodies_equal(oe, he, s2)
+    s3 = spec(3, 2, [1, 1, 1], {0: ([10, 9, 12], [0, 0, 0])}, 0.9, (4, 2, 1), snaps=6,
+              quantities=[(("sphere", 3, (5, 4, 6)), "PRESSURE", 2.0)],
+              borders={0: [(2, ("infinite",), {"Szz": lambda t: 0.0, "Sxz": lambda t: 0.0,
+                                               "Syz": lambda t: 0.0}),
+                           (0, ("cylinder", 3, (0, 4, 6), (20, 4, 6)), {"Vx": f})]})
+    oe, he = run_both(H, s3)
+    assert he.path(0) == "split"
+    assert_bodies_equal(oe, he, s3)
+
+
+def test_engine_setup_areas_waves_vectors_3d(H):
+    """MaterialsCondition / InitialCondition with every area kind, vectors,
+    waves and quantities summed in order, three materials: bitwise == oracle."""
+    s = spec(3, 2, [0.5, 1.0, 0.75], {0: ([14, 11, 16], [2, 0, 1])}, 0.7, (4, 2, 1),
+             inhomogeneities=[(("sphere", 2.5, (4, 5, 6)), (2, 1, 1.5)),
+                              (("cylinder", 1.5, (0, 0, 0), (8, 11, 12)), (3, 0.5, 2))],
+             snaps=4,
+             vectors=[(("box", (1, 1, 1), (6, 8, 9)), [0.1 * i for i in range(9)])],
+             waves=[(("box", (2, 2, 2), (5, 6, 8)), "S2_BACKWARD", 2, "Vy", 0.7),
+                    (("sphere", 3, (3, 5, 7)), "P_FORWARD", 1, "PRESSURE", -1.0)],
+             quantities=[(("infinite",), "Syz", 0.3)])
+    oe, he = run_both(H, s)
+    assert_bodies_equal(oe, he, s)
+
+
+def test_engine_bad_courant_raises(H):
+    s = spec(3, 2, [1, 1, 1], {0: ([6, 6, 6], [0, 0, 0])}, 2.5, (4, 2, 1), snaps=1)
+    he = H.Engine(host_task(s))
+    with pytest.raises(H.GcmException):
+        he.run()
