@@ -72,9 +72,8 @@ __device__ __forceinline__ double newton_minmax(const double (&s)[BS + 1], int k
 		for (int j = 0; j <= BS - i; j++) d[j] = (d[j + 1] - d[j]) * c;
 		ans += d[0];
 	}
-	if (ans > mx) ans = mx;
-	else if (ans < mn) ans = mn;
-	return ans;
+	// if (ans > max) ans = max; else if (ans < min) ans = min;  as selects
+	return (ans > mx) ? mx : ((ans < mn) ? mn : ans);
 }
 
 // Same with compile-time coefficients held in registers by the caller.

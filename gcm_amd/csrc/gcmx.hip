@@ -66,7 +66,8 @@ struct gcmx_ctx {
 	uint8_t* mat_d = nullptr;      // inner nodes, linear inner order; null = homogeneous
 	AxisTable* tabs_d = nullptr;   // [mat][D]
 	double tabs_tau = NAN;
-	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso pattern)
+	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso structure)
+	IsoAxis iso[3] = {};           // per-axis values for the fast kernels (tau part in build_tables)
 	bool ghosts_touched = false;   // border fills / contact copies happened
 	gcmx_path path = GCMX_PATH_AUTO;
 	// halo exchange
@@ -180,6 +181,24 @@ gcmx_status build_tables(gcmx_ctx* c, double tau) {
 				for (int i = 1; i <= bs; i++) t.coef[k][i - 1] = ((q - i) + 1) / i;
 			}
 		}
+	if (c->iso_fast) {
+		for (int s = 0; s < D; s++) {
+			const AxisTable& t = h[s];
+			IsoAxis& A = c->iso[s];
+			// feet k and k^1 share q; feet 2..5 share q (|L| equal, checked at extraction)
+			for (int k = 1; k < 6; k++) {
+				const int ref = (k < 2) ? 0 : 2;
+				if (t.kf[k] != t.kf[ref] || std::memcmp(t.coef[k], t.coef[ref], sizeof(t.coef[k])) != 0)
+					return fail(GCMX_ERR_STATE, "inconsistent foot data");
+			}
+			for (int i = 0; i < 3; i++) {
+				A.c1[i] = i < bs ? t.coef[0][i] : 0.0;
+				A.c2[i] = i < bs ? t.coef[2][i] : 0.0;
+			}
+			A.kf1 = t.kf[0];
+			A.kf2 = t.kf[2];
+		}
+	}
 	HIP_TRY(hipMemcpyAsync(c->tabs_d, h.data(), h.size() * sizeof(AxisTable),
 	                       hipMemcpyHostToDevice, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -240,11 +259,12 @@ gcmx_status halo_exchange_impl(gcmx_ctx* c) {
 // Fast kernels: 3-D, one material, no per-node ids, isotropic zero pattern.
 void refresh_fast(gcmx_ctx* c) {
 	const int D = c->D, M = c->M;
-	bool fits = (D == 3) && (c->mat_d == nullptr) && (c->n_mat == 1);
+	bool fits = (D == 3) && (c->mat_d == nullptr) && (c->n_mat == 1) && fast_layout_ok(c->geo);
 	for (int sx = 0; fits && sx < D; sx++)
-		fits = iso_pattern_fits(sx, &c->U[(size_t)sx * M * M], &c->U1[(size_t)sx * M * M],
-		                        &c->L[(size_t)sx * M]);
+		fits = iso_axis_extract(sx, &c->U[(size_t)sx * M * M], &c->U1[(size_t)sx * M * M],
+		                        &c->L[(size_t)sx * M], c->iso[sx]);
 	c->iso_fast = fits;
+	c->tabs_tau = NAN;
 }
 
 gcmx_path effective_path(gcmx_ctx* c) {
@@ -266,7 +286,6 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	}
 	const Geo& g = c->geo;
 	const double bytes = node_stage_bytes(c) * (double)g.n_inner;
-	const AxisTable* tab = c->tabs_d + axis;  // material 0
 	const gcmx_path p = effective_path(c);
 	bool ok;
 	if (p == GCMX_PATH_GENERIC) {
@@ -274,10 +293,10 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 		ok = launch_stage_generic(c->cur, c->nxt, g, axis, c->tabs_d, c->mat_d, c->stream);
 	} else if (axis < 2) {
 		Timed t(c, axis == 0 ? "march_x" : "march_y", bytes, c->stream);
-		ok = launch_march(c->cur, c->nxt, g, axis, tab, 0, g.sizes[0], c->stream);
+		ok = launch_march(c->cur, c->nxt, g, axis, c->iso[axis], 0, g.sizes[0], c->stream);
 	} else {
 		Timed t(c, "line_z", bytes, c->stream);
-		ok = launch_line_z(c->cur, c->nxt, g, tab, 0, g.sizes[0], c->stream);
+		ok = launch_line_z(c->cur, c->nxt, g, c->iso[2], 0, g.sizes[0], c->stream);
 	}
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "no kernel variant for this configuration");
 	HIP_TRY(hipGetLastError());
@@ -596,12 +615,11 @@ gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 	bool ok;
 	{
 		Timed t(c, "march_x", bytes, c->stream);
-		ok = launch_march(c->cur, c->nxt, g, 0, c->tabs_d + 0, 0, g.sizes[0], c->stream);
+		ok = launch_march(c->cur, c->nxt, g, 0, c->iso[0], 0, g.sizes[0], c->stream);
 	}
 	if (ok) {
 		Timed t(c, "fused_yz", bytes, c->stream);
-		ok = launch_fused_yz(c->nxt, c->cur, g, c->tabs_d + 1, c->tabs_d + 2, 0, g.sizes[0],
-		                     c->stream);
+		ok = launch_fused_yz(c->nxt, c->cur, g, c->iso[1], c->iso[2], 0, g.sizes[0], c->stream);
 	}
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
 	HIP_TRY(hipGetLastError());

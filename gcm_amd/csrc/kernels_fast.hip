@@ -2,28 +2,37 @@
 //
 // Same arithmetic as k_stage_generic (and therefore as the reference stage,
 // engine/cubic/GridCharacteristicMethod.hpp:42-52), specialised at compile time
-// on the zero pattern of the isotropic-elastic U / U1 in the axis-aligned basis
-// (ElasticModel.hpp:416-553) and on the eigenvalue structure
-// L = (c1,-c1,c2,-c2,c2,-c2,0,0,0) (ElasticModel.hpp:401-407).  The host checks
-// that the actual matrices fit the pattern before choosing these kernels.
+// on the STRUCTURE of the isotropic-elastic U / U1 in the axis-aligned basis
+// (ElasticModel.hpp:416-553) and on L = (c1,-c1,c2,-c2,c2,-c2,0,0,0)
+// (ElasticModel.hpp:401-407):
 //
-//   k_march<S>   : stage along a strided axis S in {0 (X), 1 (Y)}.  One thread per
-//                  (other axis, z) column marches along S keeping a register
-//                  window of 2*BS+1 planes, so every element is read from HBM
-//                  once (plus a 2*BS-plane halo per chunk).
-//   k_line_z     : stage along the contiguous axis Z: a 256-node row segment plus
-//                  its BS-node halos staged in LDS, neighbours read from LDS.
-//   k_fused_yz   : Y stage then Z stage of one time step in ONE pass.  A block owns
-//                  one x plane and a chunk of y rows with the whole z row; it
-//                  marches along y (register window), hands each Y-stage row to
-//                  the Z stage through LDS and writes only the Z-stage result.
-//                  Halves the HBM traffic of the Y/Z stages.
+//  * every non-zero matrix entry is either an exact constant (+-1, +-1/2) or
+//    +-one of six per-axis material magnitudes (IsoAxis::a, b, g, p1, p2, s);
+//    the host extracts them and verifies the WHOLE matrices bitwise against this
+//    structure (iso_axis_extract) before these kernels may run;
+//  * u*v with u = +-1 is exact (a sign), u = +-1/2 uses the inline constant, and
+//    -(m*v) == (-m)*v bitwise, so products and their summation order are the
+//    reference's (linal/functions.hpp:254-267, linal/operators.hpp:109-123);
+//  * feet k and k^1 share q (|L| equal), hence the Newton coefficients.
+//
+// Kernels:
+//   k_march<S>  : stage along a strided axis S in {0 (X), 1 (Y)}; one thread per
+//                 (other axis, z) column marches 64 planes along S with a ring
+//                 window of 2*BS+1 planes in registers and the next plane
+//                 prefetched: every element is read from HBM once (+ a 2*BS-plane
+//                 halo per chunk).
+//   k_line_z    : stage along the contiguous axis Z: 256-node row segment plus its
+//                 BS-node halos in LDS.
+//   k_fused_yz  : Y stage then Z stage of one time step in ONE pass: a block owns one
+//                 x plane, a chunk of y rows and the whole z row, marches y (ring
+//                 window), hands each Y-stage row to the Z stage through
+//                 double-buffered LDS and writes only the Z result.
 #include "common.hpp"
 #include "launch.hpp"
 
 namespace gcmx {
 
-// --------------------------------------------------------- zero patterns --
+// ----------------------------------------------------------- structure --
 
 // Index of sigma(i,j) in the 3-D PDE vector (VelocitySigmaVariables.hpp:82-96).
 __host__ __device__ constexpr int sig3(int i, int j) {
@@ -32,44 +41,71 @@ __host__ __device__ constexpr int sig3(int i, int j) {
 }
 __host__ __device__ constexpr unsigned bit(int i) { return 1u << i; }
 
-// Tangent axes of createLocalBasis(e_s) (linal/basis.hpp:58-65).
+// createLocalBasis(e_s) (linal/basis.hpp:58-65, geometry.hpp:35-52): the two
+// tangents are +-e_t1, +-e_t2 with these axes and signs.
 __host__ __device__ constexpr int tang1(int s) { return s == 0 ? 1 : 0; }
 __host__ __device__ constexpr int tang2(int s) { return s == 2 ? 1 : 2; }
+__host__ __device__ constexpr int sgn1(int s) { return s == 0 ? -1 : 1; }
+__host__ __device__ constexpr int sgn2(int s) { return s == 2 ? 1 : -1; }
 
-// Non-zero columns of row k of U (ElasticModel.hpp:486-553).
-__host__ __device__ constexpr unsigned iso_u_row(int s, int k) {
-	const int t1 = tang1(s), t2 = tang2(s);
-	return (k < 2)   ? (bit(s) | bit(sig3(s, s)))
-	       : (k < 4) ? (bit(t1) | bit(sig3(t1, s)))
-	       : (k < 6) ? (bit(t2) | bit(sig3(t2, s)))
-	       : (k == 6) ? bit(sig3(t1, t2))
-	       : (k == 7) ? (bit(sig3(t1, t1)) | bit(sig3(t2, t2)))
-	                  : (bit(sig3(t1, t1)) | bit(sig3(t2, t2)) | bit(sig3(s, s)));
+// A matrix entry: `sign * (slot value or constant)`.
+enum Slot : int { kZero = 0, kOne, kHalf, kA, kB, kG, kP1, kP2, kS };
+struct Coef {
+	int slot;
+	int sign;
+};
+__host__ __device__ constexpr Coef cz() { return Coef{kZero, 0}; }
+
+// U(k, j) (ElasticModel.hpp:486-553): rows are eigenstrings.
+__host__ __device__ constexpr Coef iso_u(int S, int k, int j) {
+	const int t1 = tang1(S), t2 = tang2(S), s1 = sgn1(S), s2 = sgn2(S);
+	const int ss = sig3(S, S), st1 = sig3(t1, S), st2 = sig3(t2, S);
+	const int s11 = sig3(t1, t1), s22 = sig3(t2, t2), s12 = sig3(t1, t2);
+	return (k == 0) ? (j == S ? Coef{kOne, 1} : j == ss ? Coef{kA, 1} : cz())
+	     : (k == 1) ? (j == S ? Coef{kOne, 1} : j == ss ? Coef{kA, -1} : cz())
+	     : (k == 2) ? (j == t1 ? Coef{kOne, s1} : j == st1 ? Coef{kB, s1} : cz())
+	     : (k == 3) ? (j == t1 ? Coef{kOne, s1} : j == st1 ? Coef{kB, -s1} : cz())
+	     : (k == 4) ? (j == t2 ? Coef{kOne, s2} : j == st2 ? Coef{kB, s2} : cz())
+	     : (k == 5) ? (j == t2 ? Coef{kOne, s2} : j == st2 ? Coef{kB, -s2} : cz())
+	     : (k == 6) ? (j == s12 ? Coef{kOne, s1 * s2} : cz())
+	     : (k == 7) ? (j == s11 ? Coef{kOne, 1} : j == s22 ? Coef{kOne, -1} : cz())
+	                : (j == s11 ? Coef{kOne, 1} : j == s22 ? Coef{kOne, 1}
+	                   : j == ss ? Coef{kG, 1} : cz());
 }
-// Non-zero rows of column n of U1 (ElasticModel.hpp:416-483).
-__host__ __device__ constexpr unsigned iso_u1_col(int s, int n) {
-	const int t1 = tang1(s), t2 = tang2(s);
-	return (n < 2)   ? (bit(s) | bit(sig3(0, 0)) | bit(sig3(1, 1)) | bit(sig3(2, 2)))
-	       : (n < 4) ? (bit(t1) | bit(sig3(s, t1)))
-	       : (n < 6) ? (bit(t2) | bit(sig3(s, t2)))
-	       : (n == 6) ? bit(sig3(t1, t2))
-	                  : (bit(sig3(t1, t1)) | bit(sig3(t2, t2)));
+
+// U1(c, n) (ElasticModel.hpp:416-483): columns are eigenvectors.
+__host__ __device__ constexpr Coef iso_u1(int S, int c, int n) {
+	const int t1 = tang1(S), t2 = tang2(S), s1 = sgn1(S), s2 = sgn2(S);
+	const int ss = sig3(S, S), st1 = sig3(t1, S), st2 = sig3(t2, S);
+	const int s11 = sig3(t1, t1), s22 = sig3(t2, t2), s12 = sig3(t1, t2);
+	return (n == 0) ? (c == S ? Coef{kHalf, 1} : c == ss ? Coef{kP1, 1}
+	                   : (c == s11 || c == s22) ? Coef{kP2, 1} : cz())
+	     : (n == 1) ? (c == S ? Coef{kHalf, 1} : c == ss ? Coef{kP1, -1}
+	                   : (c == s11 || c == s22) ? Coef{kP2, -1} : cz())
+	     : (n == 2) ? (c == t1 ? Coef{kHalf, s1} : c == st1 ? Coef{kS, s1} : cz())
+	     : (n == 3) ? (c == t1 ? Coef{kHalf, s1} : c == st1 ? Coef{kS, -s1} : cz())
+	     : (n == 4) ? (c == t2 ? Coef{kHalf, s2} : c == st2 ? Coef{kS, s2} : cz())
+	     : (n == 5) ? (c == t2 ? Coef{kHalf, s2} : c == st2 ? Coef{kS, -s2} : cz())
+	     : (n == 6) ? (c == s12 ? Coef{kOne, s1 * s2} : cz())
+	     : (n == 7) ? (c == s11 ? Coef{kHalf, 1} : c == s22 ? Coef{kHalf, -1} : cz())
+	                : (c == s11 ? Coef{kHalf, 1} : c == s22 ? Coef{kHalf, 1} : cz());
 }
-__host__ __device__ constexpr bool iso_u1(int s, int c, int n) {
-	return (iso_u1_col(s, n) >> c) & 1u;
+
+// Components read at the neighbours (rows 0..5) / only at the node (rows 6..8).
+__host__ __device__ constexpr unsigned iso_window(int S) {
+	unsigned m = 0;
+	for (int k = 0; k < 6; k++)
+		for (int j = 0; j < 9; j++)
+			if (iso_u(S, k, j).slot != kZero) m |= bit(j);
+	return m;
 }
-__host__ __device__ constexpr bool iso_u(int s, int k, int j) {
-	return (iso_u_row(s, k) >> j) & 1u;
+__host__ __device__ constexpr unsigned iso_center_only(int S) {
+	unsigned m = 0;
+	for (int k = 6; k < 9; k++)
+		for (int j = 0; j < 9; j++)
+			if (iso_u(S, k, j).slot != kZero) m |= bit(j);
+	return m & ~iso_window(S);
 }
-// Components read at the neighbours (rows with non-zero eigenvalue).
-__host__ __device__ constexpr unsigned iso_window(int s) {
-	return iso_u_row(s, 0) | iso_u_row(s, 2) | iso_u_row(s, 4);
-}
-// Components read only at the node itself.
-__host__ __device__ constexpr unsigned iso_center_only(int s) {
-	return (iso_u_row(s, 6) | iso_u_row(s, 7) | iso_u_row(s, 8)) & ~iso_window(s);
-}
-// Position of component j among the window components.
 __host__ __device__ constexpr int wslot(unsigned mask, int j) {
 	int n = 0;
 	for (int i = 0; i < j; i++) n += (mask >> i) & 1u;
@@ -81,142 +117,191 @@ __host__ __device__ constexpr int popc9(unsigned m) {
 	return n;
 }
 
-bool iso_pattern_fits(int s, const double* U, const double* U1, const double* L) {
-	for (int k = 0; k < 9; k++) {
-		if (k < 6) {
-			if (!((k % 2 == 0) ? (L[k] > 0) : (L[k] < 0))) return false;
-		} else if (L[k] != 0.0) {
-			return false;
-		}
-		for (int j = 0; j < 9; j++) {
-			if (U[k * 9 + j] != 0.0 && !iso_u(s, k, j)) return false;
-			if (U1[k * 9 + j] != 0.0 && !iso_u1(s, k, j)) return false;
-		}
+static double slot_value(const IsoAxis& A, int slot) {
+	switch (slot) {
+	case kOne: return 1.0;
+	case kHalf: return 0.5;
+	case kA: return A.a;
+	case kB: return A.b;
+	case kG: return A.g;
+	case kP1: return A.p1;
+	case kP2: return A.p2;
+	case kS: return A.s;
+	default: return 0.0;
 	}
+}
+
+// Extract the six magnitudes of axis S and check that U, U1, L of that axis are
+// EXACTLY the structure above (zero entries may be +-0; a structural entry may
+// be an exact zero, e.g. lambda = 0).  Fills the tau-independent part of `A`.
+bool iso_axis_extract(int S, const double* U, const double* U1, const double* L, IsoAxis& A) {
+	const int t1 = tang1(S), s1 = sgn1(S);
+	A.a = U[0 * 9 + sig3(S, S)];
+	A.b = s1 * U[2 * 9 + sig3(t1, S)];
+	A.g = U[8 * 9 + sig3(S, S)];
+	A.p1 = U1[sig3(S, S) * 9 + 0];
+	A.p2 = U1[sig3(t1, t1) * 9 + 0];
+	A.s = s1 * U1[sig3(t1, S) * 9 + 2];
+	for (int k = 0; k < 9; k++)
+		for (int j = 0; j < 9; j++) {
+			const Coef cu = iso_u(S, k, j), cu1 = iso_u1(S, k, j);
+			const double eu = cu.sign * slot_value(A, cu.slot);
+			const double eu1 = cu1.sign * slot_value(A, cu1.slot);
+			if (!(U[k * 9 + j] == eu) || !(U1[k * 9 + j] == eu1)) return false;
+			if (cu.slot == kZero && U[k * 9 + j] != 0.0) return false;
+			if (cu1.slot == kZero && U1[k * 9 + j] != 0.0) return false;
+		}
+	// eigenvalues: +-c1, +-c2, +-c2, 0, 0, 0 with the pairs bitwise opposite
+	if (!(L[0] > 0) || !(L[1] == -L[0]) || !(L[2] > 0) || !(L[3] == -L[2]) || !(L[4] == L[2]) ||
+	    !(L[5] == -L[2]) || L[6] != 0.0 || L[7] != 0.0 || L[8] != 0.0)
+		return false;
 	return true;
 }
 
-// Reads of the uniform per-axis table.  The table sits in global memory; every
-// index is a compile-time constant, so these are scalar loads through the
-// scalar cache (s_load), never VGPR traffic.
-struct Tab {
-	const AxisTable* __restrict__ t;
-	__device__ __forceinline__ double u(int k, int j) const { return t->U[k * 9 + j]; }
-	__device__ __forceinline__ double u1(int c, int n) const { return t->U1[c * 9 + n]; }
-	__device__ __forceinline__ int kf(int k) const { return t->kf[k]; }
-	__device__ __forceinline__ const double* coef(int k) const { return t->coef[k]; }
+// u * v for a structural entry; exact w.r.t. the reference product fl(u * v).
+template <int SLOT, int SIGN>
+__device__ __forceinline__ double term(const IsoAxis& A, double v) {
+	double m;
+	if constexpr (SLOT == kOne) m = v;
+	else if constexpr (SLOT == kHalf) m = v * 0.5;
+	else if constexpr (SLOT == kA) m = A.a * v;
+	else if constexpr (SLOT == kB) m = A.b * v;
+	else if constexpr (SLOT == kG) m = A.g * v;
+	else if constexpr (SLOT == kP1) m = A.p1 * v;
+	else if constexpr (SLOT == kP2) m = A.p2 * v;
+	else m = A.s * v;
+	return SIGN > 0 ? m : -m;
+}
+
+// Unrolled sum over j of U(k, j) * V(j) (or U1(c, n) * r(n)) in ascending index
+// order, skipping structural zeros, starting from the first non-zero term.
+template <int S, bool ISU1, int ROW, int J = 0>
+struct RowSum {
+	template <class F>
+	__device__ __forceinline__ static double go(const IsoAxis& A, F val, double acc, bool first) {
+		if constexpr (J == 9) {
+			return acc;
+		} else {
+			constexpr Coef c = ISU1 ? iso_u1(S, ROW, J) : iso_u(S, ROW, J);
+			if constexpr (c.slot == kZero) {
+				return RowSum<S, ISU1, ROW, J + 1>::go(A, val, acc, first);
+			} else {
+				const double t = term<c.slot, c.sign>(A, val(J));
+				return RowSum<S, ISU1, ROW, J + 1>::go(A, val, first ? t : acc + t, false);
+			}
+		}
+	}
 };
 
-// One node's stage given accessor functors:
-//   W(j, o) = value of window component j at offset o (|o| <= BS) along S,
-//   C(j)    = value of component j at the node (any component the rows 6..8 use).
-// Returns the 9 outputs.  Operation order = reference (see kernels_generic.hip).
+// One node's stage.  W(j, o): window component j at offset o along S
+// (|o| <= BS); C(j): node value of a component rows 6..8 read.
 template <int S, int BS, class WF, class CF>
-__device__ __forceinline__ void node_update(const Tab& T, WF W, CF C, double (&out)[9]) {
+__device__ __forceinline__ void node_update(const IsoAxis& A, WF W, CF C, double (&out)[9]) {
 	double r[9];
 #pragma unroll
-	for (int k = 0; k < 9; k++) {
-		double acc = 0.0;
-		bool first = true;
+	for (int k = 0; k < 6; k++) {
+		const int sh = (k % 2 == 0) ? -1 : 1;  // L > 0 -> dx < 0 -> neighbours at -1, -2, ..
+		const double* coef = (k < 2) ? A.c1 : A.c2;
+		const int kf = (k < 2) ? A.kf1 : A.kf2;
+		auto interp = [&](int j) {
+			double sv[BS + 1];
 #pragma unroll
-		for (int j = 0; j < 9; j++) {
-			if (!iso_u(S, k, j)) continue;
-			double v;
-			if (k < 6) {
-				double sv[BS + 1];
-				const int sh = (k % 2 == 0) ? -1 : 1;  // L>0 -> dx<0 -> shift -1
-#pragma unroll
-				for (int a = 0; a <= BS; a++) sv[a] = W(j, sh * a);
-				v = newton_minmax<BS>(sv, T.kf(k), T.coef(k));
-			} else {
-				v = C(j);  // q == 0: the interpolant is the node value
-			}
-			const double u = T.u(k, j);
-			acc = first ? u * v : acc + u * v;
-			first = false;
+			for (int i = 0; i <= BS; i++) sv[i] = W(j, sh * i);
+			return newton_minmax<BS>(sv, kf, coef);
+		};
+		switch (k) {
+		case 0: r[0] = RowSum<S, false, 0>::go(A, interp, 0.0, true); break;
+		case 1: r[1] = RowSum<S, false, 1>::go(A, interp, 0.0, true); break;
+		case 2: r[2] = RowSum<S, false, 2>::go(A, interp, 0.0, true); break;
+		case 3: r[3] = RowSum<S, false, 3>::go(A, interp, 0.0, true); break;
+		case 4: r[4] = RowSum<S, false, 4>::go(A, interp, 0.0, true); break;
+		default: r[5] = RowSum<S, false, 5>::go(A, interp, 0.0, true); break;
 		}
-		r[k] = acc;
 	}
-#pragma unroll
-	for (int c = 0; c < 9; c++) {
-		double acc = 0.0;
-		bool first = true;
-#pragma unroll
-		for (int n = 0; n < 9; n++) {
-			if (!iso_u1(S, c, n)) continue;
-			const double w = T.u1(c, n);
-			acc = first ? w * r[n] : acc + w * r[n];
-			first = false;
-		}
-		out[c] = acc;
-	}
+	// q == 0: the interpolant is the node value itself
+	r[6] = RowSum<S, false, 6>::go(A, C, 0.0, true);
+	r[7] = RowSum<S, false, 7>::go(A, C, 0.0, true);
+	r[8] = RowSum<S, false, 8>::go(A, C, 0.0, true);
+	auto rv = [&](int n) { return r[n]; };
+	out[0] = RowSum<S, true, 0>::go(A, rv, 0.0, true);
+	out[1] = RowSum<S, true, 1>::go(A, rv, 0.0, true);
+	out[2] = RowSum<S, true, 2>::go(A, rv, 0.0, true);
+	out[3] = RowSum<S, true, 3>::go(A, rv, 0.0, true);
+	out[4] = RowSum<S, true, 4>::go(A, rv, 0.0, true);
+	out[5] = RowSum<S, true, 5>::go(A, rv, 0.0, true);
+	out[6] = RowSum<S, true, 6>::go(A, rv, 0.0, true);
+	out[7] = RowSum<S, true, 7>::go(A, rv, 0.0, true);
+	out[8] = RowSum<S, true, 8>::go(A, rv, 0.0, true);
 }
+
+// Per-component plane base pointers are uniform; per-thread offsets are 32-bit
+// element indices (layer planes are < 2^29 elements, checked on the host), so
+// the loads use the scalar-base + 32-bit-offset addressing form.
+struct Planes {
+	const double* __restrict__ p;
+	long long cs;
+	__device__ __forceinline__ double ld(int j, unsigned off) const { return p[j * cs + off]; }
+};
 
 // ---------------------------------------------------------------- march --
 
 constexpr int kMarchThreads = 256;
 
-// Stage along S (0 = X, 1 = Y) for planes [m0, m1) of axis S in chunks of
-// `chunk` planes; threads over (a, z), a = the other strided axis.
 template <int S, int BS>
-__global__ __launch_bounds__(kMarchThreads) void k_march(const double* __restrict__ cur,
+__global__ __launch_bounds__(kMarchThreads, 4) void k_march(const double* __restrict__ cur,
                                                          double* __restrict__ nxt, Geo g,
-                                                         const AxisTable* __restrict__ tab,
-                                                         int m0, int m1, int chunk) {
+                                                         IsoAxis A, int m0, int m1, int chunk) {
 	constexpr unsigned WM = iso_window(S);
 	constexpr unsigned CM = iso_center_only(S);
 	constexpr int NW = popc9(WM);
 	constexpr int W = 2 * BS + 1;
-	constexpr int A = 1 - S;  // the other strided axis
-	const Tab T{tab};
+	constexpr int OA = 1 - S;  // the other strided axis
 
 	const int z = blockIdx.x * kMarchThreads + threadIdx.x;
 	const int a = blockIdx.y;
 	const int mb = m0 + blockIdx.z * chunk;
 	const int me = min(mb + chunk, m1);
 	if (z >= g.sizes[2]) return;
-	const long long st = g.stride[S];
-	const double* src = cur + g.origin + a * g.stride[A] + z;
-	double* dst = nxt + g.origin + a * g.stride[A] + z;
+	const unsigned st = (unsigned)g.stride[S];
+	const unsigned base = (unsigned)(g.origin + a * g.stride[OA] + z);
+	const Planes in{cur, g.cs};
 
-	double win[NW][W];
-	double ctr[9];
-	// prologue: planes mb-BS .. mb+BS-1
+	double win[NW][W];  // window: slot BS + o holds plane m + o
+	double pw[NW], pc[9], ctr[9];
 #pragma unroll
 	for (int j = 0; j < 9; j++) {
 		if (!((WM >> j) & 1u)) continue;
 #pragma unroll
 		for (int o = 0; o < W - 1; o++)
-			win[wslot(WM, j)][o] = src[j * g.cs + (long long)(mb - BS + o) * st];
+			win[wslot(WM, j)][o] = in.ld(j, base + (unsigned)(mb - BS + o) * st);
+		pw[wslot(WM, j)] = in.ld(j, base + (unsigned)(mb + BS) * st);
 	}
-	// prefetch registers for the first iteration
-	double pw[NW];
-	double pc[9];
 #pragma unroll
-	for (int j = 0; j < 9; j++) {
-		if ((WM >> j) & 1u) pw[wslot(WM, j)] = src[j * g.cs + (long long)(mb + BS) * st];
-		if ((CM >> j) & 1u) pc[j] = src[j * g.cs + (long long)mb * st];
-	}
+	for (int j = 0; j < 9; j++)
+		if ((CM >> j) & 1u) pc[j] = in.ld(j, base + (unsigned)mb * st);
+
 	for (int m = mb; m < me; m++) {
 #pragma unroll
 		for (int j = 0; j < 9; j++) {
 			if ((WM >> j) & 1u) win[wslot(WM, j)][W - 1] = pw[wslot(WM, j)];
 			if ((CM >> j) & 1u) ctr[j] = pc[j];
 		}
-		if (m + 1 < me) {  // issue next iteration's loads before computing
+		if (m + 1 < me) {  // next iteration's loads go out before this node's math
+			const unsigned offw = base + (unsigned)(m + 1 + BS) * st;
+			const unsigned offc = base + (unsigned)(m + 1) * st;
 #pragma unroll
 			for (int j = 0; j < 9; j++) {
-				if ((WM >> j) & 1u)
-					pw[wslot(WM, j)] = src[j * g.cs + (long long)(m + 1 + BS) * st];
-				if ((CM >> j) & 1u) pc[j] = src[j * g.cs + (long long)(m + 1) * st];
+				if ((WM >> j) & 1u) pw[wslot(WM, j)] = in.ld(j, offw);
+				if ((CM >> j) & 1u) pc[j] = in.ld(j, offc);
 			}
 		}
 		double out[9];
 		node_update<S, BS>(
-		    T, [&](int j, int o) { return win[wslot(WM, j)][BS + o]; },
+		    A, [&](int j, int o) { return win[wslot(WM, j)][BS + o]; },
 		    [&](int j) { return ((WM >> j) & 1u) ? win[wslot(WM, j)][BS] : ctr[j]; }, out);
+		const unsigned offo = base + (unsigned)m * st;
 #pragma unroll
-		for (int c = 0; c < 9; c++) dst[c * g.cs + (long long)m * st] = out[c];
+		for (int c = 0; c < 9; c++) nxt[c * g.cs + offo] = out[c];
 #pragma unroll
 		for (int q = 0; q < NW; q++)
 #pragma unroll
@@ -231,60 +316,55 @@ constexpr int kLineThreads = 256;
 template <int BS>
 __global__ __launch_bounds__(kLineThreads) void k_line_z(const double* __restrict__ cur,
                                                          double* __restrict__ nxt, Geo g,
-                                                         const AxisTable* __restrict__ tab,
-                                                         int x0) {
+                                                         IsoAxis A, int x0) {
 	constexpr int S = 2;
 	constexpr unsigned WM = iso_window(S);
 	constexpr unsigned CM = iso_center_only(S);
 	constexpr int NW = popc9(WM);
 	constexpr int LW = kLineThreads + 2 * BS;
 	__shared__ double lds[NW][LW];
-	const Tab T{tab};
 
 	const int z0 = blockIdx.x * kLineThreads;
 	const int y = blockIdx.y;
 	const int x = x0 + blockIdx.z;
 	const int tid = threadIdx.x;
 	const int Z = g.sizes[2];
-	const long long rowoff = g.origin + x * g.stride[0] + y * g.stride[1];
-	const double* src = cur + rowoff;
-	// stage the row segment [z0-BS, z0+256+BS) of the window components
+	const unsigned row = (unsigned)(g.origin + x * g.stride[0] + y * g.stride[1]);
+	const Planes in{cur, g.cs};
 	for (int i = tid; i < LW; i += kLineThreads) {
 		const int zz = z0 - BS + i;
 		if (zz < Z + BS) {
 #pragma unroll
 			for (int j = 0; j < 9; j++)
-				if ((WM >> j) & 1u) lds[wslot(WM, j)][i] = src[j * g.cs + zz];
+				if ((WM >> j) & 1u) lds[wslot(WM, j)][i] = in.ld(j, row + zz);
 		}
 	}
 	const int z = z0 + tid;
 	double ctr[9];
 #pragma unroll
 	for (int j = 0; j < 9; j++)
-		if (((CM >> j) & 1u) && z < Z) ctr[j] = src[j * g.cs + z];
+		if (((CM >> j) & 1u) && z < Z) ctr[j] = in.ld(j, row + z);
 	__syncthreads();
 	if (z >= Z) return;
 	double out[9];
 	node_update<S, BS>(
-	    T, [&](int j, int o) { return lds[wslot(WM, j)][BS + tid + o]; },
+	    A, [&](int j, int o) { return lds[wslot(WM, j)][BS + tid + o]; },
 	    [&](int j) { return ((WM >> j) & 1u) ? lds[wslot(WM, j)][BS + tid] : ctr[j]; }, out);
-	double* dst = nxt + rowoff + z;
 #pragma unroll
-	for (int c = 0; c < 9; c++) dst[c * g.cs] = out[c];
+	for (int c = 0; c < 9; c++) nxt[c * g.cs + row + z] = out[c];
 }
 
 // -------------------------------------------------------------- fused yz --
 
 // Block = one x plane, rows [yb, ye) of a y chunk, all z (blockDim = ZT >= Z).
-// Reads the X-stage output `in` (Y-stage input), writes the Z-stage output to
-// `out`.  `in` and `out` are different layers; the z-ghosts the Z stage reads
-// are those of `out` (the layer the Y stage would have written).
+// Reads the X-stage output `in` (Y-stage input), writes the Z-stage output into
+// `outl`.  Precondition (the host only picks this path when it holds): every
+// y/z ghost of both layers is zero, so ghost rows and the Z stage's ghost
+// neighbours are the constant 0.0 instead of memory reads.
 template <int BS, int ZT>
-__global__ __launch_bounds__(ZT) void k_fused_yz(const double* __restrict__ in,
-                                                 double* __restrict__ outl, Geo g,
-                                                 const AxisTable* __restrict__ tabY,
-                                                 const AxisTable* __restrict__ tabZ, int x0,
-                                                 int chunk) {
+__global__ __launch_bounds__(ZT, (BS <= 2 ? 4 : 2)) void k_fused_yz(const double* __restrict__ in,
+                                                 double* __restrict__ outl, Geo g, IsoAxis AY,
+                                                 IsoAxis AZ, int x0, int chunk) {
 	constexpr unsigned WMY = iso_window(1);
 	constexpr unsigned CMY = iso_center_only(1);
 	constexpr int NWY = popc9(WMY);
@@ -293,7 +373,6 @@ __global__ __launch_bounds__(ZT) void k_fused_yz(const double* __restrict__ in,
 	constexpr int W = 2 * BS + 1;
 	constexpr int LW = ZT + 2 * BS;
 	__shared__ double lds[2][NWZ][LW];
-	const Tab TY{tabY}, TZ{tabZ};
 
 	const int z = threadIdx.x;
 	const int x = x0 + blockIdx.y;
@@ -301,32 +380,38 @@ __global__ __launch_bounds__(ZT) void k_fused_yz(const double* __restrict__ in,
 	const int yb = blockIdx.x * chunk;
 	const int ye = min(yb + chunk, Y);
 	const bool live = z < Z;
-	const int zc = live ? z : Z - 1;  // clamp idle lanes onto a valid column
-	const long long st = g.stride[1];
-	const long long plane = g.origin + x * g.stride[0];
-	const double* src = in + plane + zc;
+	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
+	const unsigned st = (unsigned)g.stride[1];
+	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
+	const unsigned base = plane + zc;
+	const Planes src{in, g.cs};
 
-	// z-ghost entries of the Z stage: 2*BS per row, loaded by threads [0, 2BS)
-	const bool ghost_lane = z < 2 * BS;
-	const int gz = (z < BS) ? (z - BS) : (Z + z - BS);  // ghost z index
-	const int gslot = (z < BS) ? z : (Z + z);           // its LDS slot
+	// zero ghost slots of both LDS row buffers once (never overwritten)
+	if (z < 2 * BS) {
+		const int gslot = (z < BS) ? z : (Z + z);
+#pragma unroll
+		for (int q = 0; q < NWZ; q++) {
+			lds[0][q][gslot] = 0.0;
+			lds[1][q][gslot] = 0.0;
+		}
+	}
+	auto row_ld = [&](int j, int yy) -> double {  // ghost rows are zero
+		return (yy >= 0 && yy < Y) ? src.ld(j, base + (unsigned)yy * st) : 0.0;
+	};
 
 	double win[NWY][W];
-	double ctr[9];
+	double pw[NWY], pc[9], ctr[9];
 #pragma unroll
 	for (int j = 0; j < 9; j++) {
 		if (!((WMY >> j) & 1u)) continue;
 #pragma unroll
-		for (int o = 0; o < W - 1; o++)
-			win[wslot(WMY, j)][o] = src[j * g.cs + (long long)(yb - BS + o) * st];
+		for (int o = 0; o < W - 1; o++) win[wslot(WMY, j)][o] = row_ld(j, yb - BS + o);
+		pw[wslot(WMY, j)] = row_ld(j, yb + BS);
 	}
-	double pw[NWY];
-	double pc[9];
 #pragma unroll
-	for (int j = 0; j < 9; j++) {
-		if ((WMY >> j) & 1u) pw[wslot(WMY, j)] = src[j * g.cs + (long long)(yb + BS) * st];
-		if ((CMY >> j) & 1u) pc[j] = src[j * g.cs + (long long)yb * st];
-	}
+	for (int j = 0; j < 9; j++)
+		if ((CMY >> j) & 1u) pc[j] = src.ld(j, base + (unsigned)yb * st);
+
 	int buf = 0;
 	for (int y = yb; y < ye; y++) {
 #pragma unroll
@@ -337,38 +422,31 @@ __global__ __launch_bounds__(ZT) void k_fused_yz(const double* __restrict__ in,
 		if (y + 1 < ye) {
 #pragma unroll
 			for (int j = 0; j < 9; j++) {
-				if ((WMY >> j) & 1u)
-					pw[wslot(WMY, j)] = src[j * g.cs + (long long)(y + 1 + BS) * st];
-				if ((CMY >> j) & 1u) pc[j] = src[j * g.cs + (long long)(y + 1) * st];
+				if ((WMY >> j) & 1u) pw[wslot(WMY, j)] = row_ld(j, y + 1 + BS);
+				if ((CMY >> j) & 1u) pc[j] = src.ld(j, base + (unsigned)(y + 1) * st);
 			}
 		}
 		// ---- Y stage at (x, y, z)
 		double yv[9];
 		node_update<1, BS>(
-		    TY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
+		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
 		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : ctr[j]; }, yv);
 		// ---- hand the row to the Z stage
-		const long long rowoff = plane + (long long)y * st;
 		if (live) {
 #pragma unroll
 			for (int j = 0; j < 9; j++)
 				if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = yv[j];
 		}
-		if (ghost_lane) {
-#pragma unroll
-			for (int j = 0; j < 9; j++)
-				if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][gslot] = outl[rowoff + j * g.cs + gz];
-		}
 		__syncthreads();
 		if (live) {
 			double zv[9];
 			node_update<2, BS>(
-			    TZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
+			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
 			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; },
 			    zv);
-			double* dst = outl + rowoff + z;
+			const unsigned offo = plane + (unsigned)y * st + z;
 #pragma unroll
-			for (int c = 0; c < 9; c++) dst[c * g.cs] = zv[c];
+			for (int c = 0; c < 9; c++) outl[c * g.cs + offo] = zv[c];
 		}
 		buf ^= 1;
 #pragma unroll
@@ -384,90 +462,92 @@ static int march_chunk(int len) { return len < 128 ? len : 64; }
 
 template <int BS>
 static void launch_march_bs(const double* cur, double* nxt, const Geo& g, int s,
-                            const AxisTable* tab, int x0, int x1, hipStream_t st) {
-	// For S = 0 the march axis is X ([x0,x1)); for S = 1 threads cover x in [x0,x1).
-	if (s == 0) {
+                            const IsoAxis& A, int x0, int x1, hipStream_t st) {
+	if (s == 0) {  // march along X over [x0, x1)
 		const int len = x1 - x0;
 		const int chunk = march_chunk(len);
 		dim3 grid((g.sizes[2] + kMarchThreads - 1) / kMarchThreads, g.sizes[1],
 		          (len + chunk - 1) / chunk);
-		hipLaunchKernelGGL((k_march<0, BS>), grid, dim3(kMarchThreads), 0, st, cur, nxt, g, tab,
-		                   x0, x1, chunk);
-	} else {
+		hipLaunchKernelGGL((k_march<0, BS>), grid, dim3(kMarchThreads), 0, st, cur, nxt, g, A, x0,
+		                   x1, chunk);
+	} else {  // march along Y; threads cover x in [x0, x1)
 		const int len = g.sizes[1];
 		const int chunk = march_chunk(len);
 		Geo gg = g;
 		gg.origin = g.origin + (long long)x0 * g.stride[0];
 		dim3 grid((g.sizes[2] + kMarchThreads - 1) / kMarchThreads, x1 - x0,
 		          (len + chunk - 1) / chunk);
-		hipLaunchKernelGGL((k_march<1, BS>), grid, dim3(kMarchThreads), 0, st, cur, nxt, gg,
-		                   tab, 0, len, chunk);
+		hipLaunchKernelGGL((k_march<1, BS>), grid, dim3(kMarchThreads), 0, st, cur, nxt, gg, A, 0,
+		                   len, chunk);
 	}
 }
 
-bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const AxisTable* tab,
-                  int x0, int x1, hipStream_t st) {
-	if (g.D != 3 || s > 1 || x1 <= x0) return false;
+bool fast_layout_ok(const Geo& g) {
+	return g.D == 3 && g.bs >= 1 && g.bs <= 3 && g.cs * 8 < (1LL << 32);
+}
+
+bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const IsoAxis& A, int x0,
+                  int x1, hipStream_t st) {
+	if (!fast_layout_ok(g) || s > 1 || x1 <= x0) return false;
 	switch (g.bs) {
-	case 1: launch_march_bs<1>(cur, nxt, g, s, tab, x0, x1, st); return true;
-	case 2: launch_march_bs<2>(cur, nxt, g, s, tab, x0, x1, st); return true;
-	case 3: launch_march_bs<3>(cur, nxt, g, s, tab, x0, x1, st); return true;
+	case 1: launch_march_bs<1>(cur, nxt, g, s, A, x0, x1, st); return true;
+	case 2: launch_march_bs<2>(cur, nxt, g, s, A, x0, x1, st); return true;
+	case 3: launch_march_bs<3>(cur, nxt, g, s, A, x0, x1, st); return true;
 	default: return false;
 	}
 }
 
 template <int BS>
-static void launch_line_bs(const double* cur, double* nxt, const Geo& g, const AxisTable* tab,
+static void launch_line_bs(const double* cur, double* nxt, const Geo& g, const IsoAxis& A,
                            int x0, int x1, hipStream_t st) {
 	dim3 grid((g.sizes[2] + kLineThreads - 1) / kLineThreads, g.sizes[1], x1 - x0);
-	hipLaunchKernelGGL((k_line_z<BS>), grid, dim3(kLineThreads), 0, st, cur, nxt, g, tab, x0);
+	hipLaunchKernelGGL((k_line_z<BS>), grid, dim3(kLineThreads), 0, st, cur, nxt, g, A, x0);
 }
 
-bool launch_line_z(const double* cur, double* nxt, const Geo& g, const AxisTable* tab, int x0,
-                   int x1, hipStream_t st) {
-	if (g.D != 3 || x1 <= x0) return false;
+bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& A, int x0, int x1,
+                   hipStream_t st) {
+	if (!fast_layout_ok(g) || x1 <= x0) return false;
 	switch (g.bs) {
-	case 1: launch_line_bs<1>(cur, nxt, g, tab, x0, x1, st); return true;
-	case 2: launch_line_bs<2>(cur, nxt, g, tab, x0, x1, st); return true;
-	case 3: launch_line_bs<3>(cur, nxt, g, tab, x0, x1, st); return true;
+	case 1: launch_line_bs<1>(cur, nxt, g, A, x0, x1, st); return true;
+	case 2: launch_line_bs<2>(cur, nxt, g, A, x0, x1, st); return true;
+	case 3: launch_line_bs<3>(cur, nxt, g, A, x0, x1, st); return true;
 	default: return false;
 	}
 }
 
 bool fused_yz_supported(const Geo& g) {
-	return g.D == 3 && g.bs >= 1 && g.bs <= 3 && g.sizes[2] <= 1024 && g.sizes[2] >= 2 * g.bs;
+	return fast_layout_ok(g) && g.sizes[2] <= 1024 && g.sizes[2] >= 2 * g.bs;
 }
 
 static int fused_chunk(int Y) { return Y <= 64 ? Y : 64; }
 
 template <int BS, int ZT>
-static void launch_fused_t(const double* in, double* out, const Geo& g, const AxisTable* ty,
-                           const AxisTable* tz, int x0, int x1, hipStream_t st) {
+static void launch_fused_t(const double* in, double* out, const Geo& g, const IsoAxis& ay,
+                           const IsoAxis& az, int x0, int x1, hipStream_t st) {
 	const int chunk = fused_chunk(g.sizes[1]);
 	dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0);
-	hipLaunchKernelGGL((k_fused_yz<BS, ZT>), grid, dim3(ZT), 0, st, in, out, g, ty, tz, x0,
-	                   chunk);
+	hipLaunchKernelGGL((k_fused_yz<BS, ZT>), grid, dim3(ZT), 0, st, in, out, g, ay, az, x0, chunk);
 }
 
 template <int BS>
-static bool launch_fused_bs(const double* in, double* out, const Geo& g, const AxisTable* ty,
-                            const AxisTable* tz, int x0, int x1, hipStream_t st) {
+static bool launch_fused_bs(const double* in, double* out, const Geo& g, const IsoAxis& ay,
+                            const IsoAxis& az, int x0, int x1, hipStream_t st) {
 	const int Z = g.sizes[2];
-	if (Z <= 64) launch_fused_t<BS, 64>(in, out, g, ty, tz, x0, x1, st);
-	else if (Z <= 128) launch_fused_t<BS, 128>(in, out, g, ty, tz, x0, x1, st);
-	else if (Z <= 256) launch_fused_t<BS, 256>(in, out, g, ty, tz, x0, x1, st);
-	else if (Z <= 512) launch_fused_t<BS, 512>(in, out, g, ty, tz, x0, x1, st);
-	else launch_fused_t<BS, 1024>(in, out, g, ty, tz, x0, x1, st);
+	if (Z <= 64) launch_fused_t<BS, 64>(in, out, g, ay, az, x0, x1, st);
+	else if (Z <= 128) launch_fused_t<BS, 128>(in, out, g, ay, az, x0, x1, st);
+	else if (Z <= 256) launch_fused_t<BS, 256>(in, out, g, ay, az, x0, x1, st);
+	else if (Z <= 512) launch_fused_t<BS, 512>(in, out, g, ay, az, x0, x1, st);
+	else launch_fused_t<BS, 1024>(in, out, g, ay, az, x0, x1, st);
 	return true;
 }
 
-bool launch_fused_yz(const double* in, double* out, const Geo& g, const AxisTable* ty,
-                     const AxisTable* tz, int x0, int x1, hipStream_t st) {
+bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis& ay,
+                     const IsoAxis& az, int x0, int x1, hipStream_t st) {
 	if (!fused_yz_supported(g) || x1 <= x0) return false;
 	switch (g.bs) {
-	case 1: return launch_fused_bs<1>(in, out, g, ty, tz, x0, x1, st);
-	case 2: return launch_fused_bs<2>(in, out, g, ty, tz, x0, x1, st);
-	case 3: return launch_fused_bs<3>(in, out, g, ty, tz, x0, x1, st);
+	case 1: return launch_fused_bs<1>(in, out, g, ay, az, x0, x1, st);
+	case 2: return launch_fused_bs<2>(in, out, g, ay, az, x0, x1, st);
+	case 3: return launch_fused_bs<3>(in, out, g, ay, az, x0, x1, st);
 	default: return false;
 	}
 }

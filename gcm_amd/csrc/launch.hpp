@@ -16,17 +16,24 @@ void launch_border_fill(double* cur, const Geo& g, int axis, int inner_sign, int
                         const int* nodes_d, int n_q, const int* qs_d, const double* vals_d,
                         hipStream_t st);
 
-// kernels_fast.hip -- 3-D, homogeneous, isotropic-elastic zero pattern.
-// `tab` points to the device AxisTable of material 0 for the stage's axis.
-// x range [x0, x1) of planes to update (slab scheduling); each returns false
-// when no compiled variant covers the configuration.
-bool iso_pattern_fits(int s, const double* U, const double* U1, const double* L);
-bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const AxisTable* tab,
+// kernels_fast.hip -- 3-D, homogeneous, structured isotropic-elastic matrices.
+// Per-axis values the fast kernels receive by value (kernel arguments, i.e.
+// scalar registers): the six material magnitudes of U / U1 and the Newton data
+// of the two distinct |eigenvalues| (c1: feet 0,1; c2: feet 2..5).
+struct IsoAxis {
+	double a, b, g;      // U:  sigma_ss of rows 0/1, sigma_ts of rows 2..5, sigma_ss of row 8
+	double p1, p2, s;    // U1: sigma_ss / sigma_tt of columns 0/1, sigma_st of columns 2..5
+	double c1[3], c2[3]; // ((q - i) + 1) / i, i = 1..bs
+	int kf1, kf2;        // floor(q)
+};
+bool iso_axis_extract(int s, const double* U, const double* U1, const double* L, IsoAxis& A);
+bool fast_layout_ok(const Geo& g);
+bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const IsoAxis& A,
                   int x0, int x1, hipStream_t st);
-bool launch_line_z(const double* cur, double* nxt, const Geo& g, const AxisTable* tab, int x0,
+bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& A, int x0,
                    int x1, hipStream_t st);
-bool launch_fused_yz(const double* in, double* out, const Geo& g, const AxisTable* ty,
-                     const AxisTable* tz, int x0, int x1, hipStream_t st);
+bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis& ay,
+                     const IsoAxis& az, int x0, int x1, hipStream_t st);
 bool fused_yz_supported(const Geo& g);
 
 }  // namespace gcmx
