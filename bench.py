@@ -67,6 +67,45 @@ def cpu_baseline(seconds: float):
                       f"({threads} OpenMP threads)"}
 
 
+def multi_gpu_parity(dist, world, rank, device, U, U1, L):
+    """N > 1 self-check of the RCCL X-slab path (halo exchange overlapped with the
+    interior X stage): 3 steps on a 12*N x 40 x 64 grid split into N slabs must
+    equal, bitwise, the same grid run whole on rank 0's GPU."""
+    import numpy as np
+    import torch
+    import gcm_amd
+    Xs, Y, Z, bs, seed = 12, 40, 64, 2, 0x5EED
+    Xg = Xs * world
+    c = gcm_amd.Context(3, bs, [Xs, Y, Z], start=[rank * Xs, 0, 0], device=device)
+    c.set_materials(U[None], U1[None], L[None])
+    c.fill_random([Xg, Y, Z], seed)
+    obj = [gcm_amd.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    c.comm_init(obj[0], world, rank, rank - 1 if rank > 0 else -1,
+                rank + 1 if rank < world - 1 else -1)
+    for _ in range(3):
+        c.step(0.9)
+    mine = c.download().reshape(Xs + 2 * bs, Y + 2 * bs, Z + 2 * bs, 9)[bs:-bs, bs:-bs, bs:-bs]
+    path = c.effective_path
+    c.close()
+    t = torch.from_numpy(np.ascontiguousarray(mine))
+    parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, parts, dst=0)
+    ok = True
+    if rank == 0:
+        f = gcm_amd.Context(3, bs, [Xg, Y, Z], device=device)
+        f.set_materials(U[None], U1[None], L[None])
+        f.fill_random([Xg, Y, Z], seed)
+        for _ in range(3):
+            f.step(0.9)
+        whole = f.download().reshape(Xg + 2 * bs, Y + 2 * bs, Z + 2 * bs, 9)[bs:-bs, bs:-bs, bs:-bs]
+        f.close()
+        ok = bool(np.array_equal(np.concatenate([p.numpy() for p in parts], axis=0), whole))
+    res = [ok]
+    dist.broadcast_object_list(res, src=0)
+    return {"ok": res[0], "grid": [Xg, Y, Z], "slabs": world, "steps": 3, "path": path}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -108,6 +147,10 @@ def main():
         ctx.comm_init(obj[0], world, rank, rank - 1 if rank > 0 else -1,
                       rank + 1 if rank < world - 1 else -1)
     ctx.sync()
+    parity = None
+    if world > 1:
+        parity = multi_gpu_parity(dist, world, rank, device, U, U1, L)
+        log(f"[rank {rank}] multi-GPU slab parity: {parity}")
     log(f"[rank {rank}] slab x[{x0},{x0 + X}) of {N}^3, {ctx.device_bytes / 1e9:.1f} GB, "
         f"path {ctx.effective_path}, setup {time.perf_counter() - t_setup:.1f}s")
 
@@ -202,6 +245,7 @@ def main():
             "effective_GBps_per_stage_model": round(step_bytes * a.steps / el / 1e9, 1),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "multi_gpu_parity": parity,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

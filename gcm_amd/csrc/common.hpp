@@ -52,13 +52,16 @@ struct AxisTable {
 // at the node and its BS neighbours on the foot side.  The Newton recurrence
 // is unrolled in the reference's order; the limiter bounds come from the
 // original values s[kf], s[kf+1].
-template <int BS>
+template <int BS, bool KF0 = false>
 __device__ __forceinline__ double newton_minmax(const double (&s)[BS + 1], int kf,
                                                 const double* __restrict__ coef) {
+	// KF0: the caller knows floor(q) == 0 for every foot of the launch (Courant < 1)
 	double lo = s[0], hi = s[1];
+	if constexpr (!KF0) {
 #pragma unroll
-	for (int i = 1; i < BS; i++)
-		if (kf == i) { lo = s[i]; hi = s[i + 1]; }
+		for (int i = 1; i < BS; i++)
+			if (kf == i) { lo = s[i]; hi = s[i + 1]; }
+	}
 	const double mx = fmax(lo, hi);
 	const double mn = fmin(lo, hi);
 	double d[BS + 1];

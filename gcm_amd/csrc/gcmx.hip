@@ -35,6 +35,7 @@ gcmx_status fail(gcmx_status s, const std::string& msg) {
 
 struct PendingTiming {
 	int bucket;
+	double bytes;
 	hipEvent_t a, b;
 };
 
@@ -42,7 +43,7 @@ struct Bucket {
 	std::string name;
 	double total_ms = 0;
 	long long launches = 0;
-	double bytes = 0;  // algorithmic bytes per launch (last launch)
+	double bytes = 0;  // algorithmic bytes summed over all timed launches
 };
 
 }  // namespace
@@ -73,6 +74,7 @@ struct gcmx_ctx {
 	// halo exchange
 	ncclComm_t comm = nullptr;
 	int nranks = 1, rank = 0, left = -1, right = -1;
+	bool halo_pending = false;     // an exchange is in flight on comm_stream (ev_halo)
 	std::vector<int> halo_comps;
 	// profiling
 	bool prof = false;
@@ -98,12 +100,13 @@ int bucket_id(gcmx_ctx* c, const char* name) {
 struct Timed {
 	gcmx_ctx* c;
 	int b;
+	double bytes;
 	hipEvent_t a = nullptr, e = nullptr;
 	hipStream_t st;
-	Timed(gcmx_ctx* c_, const char* name, double bytes, hipStream_t s) : c(c_), b(-1), st(s) {
+	Timed(gcmx_ctx* c_, const char* name, double bytes_, hipStream_t s)
+	    : c(c_), b(-1), bytes(bytes_), st(s) {
 		if (!c->prof) return;
 		b = bucket_id(c, name);
-		c->buckets[b].bytes = bytes;
 		hipEventCreate(&a);
 		hipEventCreate(&e);
 		hipEventRecord(a, st);
@@ -111,7 +114,7 @@ struct Timed {
 	~Timed() {
 		if (b < 0) return;
 		hipEventRecord(e, st);
-		c->pending.push_back({b, a, e});
+		c->pending.push_back({b, bytes, a, e});
 	}
 };
 
@@ -122,6 +125,7 @@ void drain_timings(gcmx_ctx* c) {
 		hipEventElapsedTime(&ms, p.a, p.b);
 		c->buckets[p.bucket].total_ms += ms;
 		c->buckets[p.bucket].launches += 1;
+		c->buckets[p.bucket].bytes += p.bytes;
 		hipEventDestroy(p.a);
 		hipEventDestroy(p.b);
 	}
@@ -221,7 +225,10 @@ void compute_halo_comps(gcmx_ctx* c) {
 	}
 }
 
-gcmx_status halo_exchange_impl(gcmx_ctx* c) {
+// Post the X-ghost exchange of the current layer on the comm stream (ordered
+// after all work issued so far on the compute stream).  Completion is marked
+// by ev_halo; consumers call halo_wait.
+gcmx_status halo_post(gcmx_ctx* c) {
 	if (!c->comm || (c->left < 0 && c->right < 0)) return GCMX_OK;
 	if (c->D < 2) return fail(GCMX_ERR_UNSUPPORTED, "X-slab halo needs dim >= 2");
 	if (c->halo_comps.empty()) return fail(GCMX_ERR_STATE, "materials not set");
@@ -252,8 +259,23 @@ gcmx_status halo_exchange_impl(gcmx_ctx* c) {
 	}
 	if (ncclGroupEnd() != ncclSuccess) return fail(GCMX_ERR_COMM, "ncclGroupEnd");
 	HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-	HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+	c->halo_pending = true;
 	return GCMX_OK;
+}
+
+gcmx_status halo_wait(gcmx_ctx* c) {
+	if (!c->halo_pending) return GCMX_OK;
+	HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+	c->halo_pending = false;
+	return GCMX_OK;
+}
+
+gcmx_status halo_exchange_impl(gcmx_ctx* c) {
+	gcmx_status s = halo_wait(c);  // an earlier exchange of this layer is still in flight
+	if (s) return s;
+	s = halo_post(c);
+	if (s) return s;
+	return halo_wait(c);
 }
 
 // Fast kernels: 3-D, one material, no per-node ids, isotropic zero pattern.
@@ -279,6 +301,8 @@ double node_stage_bytes(const gcmx_ctx* c) { return 2.0 * c->M * sizeof(double);
 
 gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	gcmx_status s = build_tables(c, tau);
+	if (s != GCMX_OK) return s;
+	s = halo_wait(c);
 	if (s != GCMX_OK) return s;
 	if (axis == 0 && c->comm) {
 		s = halo_exchange_impl(c);
@@ -530,6 +554,8 @@ static void soa_to_aos(const gcmx_ctx* c, const double* soa, double* aos) {
 gcmx_status gcmx_upload(gcmx_ctx* c, const double* aos) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
+	s = halo_wait(c);
+	if (s) return s;
 	if (!aos) return fail(GCMX_ERR_INVALID_ARG, "null host array");
 	std::vector<double> soa(c->layer_elems, 0.0);
 	aos_to_soa(c, aos, soa.data());
@@ -561,6 +587,8 @@ gcmx_status gcmx_upload(gcmx_ctx* c, const double* aos) {
 gcmx_status gcmx_download(gcmx_ctx* c, double* aos) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
+	s = halo_wait(c);
+	if (s) return s;
 	if (!aos) return fail(GCMX_ERR_INVALID_ARG, "null host array");
 	std::vector<double> soa(c->layer_elems);
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -571,6 +599,8 @@ gcmx_status gcmx_download(gcmx_ctx* c, double* aos) {
 
 gcmx_status gcmx_fill_random(gcmx_ctx* c, const int gs[3], uint64_t seed) {
 	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	s = halo_wait(c);
 	if (s) return s;
 	if (!gs) return fail(GCMX_ERR_INVALID_ARG, "null sizes");
 	const int D = c->D;
@@ -606,20 +636,45 @@ gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 		}
 		return GCMX_OK;
 	}
-	if (c->comm) {
-		s = halo_exchange_impl(c);
-		if (s) return s;
-	}
 	const Geo& g = c->geo;
-	const double bytes = node_stage_bytes(c) * (double)g.n_inner;
-	bool ok;
-	{
-		Timed t(c, "march_x", bytes, c->stream);
-		ok = launch_march(c->cur, c->nxt, g, 0, c->iso[0], 0, g.sizes[0], c->stream);
-	}
-	if (ok) {
-		Timed t(c, "fused_yz", bytes, c->stream);
-		ok = launch_fused_yz(c->nxt, c->cur, g, c->iso[1], c->iso[2], 0, g.sizes[0], c->stream);
+	const int X = g.sizes[0], bs = c->bs;
+	const double plane_bytes = node_stage_bytes(c) * (double)g.sizes[1] * g.sizes[2];
+	auto march = [&](int x0, int x1) {
+		Timed t(c, "march_x", plane_bytes * (x1 - x0), c->stream);
+		return launch_march(c->cur, c->nxt, g, 0, c->iso[0], x0, x1, c->stream);
+	};
+	auto fused = [&](int x0, int x1) {
+		Timed t(c, "fused_yz", plane_bytes * (x1 - x0), c->stream);
+		return launch_fused_yz(c->nxt, c->cur, g, c->iso[1], c->iso[2], x0, x1, c->stream);
+	};
+	const bool halo = c->comm && (c->left >= 0 || c->right >= 0);
+	bool ok = true;
+	if (halo && X >= 4 * bs) {
+		// Boundary planes first, exchange overlapped with interior work:
+		//   [E_n in flight] X-stage interior planes [bs, X-bs) need no ghosts;
+		//   wait E_n; X-stage boundary planes; Y/Z boundary planes; post E_{n+1}
+		//   (sends the new boundary planes, receives the next ghosts); Y/Z interior.
+		if (!c->halo_pending) {
+			s = halo_post(c);
+			if (s) return s;
+		}
+		ok = march(bs, X - bs);
+		if (ok) {
+			s = halo_wait(c);
+			if (s) return s;
+			ok = march(0, bs) && march(X - bs, X) && fused(0, bs) && fused(X - bs, X);
+		}
+		if (ok) {
+			s = halo_post(c);
+			if (s) return s;
+			ok = fused(bs, X - bs);
+		}
+	} else {
+		if (halo) {
+			s = halo_exchange_impl(c);
+			if (s) return s;
+		}
+		ok = march(0, X) && fused(0, X);
 	}
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
 	HIP_TRY(hipGetLastError());
@@ -660,6 +715,8 @@ gcmx_status gcmx_border_fill(gcmx_ctx* c, int axis, int side, int n_nodes, const
 		if (!ok) return fail(GCMX_ERR_INVALID_ARG, "quantity not in this PDE vector");
 	}
 	c->ghosts_touched = true;
+	s = halo_wait(c);
+	if (s) return s;
 	if (n_nodes == 0) return GCMX_OK;
 	const size_t need = (size_t)n_nodes * D;
 	HIP_TRY(hipStreamSynchronize(c->stream));  // scratch reuse
@@ -702,6 +759,7 @@ gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dmin[3], const int dmax[3], g
 			return fail(GCMX_ERR_INVALID_ARG, "box outside the grid");
 	}
 	dst->ghosts_touched = true;
+	if ((s = halo_wait(dst)) != GCMX_OK || (s = halo_wait(src)) != GCMX_OK) return s;
 	// order the copy after the source's pending work
 	HIP_TRY(hipEventRecord(src->ev_ready, src->stream));
 	HIP_TRY(hipStreamWaitEvent(dst->stream, src->ev_ready, 0));
@@ -762,6 +820,10 @@ gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n) {
 			if (!ok) return fail(GCMX_ERR_INVALID_ARG, "slabs are not X-adjacent");
 		}
 	}
+	for (int i = 0; i < n; i++) {
+		gcmx_status s = halo_wait(slabs[i]);
+		if (s) return s;
+	}
 	if (n == 1) return GCMX_OK;
 	gcmx_ctx* lead = slabs[0];
 	HIP_TRY(hipSetDevice(lead->device));
@@ -804,6 +866,7 @@ gcmx_status gcmx_sync(gcmx_ctx* c) {
 	if (s) return s;
 	HIP_TRY(hipStreamSynchronize(c->comm_stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	c->halo_pending = false;  // the comm stream has drained
 	drain_timings(c);
 	return GCMX_OK;
 }
@@ -832,7 +895,8 @@ int gcmx_profile_read(gcmx_ctx* c, int index, const char** name, double* total_m
 		if (name) *name = c->buckets[index].name.c_str();
 		if (total_ms) *total_ms = c->buckets[index].total_ms;
 		if (launches) *launches = c->buckets[index].launches;
-		if (bytes) *bytes = c->buckets[index].bytes;
+		if (bytes)
+			*bytes = c->buckets[index].launches ? c->buckets[index].bytes / c->buckets[index].launches : 0;
 	}
 	return n;
 }

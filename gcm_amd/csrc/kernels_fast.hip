@@ -195,7 +195,7 @@ struct RowSum {
 
 // One node's stage.  W(j, o): window component j at offset o along S
 // (|o| <= BS); C(j): node value of a component rows 6..8 read.
-template <int S, int BS, class WF, class CF>
+template <int S, int BS, bool KF0, class WF, class CF>
 __device__ __forceinline__ void node_update(const IsoAxis& A, WF W, CF C, double (&out)[9]) {
 	double r[9];
 #pragma unroll
@@ -207,7 +207,7 @@ __device__ __forceinline__ void node_update(const IsoAxis& A, WF W, CF C, double
 			double sv[BS + 1];
 #pragma unroll
 			for (int i = 0; i <= BS; i++) sv[i] = W(j, sh * i);
-			return newton_minmax<BS>(sv, kf, coef);
+			return newton_minmax<BS, KF0>(sv, kf, coef);
 		};
 		switch (k) {
 		case 0: r[0] = RowSum<S, false, 0>::go(A, interp, 0.0, true); break;
@@ -240,15 +240,37 @@ __device__ __forceinline__ void node_update(const IsoAxis& A, WF W, CF C, double
 struct Planes {
 	const double* __restrict__ p;
 	long long cs;
-	__device__ __forceinline__ double ld(int j, unsigned off) const { return p[j * cs + off]; }
+	__device__ __forceinline__ double ld(int j, unsigned off) const {
+		const char* b = reinterpret_cast<const char*>(p + j * cs);  // wave-uniform
+		return *reinterpret_cast<const double*>(b + (off << 3));    // 32-bit byte offset
+	}
 };
+__device__ __forceinline__ void st_plane(double* __restrict__ p, long long cs, int j, unsigned off,
+                                         double v) {
+	char* b = reinterpret_cast<char*>(p + j * cs);
+	*reinterpret_cast<double*>(b + (off << 3)) = v;
+}
 
 // ---------------------------------------------------------------- march --
 
 constexpr int kMarchThreads = 256;
+// Tuning knobs (compile-time; see scripts/tune.sh): minimum waves per SIMD the
+// register allocator must leave room for, and planes / rows per block chunk.
+#ifndef GCMX_MARCH_MINWAVES
+#define GCMX_MARCH_MINWAVES 4
+#endif
+#ifndef GCMX_MARCH_CHUNK
+#define GCMX_MARCH_CHUNK 64
+#endif
+#ifndef GCMX_FUSED_MINWAVES
+#define GCMX_FUSED_MINWAVES 4
+#endif
+#ifndef GCMX_FUSED_CHUNK
+#define GCMX_FUSED_CHUNK 64
+#endif
 
-template <int S, int BS>
-__global__ __launch_bounds__(kMarchThreads, 4) void k_march(const double* __restrict__ cur,
+template <int S, int BS, bool KF0>
+__global__ __launch_bounds__(kMarchThreads, GCMX_MARCH_MINWAVES) void k_march(const double* __restrict__ cur,
                                                          double* __restrict__ nxt, Geo g,
                                                          IsoAxis A, int m0, int m1, int chunk) {
 	constexpr unsigned WM = iso_window(S);
@@ -296,12 +318,12 @@ __global__ __launch_bounds__(kMarchThreads, 4) void k_march(const double* __rest
 			}
 		}
 		double out[9];
-		node_update<S, BS>(
+		node_update<S, BS, KF0>(
 		    A, [&](int j, int o) { return win[wslot(WM, j)][BS + o]; },
 		    [&](int j) { return ((WM >> j) & 1u) ? win[wslot(WM, j)][BS] : ctr[j]; }, out);
 		const unsigned offo = base + (unsigned)m * st;
 #pragma unroll
-		for (int c = 0; c < 9; c++) nxt[c * g.cs + offo] = out[c];
+		for (int c = 0; c < 9; c++) st_plane(nxt, g.cs, c, offo, out[c]);
 #pragma unroll
 		for (int q = 0; q < NW; q++)
 #pragma unroll
@@ -313,7 +335,7 @@ __global__ __launch_bounds__(kMarchThreads, 4) void k_march(const double* __rest
 
 constexpr int kLineThreads = 256;
 
-template <int BS>
+template <int BS, bool KF0>
 __global__ __launch_bounds__(kLineThreads) void k_line_z(const double* __restrict__ cur,
                                                          double* __restrict__ nxt, Geo g,
                                                          IsoAxis A, int x0) {
@@ -347,11 +369,11 @@ __global__ __launch_bounds__(kLineThreads) void k_line_z(const double* __restric
 	__syncthreads();
 	if (z >= Z) return;
 	double out[9];
-	node_update<S, BS>(
+	node_update<S, BS, KF0>(
 	    A, [&](int j, int o) { return lds[wslot(WM, j)][BS + tid + o]; },
 	    [&](int j) { return ((WM >> j) & 1u) ? lds[wslot(WM, j)][BS + tid] : ctr[j]; }, out);
 #pragma unroll
-	for (int c = 0; c < 9; c++) nxt[c * g.cs + row + z] = out[c];
+	for (int c = 0; c < 9; c++) st_plane(nxt, g.cs, c, row + z, out[c]);
 }
 
 // -------------------------------------------------------------- fused yz --
@@ -361,8 +383,8 @@ __global__ __launch_bounds__(kLineThreads) void k_line_z(const double* __restric
 // `outl`.  Precondition (the host only picks this path when it holds): every
 // y/z ghost of both layers is zero, so ghost rows and the Z stage's ghost
 // neighbours are the constant 0.0 instead of memory reads.
-template <int BS, int ZT>
-__global__ __launch_bounds__(ZT, (BS <= 2 ? 4 : 2)) void k_fused_yz(const double* __restrict__ in,
+template <int BS, int ZT, bool KF0>
+__global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fused_yz(const double* __restrict__ in,
                                                  double* __restrict__ outl, Geo g, IsoAxis AY,
                                                  IsoAxis AZ, int x0, int chunk) {
 	constexpr unsigned WMY = iso_window(1);
@@ -428,7 +450,7 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? 4 : 2)) void k_fused_yz(const double
 		}
 		// ---- Y stage at (x, y, z)
 		double yv[9];
-		node_update<1, BS>(
+		node_update<1, BS, KF0>(
 		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
 		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : ctr[j]; }, yv);
 		// ---- hand the row to the Z stage
@@ -440,13 +462,13 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? 4 : 2)) void k_fused_yz(const double
 		__syncthreads();
 		if (live) {
 			double zv[9];
-			node_update<2, BS>(
+			node_update<2, BS, KF0>(
 			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
 			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; },
 			    zv);
 			const unsigned offo = plane + (unsigned)y * st + z;
 #pragma unroll
-			for (int c = 0; c < 9; c++) outl[c * g.cs + offo] = zv[c];
+			for (int c = 0; c < 9; c++) st_plane(outl, g.cs, c, offo, zv[c]);
 		}
 		buf ^= 1;
 #pragma unroll
@@ -458,7 +480,7 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? 4 : 2)) void k_fused_yz(const double
 
 // ------------------------------------------------------------- launchers --
 
-static int march_chunk(int len) { return len < 128 ? len : 64; }
+static int march_chunk(int len) { return len < 2 * GCMX_MARCH_CHUNK ? len : GCMX_MARCH_CHUNK; }
 
 template <int BS>
 static void launch_march_bs(const double* cur, double* nxt, const Geo& g, int s,
@@ -468,8 +490,12 @@ static void launch_march_bs(const double* cur, double* nxt, const Geo& g, int s,
 		const int chunk = march_chunk(len);
 		dim3 grid((g.sizes[2] + kMarchThreads - 1) / kMarchThreads, g.sizes[1],
 		          (len + chunk - 1) / chunk);
-		hipLaunchKernelGGL((k_march<0, BS>), grid, dim3(kMarchThreads), 0, st, cur, nxt, g, A, x0,
-		                   x1, chunk);
+		if (A.kf1 == 0 && A.kf2 == 0)
+			hipLaunchKernelGGL((k_march<0, BS, true>), grid, dim3(kMarchThreads), 0, st, cur, nxt, g,
+			                   A, x0, x1, chunk);
+		else
+			hipLaunchKernelGGL((k_march<0, BS, false>), grid, dim3(kMarchThreads), 0, st, cur, nxt, g,
+			                   A, x0, x1, chunk);
 	} else {  // march along Y; threads cover x in [x0, x1)
 		const int len = g.sizes[1];
 		const int chunk = march_chunk(len);
@@ -477,8 +503,12 @@ static void launch_march_bs(const double* cur, double* nxt, const Geo& g, int s,
 		gg.origin = g.origin + (long long)x0 * g.stride[0];
 		dim3 grid((g.sizes[2] + kMarchThreads - 1) / kMarchThreads, x1 - x0,
 		          (len + chunk - 1) / chunk);
-		hipLaunchKernelGGL((k_march<1, BS>), grid, dim3(kMarchThreads), 0, st, cur, nxt, gg, A, 0,
-		                   len, chunk);
+		if (A.kf1 == 0 && A.kf2 == 0)
+			hipLaunchKernelGGL((k_march<1, BS, true>), grid, dim3(kMarchThreads), 0, st, cur, nxt, gg,
+			                   A, 0, len, chunk);
+		else
+			hipLaunchKernelGGL((k_march<1, BS, false>), grid, dim3(kMarchThreads), 0, st, cur, nxt, gg,
+			                   A, 0, len, chunk);
 	}
 }
 
@@ -501,7 +531,10 @@ template <int BS>
 static void launch_line_bs(const double* cur, double* nxt, const Geo& g, const IsoAxis& A,
                            int x0, int x1, hipStream_t st) {
 	dim3 grid((g.sizes[2] + kLineThreads - 1) / kLineThreads, g.sizes[1], x1 - x0);
-	hipLaunchKernelGGL((k_line_z<BS>), grid, dim3(kLineThreads), 0, st, cur, nxt, g, A, x0);
+	if (A.kf1 == 0 && A.kf2 == 0)
+		hipLaunchKernelGGL((k_line_z<BS, true>), grid, dim3(kLineThreads), 0, st, cur, nxt, g, A, x0);
+	else
+		hipLaunchKernelGGL((k_line_z<BS, false>), grid, dim3(kLineThreads), 0, st, cur, nxt, g, A, x0);
 }
 
 bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& A, int x0, int x1,
@@ -519,14 +552,19 @@ bool fused_yz_supported(const Geo& g) {
 	return fast_layout_ok(g) && g.sizes[2] <= 1024 && g.sizes[2] >= 2 * g.bs;
 }
 
-static int fused_chunk(int Y) { return Y <= 64 ? Y : 64; }
+static int fused_chunk(int Y) { return Y <= GCMX_FUSED_CHUNK ? Y : GCMX_FUSED_CHUNK; }
 
 template <int BS, int ZT>
 static void launch_fused_t(const double* in, double* out, const Geo& g, const IsoAxis& ay,
                            const IsoAxis& az, int x0, int x1, hipStream_t st) {
 	const int chunk = fused_chunk(g.sizes[1]);
 	dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0);
-	hipLaunchKernelGGL((k_fused_yz<BS, ZT>), grid, dim3(ZT), 0, st, in, out, g, ay, az, x0, chunk);
+	if (ay.kf1 == 0 && ay.kf2 == 0 && az.kf1 == 0 && az.kf2 == 0)
+		hipLaunchKernelGGL((k_fused_yz<BS, ZT, true>), grid, dim3(ZT), 0, st, in, out, g, ay, az, x0,
+		                   chunk);
+	else
+		hipLaunchKernelGGL((k_fused_yz<BS, ZT, false>), grid, dim3(ZT), 0, st, in, out, g, ay, az, x0,
+		                   chunk);
 }
 
 template <int BS>

@@ -14,6 +14,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libgcmx.so")
+# Tuning experiments only (scripts/tune.sh): load an alternative build.
+if os.environ.get("GCMX_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["GCMX_LIB"])
 
 # include/gcmx.h
 GCMX_OK = 0
