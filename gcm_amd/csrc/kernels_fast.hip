@@ -269,6 +269,7 @@ constexpr int kMarchThreads = 256;
 #define GCMX_FUSED_CHUNK 64
 #endif
 
+
 template <int S, int BS, bool KF0>
 __global__ __launch_bounds__(kMarchThreads, GCMX_MARCH_MINWAVES) void k_march(const double* __restrict__ cur,
                                                          double* __restrict__ nxt, Geo g,
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(kMarchThreads, GCMX_MARCH_MINWAVES) void k_march(co
 	const unsigned base = (unsigned)(g.origin + a * g.stride[OA] + z);
 	const Planes in{cur, g.cs};
 
-	double win[NW][W];  // window: slot BS + o holds plane m + o
+	double win[NW][W];
 	double pw[NW], pc[9], ctr[9];
 #pragma unroll
 	for (int j = 0; j < 9; j++) {
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(kMarchThreads, GCMX_MARCH_MINWAVES) void k_march(co
 			if ((WM >> j) & 1u) win[wslot(WM, j)][W - 1] = pw[wslot(WM, j)];
 			if ((CM >> j) & 1u) ctr[j] = pc[j];
 		}
-		if (m + 1 < me) {  // next iteration's loads go out before this node's math
+		if (m + 1 < me) {
 			const unsigned offw = base + (unsigned)(m + 1 + BS) * st;
 			const unsigned offc = base + (unsigned)(m + 1) * st;
 #pragma unroll
@@ -448,12 +449,10 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fus
 				if ((CMY >> j) & 1u) pc[j] = src.ld(j, base + (unsigned)(y + 1) * st);
 			}
 		}
-		// ---- Y stage at (x, y, z)
 		double yv[9];
 		node_update<1, BS, KF0>(
 		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
 		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : ctr[j]; }, yv);
-		// ---- hand the row to the Z stage
 		if (live) {
 #pragma unroll
 			for (int j = 0; j < 9; j++)
