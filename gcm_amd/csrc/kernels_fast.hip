@@ -423,7 +423,7 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fus
 	};
 
 	double win[NWY][W];
-	double pw[NWY], pc[9], ctr[9];
+	double pw[NWY], ctr[9];
 #pragma unroll
 	for (int j = 0; j < 9; j++) {
 		if (!((WMY >> j) & 1u)) continue;
@@ -431,23 +431,19 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fus
 		for (int o = 0; o < W - 1; o++) win[wslot(WMY, j)][o] = row_ld(j, yb - BS + o);
 		pw[wslot(WMY, j)] = row_ld(j, yb + BS);
 	}
-#pragma unroll
-	for (int j = 0; j < 9; j++)
-		if ((CMY >> j) & 1u) pc[j] = src.ld(j, base + (unsigned)yb * st);
 
 	int buf = 0;
 	for (int y = yb; y < ye; y++) {
 #pragma unroll
 		for (int j = 0; j < 9; j++) {
 			if ((WMY >> j) & 1u) win[wslot(WMY, j)][W - 1] = pw[wslot(WMY, j)];
-			if ((CMY >> j) & 1u) ctr[j] = pc[j];
+			// node-only components: loaded here, first used after the window rows
+			if ((CMY >> j) & 1u) ctr[j] = src.ld(j, base + (unsigned)y * st);
 		}
 		if (y + 1 < ye) {
 #pragma unroll
-			for (int j = 0; j < 9; j++) {
+			for (int j = 0; j < 9; j++)
 				if ((WMY >> j) & 1u) pw[wslot(WMY, j)] = row_ld(j, y + 1 + BS);
-				if ((CMY >> j) & 1u) pc[j] = src.ld(j, base + (unsigned)(y + 1) * st);
-			}
 		}
 		double yv[9];
 		node_update<1, BS, KF0>(

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Turn a scripts/gpu_profile.sh output directory into profiles/pmc_traffic.json:
+per-kernel HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (separate --pmc
+passes), corrected with the calibration stream of tools/calib_fetch.hip
+(MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of a coalesced stream)."""
+import collections
+import csv
+import json
+import sys
+
+
+def agg(path, counter):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in d.items()}
+
+
+def main(prof_dir, out, n=512):
+    f = agg(f"{prof_dir}/fetch/run_counter_collection.csv", "FETCH_SIZE")
+    w = agg(f"{prof_dir}/write/run_counter_collection.csv", "WRITE_SIZE")
+    cf = agg(f"{prof_dir}/calib_fetch/run_counter_collection.csv", "FETCH_SIZE")
+    cw = agg(f"{prof_dir}/calib_write/run_counter_collection.csv", "WRITE_SIZE")
+    true = 8 * (1 << 30)
+    r8 = [v for k, v in cf.items() if k.startswith("read8")][0] * 1024
+    w8 = [v for k, v in cw.items() if k.startswith("write8")][0] * 1024
+    ff, wf = true / r8, true / w8
+    alg = 144 * n ** 3
+    res = {"n": n, "ranks": 1, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, {prof_dir}",
+           "calibration": {"tool": "tools/calib_fetch.hip", "true_bytes": true,
+                           "read8_fetch_bytes": r8, "fetch_factor": ff,
+                           "write8_write_bytes": w8, "write_factor": wf},
+           "kernels": {}}
+    for short, frag in (("march_x", "k_march<0, 2"), ("fused_yz", "k_fused_yz<2, 512")):
+        fk = [v for k, v in f.items() if frag in k][0] * 1024 * ff
+        wk = [v for k, v in w.items() if frag in k][0] * 1024 * wf
+        res["kernels"][short] = {"fetch_bytes_per_launch": fk, "write_bytes_per_launch": wk,
+                                 "hbm_bytes_per_launch": fk + wk,
+                                 "algorithmic_bytes_per_launch": alg,
+                                 "traffic_over_algorithmic": (fk + wk) / alg}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res["kernels"], indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
