@@ -90,6 +90,26 @@ struct PyEngine {
 	}
 };
 
+/// buildHostState for body `id` of `task`, as numpy arrays shaped like the grid.
+template <int D>
+py::dict hostState(const Task& task, size_t id) {
+	cubic::CubicGrid<D> grid(id, cubic::constructionPack<D>(task, id));
+	auto st = cubic::buildHostState<D>(task, grid);
+	std::vector<ssize_t> shape;
+	for (int i = 0; i < D; i++) shape.push_back(grid.sizes[i] + 2 * grid.borderSize);
+	py::array_t<uint8_t> ids(shape);
+	std::copy(st.matId.begin(), st.matId.end(), ids.mutable_data());
+	shape.push_back(pdeSize(D));
+	py::array_t<real> pde(shape);
+	std::copy(st.pde.begin(), st.pde.end(), pde.mutable_data());
+	py::dict d;
+	d["pde"] = pde;
+	d["mat_ids"] = ids;
+	d["maximal_eigenvalue"] = st.maximalEigenvalue;
+	d["n_conditions"] = st.matrices.size();
+	return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_gcm_host, m) {
@@ -153,6 +173,18 @@ PYBIND11_MODULE(_gcm_host, m) {
 		         for (auto& kv : values) bc.values[quantity(kv.first)] = kv.second;
 		         t.cubicBorderConditions[body].push_back(bc);
 	         });
+
+	m.def(
+	    "host_state",
+	    [](const Task& t, size_t id) {
+		    const int D = t.globalSettings.dimensionality;
+		    if (D == 1) return hostState<1>(t, id);
+		    if (D == 2) return hostState<2>(t, id);
+		    if (D == 3) return hostState<3>(t, id);
+		    throw Exception("dimensionality must be 1, 2 or 3");
+	    },
+	    "GPU-free MaterialsCondition + InitialCondition set-up of one body", py::arg("task"),
+	    py::arg("body_id"));
 
 	py::class_<PyEngine>(m, "Engine")
 	    .def(py::init([](const Task& t, int device) {

@@ -136,12 +136,33 @@ HipMesh<D>::~HipMesh() {
 }
 
 template <int D>
-void HipMesh<D>::setUpPde(const Task& task) {
-	if (pdeIsSetUp) throw Exception("setUpPde called twice");
-	pdeIsSetUp = true;
-	const long long nAll = this->sizeOfAllNodes();
-	std::vector<real> pde((size_t)nAll * M, 0.0);
-	std::vector<uint8_t> matId((size_t)nAll, 0);
+typename CubicGrid<D>::ConstructionPack constructionPack(const Task& task, size_t id) {
+	typename CubicGrid<D>::ConstructionPack cp;
+	cp.borderSize = task.cubicGrid.borderSize;
+	if ((int)task.cubicGrid.h.size() != D) throw Exception("h has the wrong size");
+	const auto& cube = task.cubicGrid.cubics.at(id);
+	if ((int)cube.sizes.size() != D || (int)cube.start.size() != D)
+		throw Exception("cube sizes/start have the wrong size");
+	for (int i = 0; i < D; i++) {
+		cp.h[i] = task.cubicGrid.h[i];
+		cp.sizes[i] = cube.sizes[i];
+		cp.start[i] = cube.start[i];
+	}
+	return cp;
+}
+
+// DefaultMesh::setUpPde's host half (DefaultMesh.hpp:60-66): everything before
+// the data would be stored, without touching a GPU.
+template <int D>
+HostState<D> buildHostState(const Task& task, const CubicGrid<D>& grid) {
+	constexpr int M = pdeSize(D);
+	HostState<D> st;
+	const long long nAll = grid.sizeOfAllNodes();
+	st.pde.assign((size_t)nAll * M, 0.0);
+	st.matId.assign((size_t)nAll, 0);
+	auto& pde = st.pde;
+	auto& matId = st.matId;
+	auto& matrices = st.matrices;
 
 	// ---- MaterialsCondition::apply (util/task/MaterialsCondition.hpp:23-36, 70-91)
 	std::vector<std::pair<std::shared_ptr<Area>, std::shared_ptr<IsotropicMaterial>>> conds;
@@ -150,7 +171,7 @@ void HipMesh<D>::setUpPde(const Task& task) {
 		conds.push_back({std::make_shared<InfiniteArea>(), mc.byAreas.defaultMaterial});
 		for (const auto& m : mc.byAreas.materials) conds.push_back({m.area, m.material});
 	} else {
-		conds.push_back({std::make_shared<InfiniteArea>(), mc.byBodies.bodyMaterialMap.at(this->id)});
+		conds.push_back({std::make_shared<InfiniteArea>(), mc.byBodies.bodyMaterialMap.at(grid.id)});
 	}
 	if (conds.size() > 255) throw Exception("at most 255 material conditions per body");
 	matrices.assign(conds.size(), GcmMatrices<D>());
@@ -158,13 +179,14 @@ void HipMesh<D>::setUpPde(const Task& task) {
 		if (!conds[c].second) throw Exception("material condition without a material");
 		ElasticModel<D>::constructGcmMatrices(matrices[c], *conds[c].second);
 	}
-	forEachInner<D>(this->sizes, [&](const IntD& it) {
-		const Real3 x = this->coords(it);
+	forEachInner<D>(grid.sizes, [&](const std::array<int, D>& it) {
+		const Real3 x = grid.coords(it);
 		for (size_t c = 0; c < conds.size(); c++)
-			if (conds[c].first->contains(x)) matId[(size_t)this->getIndex(it)] = (uint8_t)c;
+			if (conds[c].first->contains(x)) matId[(size_t)grid.getIndex(it)] = (uint8_t)c;
 	});
-	maximalEigenvalue = 0;
-	for (const auto& m : matrices) maximalEigenvalue = std::fmax(maximalEigenvalue, m.getMaximalEigenvalue());
+	st.maximalEigenvalue = 0;
+	for (const auto& m : matrices)
+		st.maximalEigenvalue = std::fmax(st.maximalEigenvalue, m.getMaximalEigenvalue());
 
 	// ---- InitialCondition::apply (util/task/InitialCondition.hpp:23-88)
 	std::vector<std::pair<std::shared_ptr<Area>, std::array<real, M>>> ics;
@@ -194,14 +216,25 @@ void HipMesh<D>::setUpPde(const Task& task) {
 		setQuantity(D, q.physicalQuantity, q.value, tmp.data());
 		ics.push_back({q.area, tmp});
 	}
-	forEachInner<D>(this->sizes, [&](const IntD& it) {
-		const Real3 x = this->coords(it);
-		real* v = &pde[(size_t)this->getIndex(it) * M];
+	forEachInner<D>(grid.sizes, [&](const std::array<int, D>& it) {
+		const Real3 x = grid.coords(it);
+		real* v = &pde[(size_t)grid.getIndex(it) * M];
 		for (int c = 0; c < M; c++) v[c] = 0;
 		for (const auto& ic : ics)
 			if (ic.first->contains(x))
 				for (int c = 0; c < M; c++) v[c] += ic.second[c];
 	});
+	return st;
+}
+
+template <int D>
+void HipMesh<D>::setUpPde(const Task& task) {
+	if (pdeIsSetUp) throw Exception("setUpPde called twice");
+	pdeIsSetUp = true;
+	HostState<D> st = buildHostState<D>(task, *this);
+	matrices = st.matrices;
+	maximalEigenvalue = st.maximalEigenvalue;
+	auto& matId = st.matId;
 
 	// ---- device tables: only the materials the nodes actually use
 	std::vector<int> used(matrices.size(), 0);
@@ -225,7 +258,7 @@ void HipMesh<D>::setUpPde(const Task& task) {
 		for (auto& m : matId) m = (uint8_t)std::max(0, remap[m]);
 		gcmxCheck(gcmx_set_material_ids(ctx_, matId.data()), "gcmx_set_material_ids");
 	}
-	gcmxCheck(gcmx_upload(ctx_, pde.data()), "gcmx_upload");
+	gcmxCheck(gcmx_upload(ctx_, st.pde.data()), "gcmx_upload");
 }
 
 template <int D>
@@ -357,17 +390,7 @@ void Engine<D>::createGridsAndContacts(const Task& task) {
 			throw Exception("only isotropic elastic bodies are on this path");
 		Body body;
 		body.factory = std::make_shared<HipFactory<D>>(device);
-		typename Grid::ConstructionPack cp;
-		cp.borderSize = task.cubicGrid.borderSize;
-		if ((int)task.cubicGrid.h.size() != D) throw Exception("h has the wrong size");
-		const auto& cube = task.cubicGrid.cubics.at(tb.first);
-		if ((int)cube.sizes.size() != D || (int)cube.start.size() != D)
-			throw Exception("cube sizes/start have the wrong size");
-		for (int i = 0; i < D; i++) {
-			cp.h[i] = task.cubicGrid.h[i];
-			cp.sizes[i] = cube.sizes[i];
-			cp.start[i] = cube.start[i];
-		}
+		const auto cp = constructionPack<D>(task, tb.first);
 		body.mesh = body.factory->createMesh(task, tb.first, cp, 1);
 		bodies.push_back(body);
 	}
@@ -465,6 +488,12 @@ template class HipBorderConditions<3>;
 template class HipContactCopier<1>;
 template class HipContactCopier<2>;
 template class HipContactCopier<3>;
+template CubicGrid<1>::ConstructionPack constructionPack<1>(const Task&, size_t);
+template CubicGrid<2>::ConstructionPack constructionPack<2>(const Task&, size_t);
+template CubicGrid<3>::ConstructionPack constructionPack<3>(const Task&, size_t);
+template HostState<1> buildHostState<1>(const Task&, const CubicGrid<1>&);
+template HostState<2> buildHostState<2>(const Task&, const CubicGrid<2>&);
+template HostState<3> buildHostState<3>(const Task&, const CubicGrid<3>&);
 template class Engine<1>;
 template class Engine<2>;
 template class Engine<3>;

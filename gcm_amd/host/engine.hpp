@@ -114,6 +114,26 @@ public:
 	virtual void swapCurrAndNextPdeTimeLayer(int indexOfNextPde) = 0;
 };
 
+/// Host half of DefaultMesh::setUpPde (DefaultMesh.hpp:60-66): the PDE layer
+/// after MaterialsCondition::apply + InitialCondition::apply in the reference
+/// AoS all-nodes order, the material-condition index of every node (0 =
+/// default, i = i-th area condition) and the GcmMatrices per condition.
+/// No GPU involved; HipMesh::setUpPde uploads it.
+template <int D>
+struct HostState {
+	std::vector<real> pde;
+	std::vector<uint8_t> matId;
+	std::vector<GcmMatrices<D>> matrices;
+	real maximalEigenvalue = 0;
+};
+
+/// Engine::createGridsAndContacts's ConstructionPack for body `id` (Engine.cpp:38-60).
+template <int D>
+typename CubicGrid<D>::ConstructionPack constructionPack(const Task& task, size_t id);
+
+template <int D>
+HostState<D> buildHostState(const Task& task, const CubicGrid<D>& grid);
+
 /// DefaultMesh's role with GPU-resident storage: the context owns both time
 /// layers on the device; the host holds only set-up data.
 template <int D>
