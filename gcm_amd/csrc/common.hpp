@@ -47,6 +47,33 @@ struct AxisTable {
 	int pad_[kMaxM];
 };
 
+// v_max_f64 / v_min_f64 without the operand canonicalisation the compiler adds
+// in front of fmax/fmin for values it cannot prove canonical (loads, LDS).
+#ifndef GCMX_ASM_MINMAX
+#define GCMX_ASM_MINMAX 1
+#endif
+#ifndef GCMX_CLAMP_MINMAX
+#define GCMX_CLAMP_MINMAX 1
+#endif
+__device__ __forceinline__ double vmax(double a, double b) {
+#if GCMX_ASM_MINMAX
+	double r;
+	asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+	return r;
+#else
+	return fmax(a, b);
+#endif
+}
+__device__ __forceinline__ double vmin(double a, double b) {
+#if GCMX_ASM_MINMAX
+	double r;
+	asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+	return r;
+#else
+	return fmin(a, b);
+#endif
+}
+
 // EqualDistanceLineInterpolator::minMaxInterpolate for ONE component
 // (EqualDistanceLineInterpolator.hpp:18-43 + 56-71).  s[0..BS] are the values
 // at the node and its BS neighbours on the foot side.  The Newton recurrence
@@ -62,8 +89,8 @@ __device__ __forceinline__ double newton_minmax(const double (&s)[BS + 1], int k
 		for (int i = 1; i < BS; i++)
 			if (kf == i) { lo = s[i]; hi = s[i + 1]; }
 	}
-	const double mx = fmax(lo, hi);
-	const double mn = fmin(lo, hi);
+	const double mx = vmax(lo, hi);
+	const double mn = vmin(lo, hi);
 	double d[BS + 1];
 #pragma unroll
 	for (int i = 0; i <= BS; i++) d[i] = s[i];
@@ -75,8 +102,14 @@ __device__ __forceinline__ double newton_minmax(const double (&s)[BS + 1], int k
 		for (int j = 0; j <= BS - i; j++) d[j] = (d[j + 1] - d[j]) * c;
 		ans += d[0];
 	}
-	// if (ans > max) ans = max; else if (ans < min) ans = min;  as selects
+	// if (ans > max) ans = max; else if (ans < min) ans = min;
+	// == min(max(ans, mn), mx) for every non-NaN ans (mn <= mx); only the sign of
+	// an exact zero may differ.
+#if GCMX_CLAMP_MINMAX
+	return vmin(vmax(ans, mn), mx);
+#else
 	return (ans > mx) ? mx : ((ans < mn) ? mn : ans);
+#endif
 }
 
 // Same with compile-time coefficients held in registers by the caller.

@@ -623,6 +623,16 @@ gcmx_status gcmx_stage(gcmx_ctx* c, int axis, double tau) {
 	return stage_impl(c, axis, tau);
 }
 
+// GCMX_FUSED_XYZ=0 selects the two-pass fused schedule (march X + fused Y/Z);
+// default is the one-pass k_fused_xyz.
+static bool use_xyz() {
+	static const bool on = [] {
+		const char* e = std::getenv("GCMX_FUSED_XYZ");
+		return !(e && e[0] == '0');
+	}();
+	return on;
+}
+
 gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
@@ -649,6 +659,41 @@ gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 	};
 	const bool halo = c->comm && (c->left >= 0 || c->right >= 0);
 	bool ok = true;
+	if (use_xyz()) {
+		// One pass per step (cur -> nxt, then swap).  Ghost planes of `cur` must
+		// hold E_n; the exchange of the NEW boundary planes (E_{n+1}, into the
+		// ghost planes of `nxt`) runs while the interior planes are computed.
+		auto xyz = [&](int x0, int x1) {
+			Timed t(c, "fused_xyz", plane_bytes * (x1 - x0), c->stream);
+			return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, c->stream);
+		};
+		if (halo && X >= 4 * bs) {
+			if (!c->halo_pending) {
+				s = halo_post(c);
+				if (s) return s;
+			}
+			s = halo_wait(c);
+			if (s) return s;
+			ok = xyz(0, bs) && xyz(X - bs, X);
+			if (ok) {
+				std::swap(c->cur, c->nxt);  // E_{n+1} exchanges the new layer
+				s = halo_post(c);
+				std::swap(c->cur, c->nxt);
+				if (s) return s;
+				ok = xyz(bs, X - bs);
+			}
+		} else {
+			if (halo) {
+				s = halo_exchange_impl(c);
+				if (s) return s;
+			}
+			ok = xyz(0, X);
+		}
+		if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
+		HIP_TRY(hipGetLastError());
+		std::swap(c->cur, c->nxt);
+		return GCMX_OK;
+	}
 	if (halo && X >= 4 * bs) {
 		// Boundary planes first, exchange overlapped with interior work:
 		//   [E_n in flight] X-stage interior planes [bs, X-bs) need no ghosts;

@@ -235,21 +235,51 @@ __device__ __forceinline__ void node_update(const IsoAxis& A, WF W, CF C, double
 }
 
 // Per-component plane base pointers are uniform; per-thread offsets are 32-bit
-// element indices (layer planes are < 2^29 elements, checked on the host), so
-// the loads use the scalar-base + 32-bit-offset addressing form.
+// element indices (layer planes are < 2^29 elements, checked on the host).  The
+// nine bases are made opaque SGPR values once per kernel so that every access
+// is the scalar-base + 32-bit-VGPR-offset form (one shared offset register, no
+// 64-bit address arithmetic per component).
+typedef const __attribute__((address_space(1))) double* gcptr;
+typedef __attribute__((address_space(1))) double* gptr;
+#ifndef GCMX_SGPR_BASES
+#define GCMX_SGPR_BASES 1
+#endif
+__device__ __forceinline__ gcptr sgpr_ptr(const double* p) {
+	gcptr q = (gcptr)p;
+#if GCMX_SGPR_BASES
+	asm volatile("" : "+s"(q));
+#endif
+	return q;
+}
+__device__ __forceinline__ gptr sgpr_ptr(double* p) {
+	gptr q = (gptr)p;
+#if GCMX_SGPR_BASES
+	asm volatile("" : "+s"(q));
+#endif
+	return q;
+}
 struct Planes {
-	const double* __restrict__ p;
-	long long cs;
+	gcptr b[kMaxM];
+	__device__ __forceinline__ Planes(const double* p, long long cs) {
+#pragma unroll
+		for (int j = 0; j < kMaxM; j++) b[j] = sgpr_ptr(p + j * cs);
+	}
 	__device__ __forceinline__ double ld(int j, unsigned off) const {
-		const char* b = reinterpret_cast<const char*>(p + j * cs);  // wave-uniform
-		return *reinterpret_cast<const double*>(b + (off << 3));    // 32-bit byte offset
+		typedef const __attribute__((address_space(1))) char* gcb;
+		return *reinterpret_cast<gcptr>(reinterpret_cast<gcb>(b[j]) + (size_t)(off << 3));
 	}
 };
-__device__ __forceinline__ void st_plane(double* __restrict__ p, long long cs, int j, unsigned off,
-                                         double v) {
-	char* b = reinterpret_cast<char*>(p + j * cs);
-	*reinterpret_cast<double*>(b + (off << 3)) = v;
-}
+struct PlanesW {
+	gptr b[kMaxM];
+	__device__ __forceinline__ PlanesW(double* p, long long cs) {
+#pragma unroll
+		for (int j = 0; j < kMaxM; j++) b[j] = sgpr_ptr(p + j * cs);
+	}
+	__device__ __forceinline__ void st(int j, unsigned off, double v) const {
+		typedef __attribute__((address_space(1))) char* gb;
+		*reinterpret_cast<gptr>(reinterpret_cast<gb>(b[j]) + (size_t)(off << 3)) = v;
+	}
+};
 
 // ---------------------------------------------------------------- march --
 
@@ -287,7 +317,8 @@ __global__ __launch_bounds__(kMarchThreads, GCMX_MARCH_MINWAVES) void k_march(co
 	if (z >= g.sizes[2]) return;
 	const unsigned st = (unsigned)g.stride[S];
 	const unsigned base = (unsigned)(g.origin + a * g.stride[OA] + z);
-	const Planes in{cur, g.cs};
+	const Planes in(cur, g.cs);
+	const PlanesW out_p(nxt, g.cs);
 
 	double win[NW][W];
 	double pw[NW], pc[9], ctr[9];
@@ -324,7 +355,7 @@ __global__ __launch_bounds__(kMarchThreads, GCMX_MARCH_MINWAVES) void k_march(co
 		    [&](int j) { return ((WM >> j) & 1u) ? win[wslot(WM, j)][BS] : ctr[j]; }, out);
 		const unsigned offo = base + (unsigned)m * st;
 #pragma unroll
-		for (int c = 0; c < 9; c++) st_plane(nxt, g.cs, c, offo, out[c]);
+		for (int c = 0; c < 9; c++) out_p.st(c, offo, out[c]);
 #pragma unroll
 		for (int q = 0; q < NW; q++)
 #pragma unroll
@@ -353,7 +384,8 @@ __global__ __launch_bounds__(kLineThreads) void k_line_z(const double* __restric
 	const int tid = threadIdx.x;
 	const int Z = g.sizes[2];
 	const unsigned row = (unsigned)(g.origin + x * g.stride[0] + y * g.stride[1]);
-	const Planes in{cur, g.cs};
+	const Planes in(cur, g.cs);
+	const PlanesW out_p(nxt, g.cs);
 	for (int i = tid; i < LW; i += kLineThreads) {
 		const int zz = z0 - BS + i;
 		if (zz < Z + BS) {
@@ -374,7 +406,7 @@ __global__ __launch_bounds__(kLineThreads) void k_line_z(const double* __restric
 	    A, [&](int j, int o) { return lds[wslot(WM, j)][BS + tid + o]; },
 	    [&](int j) { return ((WM >> j) & 1u) ? lds[wslot(WM, j)][BS + tid] : ctr[j]; }, out);
 #pragma unroll
-	for (int c = 0; c < 9; c++) st_plane(nxt, g.cs, c, row + z, out[c]);
+	for (int c = 0; c < 9; c++) out_p.st(c, row + z, out[c]);
 }
 
 // -------------------------------------------------------------- fused yz --
@@ -407,7 +439,8 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fus
 	const unsigned st = (unsigned)g.stride[1];
 	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
 	const unsigned base = plane + zc;
-	const Planes src{in, g.cs};
+	const Planes src(in, g.cs);
+	const PlanesW out_p(outl, g.cs);
 
 	// zero ghost slots of both LDS row buffers once (never overwritten)
 	if (z < 2 * BS) {
@@ -463,13 +496,188 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fus
 			    zv);
 			const unsigned offo = plane + (unsigned)y * st + z;
 #pragma unroll
-			for (int c = 0; c < 9; c++) st_plane(outl, g.cs, c, offo, zv[c]);
+			for (int c = 0; c < 9; c++) out_p.st(c, offo, zv[c]);
 		}
 		buf ^= 1;
 #pragma unroll
 		for (int q = 0; q < NWY; q++)
 #pragma unroll
 			for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
+	}
+}
+
+// ------------------------------------------------------------- fused xyz --
+
+// The whole time step in ONE pass (X stage, then Y, then Z, as
+// Engine::nextTimeStep orders them, Engine.cpp:90-121): block = one x plane, a
+// chunk of y rows and the whole z row.  Each thread marches y; at row y it
+//   * computes the X stage of row y+BS straight from the input layer (its
+//     2*BS+1 x-neighbours are plain loads; the neighbouring planes' blocks read
+//     the same lines, so they come from L2 / Infinity Cache, not HBM),
+//   * pushes that X result into a register window of 2*BS+1 rows and runs the
+//     Y stage of row y,
+//   * hands the Y result to the Z stage through double-buffered LDS.
+// HBM traffic: the input layer once, the output layer once (144 B/node/step).
+// Reads `in` (all components, x ghost planes valid), writes `outl`.
+// Precondition as k_fused_yz: every y/z ghost of both layers is zero, so the
+// intermediate results at ghost rows / columns are the constant 0.0.
+#ifndef GCMX_XYZ_MINWAVES
+#define GCMX_XYZ_MINWAVES 2
+#endif
+#ifndef GCMX_XYZ_CHUNK
+#define GCMX_XYZ_CHUNK 64
+#endif
+#ifndef GCMX_XYZ_PREFETCH
+#define GCMX_XYZ_PREFETCH 1
+#endif
+
+template <int BS, int ZT, bool KF0>
+__global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
+    const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY,
+    IsoAxis AZ, int x0, int chunk) {
+	constexpr unsigned WMX = iso_window(0);
+	constexpr unsigned CMX = iso_center_only(0);
+	constexpr int NWX = popc9(WMX);
+	constexpr unsigned WMY = iso_window(1);
+	constexpr unsigned CMY = iso_center_only(1);
+	constexpr int NWY = popc9(WMY);
+	constexpr int NCY = popc9(CMY);
+	constexpr unsigned WMZ = iso_window(2);
+	constexpr int NWZ = popc9(WMZ);
+	constexpr int W = 2 * BS + 1;
+	constexpr int LW = ZT + 2 * BS;
+	__shared__ double lds[2][NWZ][LW];
+
+	const int z = threadIdx.x;
+	const int x = x0 + blockIdx.y;
+	const int Y = g.sizes[1], Z = g.sizes[2];
+	const int yb = blockIdx.x * chunk;
+	const int ye = min(yb + chunk, Y);
+	const bool live = z < Z;
+	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
+	const unsigned stx = (unsigned)g.stride[0];
+	const unsigned sty = (unsigned)g.stride[1];
+	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
+	const unsigned base = plane + zc;
+	const Planes src(in, g.cs);
+	const PlanesW out_p(outl, g.cs);
+
+	if (z < 2 * BS) {  // ghost slots of both LDS row buffers: zero, never overwritten
+		const int gslot = (z < BS) ? z : (Z + z);
+#pragma unroll
+		for (int q = 0; q < NWZ; q++) {
+			lds[0][q][gslot] = 0.0;
+			lds[1][q][gslot] = 0.0;
+		}
+	}
+
+	// X-stage input of one row: window components at x-BS..x+BS, the rest at x
+	struct XIn {
+		double w[NWX][W];
+		double c[9];
+	};
+	auto x_load = [&](XIn& v, int r) {
+		const unsigned o = base + (unsigned)r * sty;
+#pragma unroll
+		for (int j = 0; j < 9; j++) {
+			if ((WMX >> j) & 1u) {
+#pragma unroll
+				for (int k = 0; k < W; k++) v.w[wslot(WMX, j)][k] = src.ld(j, o + (unsigned)(k - BS) * stx);
+			}
+			if ((CMX >> j) & 1u) v.c[j] = src.ld(j, o);
+		}
+	};
+	auto x_stage = [&](const XIn& v, double (&xr)[9]) {
+		node_update<0, BS, KF0>(
+		    AX, [&](int j, int o) { return v.w[wslot(WMX, j)][BS + o]; },
+		    [&](int j) { return ((WMX >> j) & 1u) ? v.w[wslot(WMX, j)][BS] : v.c[j]; }, xr);
+	};
+	auto in_rows = [&](int r) { return r >= 0 && r < Y; };
+
+	// Y window over X results of rows y-BS..y+BS; node-only components of rows
+	// y..y+BS wait in a small delay line.
+	double win[NWY][W];
+	double cen[BS + 1][NCY > 0 ? NCY : 1];
+	auto push = [&](const double (&xr)[9], int slot) {  // slot: window index of the row
+#pragma unroll
+		for (int j = 0; j < 9; j++) {
+			if ((WMY >> j) & 1u) win[wslot(WMY, j)][slot] = xr[j];
+			if ((CMY >> j) & 1u) {
+				if (slot >= BS) cen[slot - BS][wslot(CMY, j)] = xr[j];
+			}
+		}
+	};
+	// prologue: X results of rows yb-BS .. yb+BS-1
+#pragma unroll
+	for (int k = 0; k < W - 1; k++) {
+		const int r = yb - BS + k;
+		double xr[9];
+		if (in_rows(r)) {
+			XIn v;
+			x_load(v, r);
+			x_stage(v, xr);
+		} else {
+#pragma unroll
+			for (int j = 0; j < 9; j++) xr[j] = 0.0;
+		}
+		push(xr, k);
+	}
+#if GCMX_XYZ_PREFETCH
+	XIn nxt_in;
+	if (in_rows(yb + BS)) x_load(nxt_in, yb + BS);
+#endif
+
+	int buf = 0;
+	for (int y = yb; y < ye; y++) {
+		{  // X stage of row y+BS -> window slot W-1
+			const int r = y + BS;
+			double xr[9];
+			if (in_rows(r)) {
+#if GCMX_XYZ_PREFETCH
+				x_stage(nxt_in, xr);
+#else
+				XIn v;
+				x_load(v, r);
+				x_stage(v, xr);
+#endif
+			} else {
+#pragma unroll
+				for (int j = 0; j < 9; j++) xr[j] = 0.0;
+			}
+			push(xr, W - 1);
+#if GCMX_XYZ_PREFETCH
+			if (y + 1 < ye && in_rows(r + 1)) x_load(nxt_in, r + 1);
+#endif
+		}
+		double yv[9];
+		node_update<1, BS, KF0>(
+		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
+		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : cen[0][wslot(CMY, j)]; },
+		    yv);
+		if (live) {
+#pragma unroll
+			for (int j = 0; j < 9; j++)
+				if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = yv[j];
+		}
+		__syncthreads();
+		if (live) {
+			double zv[9];
+			node_update<2, BS, KF0>(
+			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
+			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
+			const unsigned offo = plane + (unsigned)y * sty + z;
+#pragma unroll
+			for (int c = 0; c < 9; c++) out_p.st(c, offo, zv[c]);
+		}
+		buf ^= 1;
+#pragma unroll
+		for (int q = 0; q < NWY; q++)
+#pragma unroll
+			for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
+#pragma unroll
+		for (int k = 0; k < BS; k++)
+#pragma unroll
+			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
 	}
 }
 
@@ -572,6 +780,46 @@ static bool launch_fused_bs(const double* in, double* out, const Geo& g, const I
 	else if (Z <= 512) launch_fused_t<BS, 512>(in, out, g, ay, az, x0, x1, st);
 	else launch_fused_t<BS, 1024>(in, out, g, ay, az, x0, x1, st);
 	return true;
+}
+
+static int xyz_chunk(int Y) { return Y <= GCMX_XYZ_CHUNK ? Y : GCMX_XYZ_CHUNK; }
+
+template <int BS, int ZT>
+static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                         int x1, hipStream_t st) {
+	const int chunk = xyz_chunk(g.sizes[1]);
+	dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0);
+	bool kf0 = true;
+	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
+	if (kf0)
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk);
+	else
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, false>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk);
+}
+
+template <int BS>
+static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                          int x1, hipStream_t st) {
+	const int Z = g.sizes[2];
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st);
+	return true;
+}
+
+bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                      int x1, hipStream_t st) {
+	if (!fused_yz_supported(g) || x1 <= x0) return false;
+	switch (g.bs) {
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st);
+	default: return false;
+	}
 }
 
 bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis& ay,

@@ -35,5 +35,8 @@ bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& 
 bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis& ay,
                      const IsoAxis& az, int x0, int x1, hipStream_t st);
 bool fused_yz_supported(const Geo& g);
+// One pass per time step: X, Y, Z stages of planes [x0, x1), `a` = the three axes.
+bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                      int x1, hipStream_t st);
 
 }  // namespace gcmx
