@@ -20,11 +20,15 @@ def agg(path, counter):
 def main(prof_dir, out, n=512):
     f = agg(f"{prof_dir}/fetch/run_counter_collection.csv", "FETCH_SIZE")
     w = agg(f"{prof_dir}/write/run_counter_collection.csv", "WRITE_SIZE")
-    cf = agg(f"{prof_dir}/calib_fetch/run_counter_collection.csv", "FETCH_SIZE")
-    cw = agg(f"{prof_dir}/calib_write/run_counter_collection.csv", "WRITE_SIZE")
     true = 8 * (1 << 30)
-    r8 = [v for k, v in cf.items() if k.startswith("read8")][0] * 1024
-    w8 = [v for k, v in cw.items() if k.startswith("write8")][0] * 1024
+    try:
+        cf = agg(f"{prof_dir}/calib_fetch/run_counter_collection.csv", "FETCH_SIZE")
+        cw = agg(f"{prof_dir}/calib_write/run_counter_collection.csv", "WRITE_SIZE")
+        r8 = [v for k, v in cf.items() if k.startswith("read8")][0] * 1024
+        w8 = [v for k, v in cw.items() if k.startswith("write8")][0] * 1024
+    except (FileNotFoundError, IndexError):  # reuse the stored calibration run
+        old = json.load(open(out))["calibration"]
+        r8, w8 = old["read8_fetch_bytes"], old["write8_write_bytes"]
     ff, wf = true / r8, true / w8
     alg = 144 * n ** 3
     res = {"n": n, "ranks": 1, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, {prof_dir}",
@@ -32,9 +36,14 @@ def main(prof_dir, out, n=512):
                            "read8_fetch_bytes": r8, "fetch_factor": ff,
                            "write8_write_bytes": w8, "write_factor": wf},
            "kernels": {}}
-    for short, frag in (("march_x", "k_march<0, 2"), ("fused_yz", "k_fused_yz<2, 512")):
-        fk = [v for k, v in f.items() if frag in k][0] * 1024 * ff
-        wk = [v for k, v in w.items() if frag in k][0] * 1024 * wf
+    for short, frag in (("march_x", "k_march<0, 2"), ("fused_yz", "k_fused_yz<2, 512"),
+                        ("fused_xyz", "k_fused_xyz<2, 512")):
+        fks = [v for k, v in f.items() if frag in k]
+        wks = [v for k, v in w.items() if frag in k]
+        if not fks or not wks:
+            continue
+        fk = fks[0] * 1024 * ff
+        wk = wks[0] * 1024 * wf
         res["kernels"][short] = {"fetch_bytes_per_launch": fk, "write_bytes_per_launch": wk,
                                  "hbm_bytes_per_launch": fk + wk,
                                  "algorithmic_bytes_per_launch": alg,
