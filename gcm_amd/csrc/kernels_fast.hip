@@ -27,95 +27,10 @@
 //                 x plane, a chunk of y rows and the whole z row, marches y (ring
 //                 window), hands each Y-stage row to the Z stage through
 //                 double-buffered LDS and writes only the Z result.
-#include "common.hpp"
-#include "launch.hpp"
+#include "iso.hpp"
 
 namespace gcmx {
 
-// ----------------------------------------------------------- structure --
-
-// Index of sigma(i,j) in the 3-D PDE vector (VelocitySigmaVariables.hpp:82-96).
-__host__ __device__ constexpr int sig3(int i, int j) {
-	return (i <= j) ? 3 + (i * 3 - ((i - 1) * i) / 2 + j - i)
-	                : 3 + (j * 3 - ((j - 1) * j) / 2 + i - j);
-}
-__host__ __device__ constexpr unsigned bit(int i) { return 1u << i; }
-
-// createLocalBasis(e_s) (linal/basis.hpp:58-65, geometry.hpp:35-52): the two
-// tangents are +-e_t1, +-e_t2 with these axes and signs.
-__host__ __device__ constexpr int tang1(int s) { return s == 0 ? 1 : 0; }
-__host__ __device__ constexpr int tang2(int s) { return s == 2 ? 1 : 2; }
-__host__ __device__ constexpr int sgn1(int s) { return s == 0 ? -1 : 1; }
-__host__ __device__ constexpr int sgn2(int s) { return s == 2 ? 1 : -1; }
-
-// A matrix entry: `sign * (slot value or constant)`.
-enum Slot : int { kZero = 0, kOne, kHalf, kA, kB, kG, kP1, kP2, kS };
-struct Coef {
-	int slot;
-	int sign;
-};
-__host__ __device__ constexpr Coef cz() { return Coef{kZero, 0}; }
-
-// U(k, j) (ElasticModel.hpp:486-553): rows are eigenstrings.
-__host__ __device__ constexpr Coef iso_u(int S, int k, int j) {
-	const int t1 = tang1(S), t2 = tang2(S), s1 = sgn1(S), s2 = sgn2(S);
-	const int ss = sig3(S, S), st1 = sig3(t1, S), st2 = sig3(t2, S);
-	const int s11 = sig3(t1, t1), s22 = sig3(t2, t2), s12 = sig3(t1, t2);
-	return (k == 0) ? (j == S ? Coef{kOne, 1} : j == ss ? Coef{kA, 1} : cz())
-	     : (k == 1) ? (j == S ? Coef{kOne, 1} : j == ss ? Coef{kA, -1} : cz())
-	     : (k == 2) ? (j == t1 ? Coef{kOne, s1} : j == st1 ? Coef{kB, s1} : cz())
-	     : (k == 3) ? (j == t1 ? Coef{kOne, s1} : j == st1 ? Coef{kB, -s1} : cz())
-	     : (k == 4) ? (j == t2 ? Coef{kOne, s2} : j == st2 ? Coef{kB, s2} : cz())
-	     : (k == 5) ? (j == t2 ? Coef{kOne, s2} : j == st2 ? Coef{kB, -s2} : cz())
-	     : (k == 6) ? (j == s12 ? Coef{kOne, s1 * s2} : cz())
-	     : (k == 7) ? (j == s11 ? Coef{kOne, 1} : j == s22 ? Coef{kOne, -1} : cz())
-	                : (j == s11 ? Coef{kOne, 1} : j == s22 ? Coef{kOne, 1}
-	                   : j == ss ? Coef{kG, 1} : cz());
-}
-
-// U1(c, n) (ElasticModel.hpp:416-483): columns are eigenvectors.
-__host__ __device__ constexpr Coef iso_u1(int S, int c, int n) {
-	const int t1 = tang1(S), t2 = tang2(S), s1 = sgn1(S), s2 = sgn2(S);
-	const int ss = sig3(S, S), st1 = sig3(t1, S), st2 = sig3(t2, S);
-	const int s11 = sig3(t1, t1), s22 = sig3(t2, t2), s12 = sig3(t1, t2);
-	return (n == 0) ? (c == S ? Coef{kHalf, 1} : c == ss ? Coef{kP1, 1}
-	                   : (c == s11 || c == s22) ? Coef{kP2, 1} : cz())
-	     : (n == 1) ? (c == S ? Coef{kHalf, 1} : c == ss ? Coef{kP1, -1}
-	                   : (c == s11 || c == s22) ? Coef{kP2, -1} : cz())
-	     : (n == 2) ? (c == t1 ? Coef{kHalf, s1} : c == st1 ? Coef{kS, s1} : cz())
-	     : (n == 3) ? (c == t1 ? Coef{kHalf, s1} : c == st1 ? Coef{kS, -s1} : cz())
-	     : (n == 4) ? (c == t2 ? Coef{kHalf, s2} : c == st2 ? Coef{kS, s2} : cz())
-	     : (n == 5) ? (c == t2 ? Coef{kHalf, s2} : c == st2 ? Coef{kS, -s2} : cz())
-	     : (n == 6) ? (c == s12 ? Coef{kOne, s1 * s2} : cz())
-	     : (n == 7) ? (c == s11 ? Coef{kHalf, 1} : c == s22 ? Coef{kHalf, -1} : cz())
-	                : (c == s11 ? Coef{kHalf, 1} : c == s22 ? Coef{kHalf, 1} : cz());
-}
-
-// Components read at the neighbours (rows 0..5) / only at the node (rows 6..8).
-__host__ __device__ constexpr unsigned iso_window(int S) {
-	unsigned m = 0;
-	for (int k = 0; k < 6; k++)
-		for (int j = 0; j < 9; j++)
-			if (iso_u(S, k, j).slot != kZero) m |= bit(j);
-	return m;
-}
-__host__ __device__ constexpr unsigned iso_center_only(int S) {
-	unsigned m = 0;
-	for (int k = 6; k < 9; k++)
-		for (int j = 0; j < 9; j++)
-			if (iso_u(S, k, j).slot != kZero) m |= bit(j);
-	return m & ~iso_window(S);
-}
-__host__ __device__ constexpr int wslot(unsigned mask, int j) {
-	int n = 0;
-	for (int i = 0; i < j; i++) n += (mask >> i) & 1u;
-	return n;
-}
-__host__ __device__ constexpr int popc9(unsigned m) {
-	int n = 0;
-	for (int i = 0; i < 9; i++) n += (m >> i) & 1u;
-	return n;
-}
 
 static double slot_value(const IsoAxis& A, int slot) {
 	switch (slot) {
@@ -157,129 +72,6 @@ bool iso_axis_extract(int S, const double* U, const double* U1, const double* L,
 		return false;
 	return true;
 }
-
-// u * v for a structural entry; exact w.r.t. the reference product fl(u * v).
-template <int SLOT, int SIGN>
-__device__ __forceinline__ double term(const IsoAxis& A, double v) {
-	double m;
-	if constexpr (SLOT == kOne) m = v;
-	else if constexpr (SLOT == kHalf) m = v * 0.5;
-	else if constexpr (SLOT == kA) m = A.a * v;
-	else if constexpr (SLOT == kB) m = A.b * v;
-	else if constexpr (SLOT == kG) m = A.g * v;
-	else if constexpr (SLOT == kP1) m = A.p1 * v;
-	else if constexpr (SLOT == kP2) m = A.p2 * v;
-	else m = A.s * v;
-	return SIGN > 0 ? m : -m;
-}
-
-// Unrolled sum over j of U(k, j) * V(j) (or U1(c, n) * r(n)) in ascending index
-// order, skipping structural zeros, starting from the first non-zero term.
-template <int S, bool ISU1, int ROW, int J = 0>
-struct RowSum {
-	template <class F>
-	__device__ __forceinline__ static double go(const IsoAxis& A, F val, double acc, bool first) {
-		if constexpr (J == 9) {
-			return acc;
-		} else {
-			constexpr Coef c = ISU1 ? iso_u1(S, ROW, J) : iso_u(S, ROW, J);
-			if constexpr (c.slot == kZero) {
-				return RowSum<S, ISU1, ROW, J + 1>::go(A, val, acc, first);
-			} else {
-				const double t = term<c.slot, c.sign>(A, val(J));
-				return RowSum<S, ISU1, ROW, J + 1>::go(A, val, first ? t : acc + t, false);
-			}
-		}
-	}
-};
-
-// One node's stage.  W(j, o): window component j at offset o along S
-// (|o| <= BS); C(j): node value of a component rows 6..8 read.
-template <int S, int BS, bool KF0, class WF, class CF>
-__device__ __forceinline__ void node_update(const IsoAxis& A, WF W, CF C, double (&out)[9]) {
-	double r[9];
-#pragma unroll
-	for (int k = 0; k < 6; k++) {
-		const int sh = (k % 2 == 0) ? -1 : 1;  // L > 0 -> dx < 0 -> neighbours at -1, -2, ..
-		const double* coef = (k < 2) ? A.c1 : A.c2;
-		const int kf = (k < 2) ? A.kf1 : A.kf2;
-		auto interp = [&](int j) {
-			double sv[BS + 1];
-#pragma unroll
-			for (int i = 0; i <= BS; i++) sv[i] = W(j, sh * i);
-			return newton_minmax<BS, KF0>(sv, kf, coef);
-		};
-		switch (k) {
-		case 0: r[0] = RowSum<S, false, 0>::go(A, interp, 0.0, true); break;
-		case 1: r[1] = RowSum<S, false, 1>::go(A, interp, 0.0, true); break;
-		case 2: r[2] = RowSum<S, false, 2>::go(A, interp, 0.0, true); break;
-		case 3: r[3] = RowSum<S, false, 3>::go(A, interp, 0.0, true); break;
-		case 4: r[4] = RowSum<S, false, 4>::go(A, interp, 0.0, true); break;
-		default: r[5] = RowSum<S, false, 5>::go(A, interp, 0.0, true); break;
-		}
-	}
-	// q == 0: the interpolant is the node value itself
-	r[6] = RowSum<S, false, 6>::go(A, C, 0.0, true);
-	r[7] = RowSum<S, false, 7>::go(A, C, 0.0, true);
-	r[8] = RowSum<S, false, 8>::go(A, C, 0.0, true);
-	auto rv = [&](int n) { return r[n]; };
-	out[0] = RowSum<S, true, 0>::go(A, rv, 0.0, true);
-	out[1] = RowSum<S, true, 1>::go(A, rv, 0.0, true);
-	out[2] = RowSum<S, true, 2>::go(A, rv, 0.0, true);
-	out[3] = RowSum<S, true, 3>::go(A, rv, 0.0, true);
-	out[4] = RowSum<S, true, 4>::go(A, rv, 0.0, true);
-	out[5] = RowSum<S, true, 5>::go(A, rv, 0.0, true);
-	out[6] = RowSum<S, true, 6>::go(A, rv, 0.0, true);
-	out[7] = RowSum<S, true, 7>::go(A, rv, 0.0, true);
-	out[8] = RowSum<S, true, 8>::go(A, rv, 0.0, true);
-}
-
-// Per-component plane base pointers are uniform; per-thread offsets are 32-bit
-// element indices (layer planes are < 2^29 elements, checked on the host).  The
-// nine bases are made opaque SGPR values once per kernel so that every access
-// is the scalar-base + 32-bit-VGPR-offset form (one shared offset register, no
-// 64-bit address arithmetic per component).
-typedef const __attribute__((address_space(1))) double* gcptr;
-typedef __attribute__((address_space(1))) double* gptr;
-#ifndef GCMX_SGPR_BASES
-#define GCMX_SGPR_BASES 1
-#endif
-__device__ __forceinline__ gcptr sgpr_ptr(const double* p) {
-	gcptr q = (gcptr)p;
-#if GCMX_SGPR_BASES
-	asm volatile("" : "+s"(q));
-#endif
-	return q;
-}
-__device__ __forceinline__ gptr sgpr_ptr(double* p) {
-	gptr q = (gptr)p;
-#if GCMX_SGPR_BASES
-	asm volatile("" : "+s"(q));
-#endif
-	return q;
-}
-struct Planes {
-	gcptr b[kMaxM];
-	__device__ __forceinline__ Planes(const double* p, long long cs) {
-#pragma unroll
-		for (int j = 0; j < kMaxM; j++) b[j] = sgpr_ptr(p + j * cs);
-	}
-	__device__ __forceinline__ double ld(int j, unsigned off) const {
-		typedef const __attribute__((address_space(1))) char* gcb;
-		return *reinterpret_cast<gcptr>(reinterpret_cast<gcb>(b[j]) + (size_t)(off << 3));
-	}
-};
-struct PlanesW {
-	gptr b[kMaxM];
-	__device__ __forceinline__ PlanesW(double* p, long long cs) {
-#pragma unroll
-		for (int j = 0; j < kMaxM; j++) b[j] = sgpr_ptr(p + j * cs);
-	}
-	__device__ __forceinline__ void st(int j, unsigned off, double v) const {
-		typedef __attribute__((address_space(1))) char* gb;
-		*reinterpret_cast<gptr>(reinterpret_cast<gb>(b[j]) + (size_t)(off << 3)) = v;
-	}
-};
 
 // ---------------------------------------------------------------- march --
 
@@ -506,181 +298,6 @@ __global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fus
 	}
 }
 
-// ------------------------------------------------------------- fused xyz --
-
-// The whole time step in ONE pass (X stage, then Y, then Z, as
-// Engine::nextTimeStep orders them, Engine.cpp:90-121): block = one x plane, a
-// chunk of y rows and the whole z row.  Each thread marches y; at row y it
-//   * computes the X stage of row y+BS straight from the input layer (its
-//     2*BS+1 x-neighbours are plain loads; the neighbouring planes' blocks read
-//     the same lines, so they come from L2 / Infinity Cache, not HBM),
-//   * pushes that X result into a register window of 2*BS+1 rows and runs the
-//     Y stage of row y,
-//   * hands the Y result to the Z stage through double-buffered LDS.
-// HBM traffic: the input layer once, the output layer once (144 B/node/step).
-// Reads `in` (all components, x ghost planes valid), writes `outl`.
-// Precondition as k_fused_yz: every y/z ghost of both layers is zero, so the
-// intermediate results at ghost rows / columns are the constant 0.0.
-#ifndef GCMX_XYZ_MINWAVES
-#define GCMX_XYZ_MINWAVES 2
-#endif
-#ifndef GCMX_XYZ_CHUNK
-#define GCMX_XYZ_CHUNK 64
-#endif
-#ifndef GCMX_XYZ_PREFETCH
-#define GCMX_XYZ_PREFETCH 1
-#endif
-
-template <int BS, int ZT, bool KF0>
-__global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
-    const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY,
-    IsoAxis AZ, int x0, int chunk) {
-	constexpr unsigned WMX = iso_window(0);
-	constexpr unsigned CMX = iso_center_only(0);
-	constexpr int NWX = popc9(WMX);
-	constexpr unsigned WMY = iso_window(1);
-	constexpr unsigned CMY = iso_center_only(1);
-	constexpr int NWY = popc9(WMY);
-	constexpr int NCY = popc9(CMY);
-	constexpr unsigned WMZ = iso_window(2);
-	constexpr int NWZ = popc9(WMZ);
-	constexpr int W = 2 * BS + 1;
-	constexpr int LW = ZT + 2 * BS;
-	__shared__ double lds[2][NWZ][LW];
-
-	const int z = threadIdx.x;
-	const int x = x0 + blockIdx.y;
-	const int Y = g.sizes[1], Z = g.sizes[2];
-	const int yb = blockIdx.x * chunk;
-	const int ye = min(yb + chunk, Y);
-	const bool live = z < Z;
-	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
-	const unsigned stx = (unsigned)g.stride[0];
-	const unsigned sty = (unsigned)g.stride[1];
-	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
-	const unsigned base = plane + zc;
-	const Planes src(in, g.cs);
-	const PlanesW out_p(outl, g.cs);
-
-	if (z < 2 * BS) {  // ghost slots of both LDS row buffers: zero, never overwritten
-		const int gslot = (z < BS) ? z : (Z + z);
-#pragma unroll
-		for (int q = 0; q < NWZ; q++) {
-			lds[0][q][gslot] = 0.0;
-			lds[1][q][gslot] = 0.0;
-		}
-	}
-
-	// X-stage input of one row: window components at x-BS..x+BS, the rest at x
-	struct XIn {
-		double w[NWX][W];
-		double c[9];
-	};
-	auto x_load = [&](XIn& v, int r) {
-		const unsigned o = base + (unsigned)r * sty;
-#pragma unroll
-		for (int j = 0; j < 9; j++) {
-			if ((WMX >> j) & 1u) {
-#pragma unroll
-				for (int k = 0; k < W; k++) v.w[wslot(WMX, j)][k] = src.ld(j, o + (unsigned)(k - BS) * stx);
-			}
-			if ((CMX >> j) & 1u) v.c[j] = src.ld(j, o);
-		}
-	};
-	auto x_stage = [&](const XIn& v, double (&xr)[9]) {
-		node_update<0, BS, KF0>(
-		    AX, [&](int j, int o) { return v.w[wslot(WMX, j)][BS + o]; },
-		    [&](int j) { return ((WMX >> j) & 1u) ? v.w[wslot(WMX, j)][BS] : v.c[j]; }, xr);
-	};
-	auto in_rows = [&](int r) { return r >= 0 && r < Y; };
-
-	// Y window over X results of rows y-BS..y+BS; node-only components of rows
-	// y..y+BS wait in a small delay line.
-	double win[NWY][W];
-	double cen[BS + 1][NCY > 0 ? NCY : 1];
-	auto push = [&](const double (&xr)[9], int slot) {  // slot: window index of the row
-#pragma unroll
-		for (int j = 0; j < 9; j++) {
-			if ((WMY >> j) & 1u) win[wslot(WMY, j)][slot] = xr[j];
-			if ((CMY >> j) & 1u) {
-				if (slot >= BS) cen[slot - BS][wslot(CMY, j)] = xr[j];
-			}
-		}
-	};
-	// prologue: X results of rows yb-BS .. yb+BS-1
-#pragma unroll
-	for (int k = 0; k < W - 1; k++) {
-		const int r = yb - BS + k;
-		double xr[9];
-		if (in_rows(r)) {
-			XIn v;
-			x_load(v, r);
-			x_stage(v, xr);
-		} else {
-#pragma unroll
-			for (int j = 0; j < 9; j++) xr[j] = 0.0;
-		}
-		push(xr, k);
-	}
-#if GCMX_XYZ_PREFETCH
-	XIn nxt_in;
-	if (in_rows(yb + BS)) x_load(nxt_in, yb + BS);
-#endif
-
-	int buf = 0;
-	for (int y = yb; y < ye; y++) {
-		{  // X stage of row y+BS -> window slot W-1
-			const int r = y + BS;
-			double xr[9];
-			if (in_rows(r)) {
-#if GCMX_XYZ_PREFETCH
-				x_stage(nxt_in, xr);
-#else
-				XIn v;
-				x_load(v, r);
-				x_stage(v, xr);
-#endif
-			} else {
-#pragma unroll
-				for (int j = 0; j < 9; j++) xr[j] = 0.0;
-			}
-			push(xr, W - 1);
-#if GCMX_XYZ_PREFETCH
-			if (y + 1 < ye && in_rows(r + 1)) x_load(nxt_in, r + 1);
-#endif
-		}
-		double yv[9];
-		node_update<1, BS, KF0>(
-		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
-		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : cen[0][wslot(CMY, j)]; },
-		    yv);
-		if (live) {
-#pragma unroll
-			for (int j = 0; j < 9; j++)
-				if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = yv[j];
-		}
-		__syncthreads();
-		if (live) {
-			double zv[9];
-			node_update<2, BS, KF0>(
-			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
-			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
-			const unsigned offo = plane + (unsigned)y * sty + z;
-#pragma unroll
-			for (int c = 0; c < 9; c++) out_p.st(c, offo, zv[c]);
-		}
-		buf ^= 1;
-#pragma unroll
-		for (int q = 0; q < NWY; q++)
-#pragma unroll
-			for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
-#pragma unroll
-		for (int k = 0; k < BS; k++)
-#pragma unroll
-			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
-	}
-}
-
 // ------------------------------------------------------------- launchers --
 
 static int march_chunk(int len) { return len < 2 * GCMX_MARCH_CHUNK ? len : GCMX_MARCH_CHUNK; }
@@ -780,46 +397,6 @@ static bool launch_fused_bs(const double* in, double* out, const Geo& g, const I
 	else if (Z <= 512) launch_fused_t<BS, 512>(in, out, g, ay, az, x0, x1, st);
 	else launch_fused_t<BS, 1024>(in, out, g, ay, az, x0, x1, st);
 	return true;
-}
-
-static int xyz_chunk(int Y) { return Y <= GCMX_XYZ_CHUNK ? Y : GCMX_XYZ_CHUNK; }
-
-template <int BS, int ZT>
-static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                         int x1, hipStream_t st) {
-	const int chunk = xyz_chunk(g.sizes[1]);
-	dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0);
-	bool kf0 = true;
-	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
-	if (kf0)
-		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
-		                   a[2], x0, chunk);
-	else
-		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, false>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
-		                   a[2], x0, chunk);
-}
-
-template <int BS>
-static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                          int x1, hipStream_t st) {
-	const int Z = g.sizes[2];
-	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st);
-	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st);
-	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st);
-	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st);
-	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st);
-	return true;
-}
-
-bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                      int x1, hipStream_t st) {
-	if (!fused_yz_supported(g) || x1 <= x0) return false;
-	switch (g.bs) {
-	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st);
-	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st);
-	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st);
-	default: return false;
-	}
 }
 
 bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis& ay,

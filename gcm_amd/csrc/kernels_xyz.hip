@@ -1,0 +1,434 @@
+// kernels_xyz.hip -- the one-pass 3-D time step (X, Y and Z stages of
+// cubic::Engine::nextTimeStep, Engine.cpp:90-121, fused into one kernel).
+// Arithmetic identical to k_stage_generic / the reference stage
+// (engine/cubic/GridCharacteristicMethod.hpp:42-52) through node_update (iso.hpp).
+#include "iso.hpp"
+
+#include <type_traits>
+
+namespace gcmx {
+
+// ------------------------------------------------------------- fused xyz --
+
+// The whole time step in ONE pass (X stage, then Y, then Z, as
+// Engine::nextTimeStep orders them, Engine.cpp:90-121): block = one x plane, a
+// chunk of y rows and the whole z row.  Each thread marches y; at row y it
+//   * computes the X stage of row y+BS straight from the input layer (its
+//     2*BS+1 x-neighbours are plain loads; the neighbouring planes' blocks read
+//     the same lines, so they come from L2 / Infinity Cache, not HBM),
+//   * pushes that X result into a register window of 2*BS+1 rows and runs the
+//     Y stage of row y,
+//   * hands the Y result to the Z stage through double-buffered LDS.
+// HBM traffic: the input layer once, the output layer once (144 B/node/step).
+// Reads `in` (all components, x ghost planes valid), writes `outl`.
+// Precondition as k_fused_yz: every y/z ghost of both layers is zero, so the
+// intermediate results at ghost rows / columns are the constant 0.0.
+#ifndef GCMX_XYZ_MINWAVES
+#define GCMX_XYZ_MINWAVES 4
+#endif
+#ifndef GCMX_XYZ_CHUNK
+#define GCMX_XYZ_CHUNK 64
+#endif
+#ifndef GCMX_XYZ_ROTATE
+#define GCMX_XYZ_ROTATE 1
+#endif
+#ifndef GCMX_XYZ_UNROLL
+#define GCMX_XYZ_UNROLL 1
+#endif
+#ifndef GCMX_XYZ_GROUPED
+#define GCMX_XYZ_GROUPED 1
+#endif
+#ifndef GCMX_XYZ_SCHED_BARRIER
+#define GCMX_XYZ_SCHED_BARRIER 1
+#endif
+#ifndef GCMX_XYZ_PREFETCH
+#define GCMX_XYZ_PREFETCH 1
+#endif
+// Diagnostic builds only (scripts/ab_build.sh; results are wrong by design).
+#ifndef GCMX_DIAG_L2HOT
+#define GCMX_DIAG_L2HOT 0
+#endif
+#ifndef GCMX_DIAG_NOSTORE
+#define GCMX_DIAG_NOSTORE 0
+#endif
+#ifndef GCMX_XYZ_NT_STORE
+#define GCMX_XYZ_NT_STORE 0
+#endif
+#if GCMX_XYZ_NT_STORE
+#define XYZ_ST out_p.st_nt
+#else
+#define XYZ_ST out_p.st
+#endif
+#ifndef GCMX_DIAG_HALFZ
+#define GCMX_DIAG_HALFZ 0
+#endif
+#ifndef GCMX_DIAG_NOBAR
+#define GCMX_DIAG_NOBAR 0
+#endif
+
+template <int BS, int ZT, bool KF0>
+__global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
+    const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY,
+    IsoAxis AZ, int x0, int chunk) {
+	constexpr unsigned WMX = iso_window(0);
+	constexpr unsigned CMX = iso_center_only(0);
+	constexpr int NWX = popc9(WMX);
+	constexpr unsigned WMY = iso_window(1);
+	constexpr unsigned CMY = iso_center_only(1);
+	constexpr int NWY = popc9(WMY);
+	constexpr int NCY = popc9(CMY);
+	constexpr unsigned WMZ = iso_window(2);
+	constexpr int NWZ = popc9(WMZ);
+	constexpr int W = 2 * BS + 1;
+	constexpr int LW = ZT + 2 * BS;
+	__shared__ double lds[2][NWZ][LW];
+
+	const int z = threadIdx.x;
+	const int x = x0 + blockIdx.y;
+	const int Y = g.sizes[1], Z = g.sizes[2];
+	const int yb = blockIdx.x * chunk;
+	const int ye = min(yb + chunk, Y);
+#if GCMX_DIAG_HALFZ  // diagnostic: ZT-wide z tiles, no halo (wrong at tile edges)
+	const unsigned zoff = blockIdx.z * ZT;
+	const int ZL = ZT;
+#else
+	const unsigned zoff = 0;
+	const int ZL = Z;
+#endif
+	const bool live = z < ZL;
+	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
+	const unsigned stx = (unsigned)g.stride[0];
+	const unsigned sty = (unsigned)g.stride[1];
+	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]) + zoff;
+#if GCMX_DIAG_L2HOT  // diagnostic: every block reads x plane 2 (L2-resident loads)
+	const unsigned base = (unsigned)(g.origin + 2 * g.stride[0]) + zc;
+#else
+	const unsigned base = plane + zc;
+#endif
+	const Planes src(in, g.cs);
+	const PlanesW out_p(outl, g.cs);
+
+	if (z < 2 * BS) {  // ghost slots of both LDS row buffers: zero, never overwritten
+		const int gslot = (z < BS) ? z : (ZL + z);
+#pragma unroll
+		for (int q = 0; q < NWZ; q++) {
+			lds[0][q][gslot] = 0.0;
+			lds[1][q][gslot] = 0.0;
+		}
+	}
+
+	// X-stage input of one row: window components at x-BS..x+BS, the rest at x
+	struct XIn {
+		double w[NWX][W];
+		double c[9];
+	};
+	auto x_load = [&](XIn& v, int r) {
+		const unsigned o = base + (unsigned)r * sty;
+#pragma unroll
+		for (int j = 0; j < 9; j++) {
+			if ((WMX >> j) & 1u) {
+#pragma unroll
+				for (int k = 0; k < W; k++) v.w[wslot(WMX, j)][k] = src.ld(j, o + (unsigned)(k - BS) * stx);
+			}
+			if ((CMX >> j) & 1u) v.c[j] = src.ld(j, o);
+		}
+	};
+	auto x_stage = [&](const XIn& v, double (&xr)[9]) {
+		node_update<0, BS, KF0>(
+		    AX, [&](int j, int o) { return v.w[wslot(WMX, j)][BS + o]; },
+		    [&](int j) { return ((WMX >> j) & 1u) ? v.w[wslot(WMX, j)][BS] : v.c[j]; }, xr);
+	};
+	auto in_rows = [&](int r) { return r >= 0 && r < Y; };
+
+	// Grouped X stage (GCMX_XYZ_GROUPED): the row's 33 inputs are loaded one
+	// characteristic pair at a time (10 values), the next pair's loads in flight
+	// while the current pair is computed, so at most two pairs are live in
+	// registers (instead of all 33 values): the kernel fits 128 VGPRs, i.e. two
+	// 512-thread blocks per CU.  Same node_update arithmetic (iso.hpp).
+	typedef double PairWin[2][W];
+	auto pair_load = [&](auto PC, PairWin& w, unsigned o) {
+		constexpr int P = decltype(PC)::value;
+#pragma unroll
+		for (int k = 0; k < W; k++) {
+			w[0][k] = src.ld(pair_vel(0, P), o + (unsigned)(k - BS) * stx);
+			w[1][k] = src.ld(pair_sig(0, P), o + (unsigned)(k - BS) * stx);
+		}
+	};
+	auto pair_acc = [&](auto PC, const PairWin& w) {
+		constexpr int P = decltype(PC)::value;
+		return [&w](int j, int o) { return j == pair_vel(0, P) ? w[0][BS + o] : w[1][BS + o]; };
+	};
+	auto sched_fence = [] {
+#if GCMX_XYZ_SCHED_BARRIER
+		__builtin_amdgcn_sched_barrier(0);
+#endif
+	};
+	auto x_stage_grouped = [&](int r, double (&xr)[9]) {
+		const unsigned o = base + (unsigned)r * sty;
+		using P0 = std::integral_constant<int, 0>;
+		using P1 = std::integral_constant<int, 1>;
+		using P2 = std::integral_constant<int, 2>;
+		double rr[9], n0[9], cv[9];
+		PairWin wa, wb;
+		pair_load(P0{}, wa, o);
+		sched_fence();
+		pair_load(P1{}, wb, o);
+		pair_update<0, BS, KF0, 0>(AX, pair_acc(P0{}, wa), rr[0], rr[1]);
+		n0[pair_vel(0, 0)] = wa[0][BS];
+		n0[pair_sig(0, 0)] = wa[1][BS];
+		sched_fence();
+		pair_load(P2{}, wa, o);
+		pair_update<0, BS, KF0, 1>(AX, pair_acc(P1{}, wb), rr[2], rr[3]);
+		n0[pair_vel(0, 1)] = wb[0][BS];
+		n0[pair_sig(0, 1)] = wb[1][BS];
+		sched_fence();
+#pragma unroll
+		for (int j = 0; j < 9; j++)
+			if ((CMX >> j) & 1u) cv[j] = src.ld(j, o);
+		pair_update<0, BS, KF0, 2>(AX, pair_acc(P2{}, wa), rr[4], rr[5]);
+		n0[pair_vel(0, 2)] = wa[0][BS];
+		n0[pair_sig(0, 2)] = wa[1][BS];
+		sched_fence();
+		center_update<0>(AX, [&](int j) { return ((WMX >> j) & 1u) ? n0[j] : cv[j]; }, rr);
+		u1_apply<0>(AX, rr, xr);
+	};
+
+	// Y window over X results of rows y-BS..y+BS; node-only components of rows
+	// y..y+BS wait in a small delay line.
+	double win[NWY][W];
+	double cen[BS + 1][NCY > 0 ? NCY : 1];
+	auto push = [&](const double (&xr)[9], int slot) {  // slot: window index of the row
+#pragma unroll
+		for (int j = 0; j < 9; j++) {
+			if ((WMY >> j) & 1u) win[wslot(WMY, j)][slot] = xr[j];
+			if ((CMY >> j) & 1u) {
+				if (slot >= BS) cen[slot - BS][wslot(CMY, j)] = xr[j];
+			}
+		}
+	};
+#if GCMX_XYZ_ROTATE
+	// Rotated schedule: the loads of an X row are issued at the END of an
+	// iteration and consumed after the next iteration's stores, so in every path
+	// into the loop they are older than 9 stores and the compiler's vmcnt waits
+	// never include the stores' completion.  Stores, LDS writes and the Z stage
+	// are unconditional (idle lanes z >= Z write 0.0 into the first z ghost, which
+	// the precondition keeps zero), and the in-loop X rows are loaded without a
+	// branch: rows outside [0, Y) are zero ghost rows, clamped into the plane.
+	// prologue: X results of rows yb-BS .. yb+BS
+#pragma unroll
+	for (int k = 0; k < W; k++) {
+		const int r = yb - BS + k;
+		double xr[9];
+		if (in_rows(r)) {
+			XIn v;
+			x_load(v, r);
+			x_stage(v, xr);
+		} else {
+#pragma unroll
+			for (int j = 0; j < 9; j++) xr[j] = 0.0;
+		}
+		push(xr, k);
+	}
+	auto clamp_row = [&](int r) { return r < Y + BS - 1 ? r : Y + BS - 1; };
+#if !GCMX_XYZ_GROUPED
+	XIn nxt_in;
+	x_load(nxt_in, clamp_row(yb + BS + 1));
+#endif
+	const unsigned zo = live ? (unsigned)z : (unsigned)Z;
+
+	int buf = 0;
+#if GCMX_XYZ_UNROLL > 1
+#pragma unroll GCMX_XYZ_UNROLL
+#endif
+	for (int y = yb; y < ye; y++) {
+		double yv[9];
+		node_update<1, BS, KF0>(
+		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
+		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : cen[0][wslot(CMY, j)]; },
+		    yv);
+#pragma unroll
+		for (int j = 0; j < 9; j++)
+			if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = live ? yv[j] : 0.0;
+#if !GCMX_DIAG_NOBAR
+		__syncthreads();
+#endif
+		{
+			double zv[9];
+			node_update<2, BS, KF0>(
+			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
+			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
+			const unsigned offo = plane + (unsigned)y * sty + zo;
+#if GCMX_DIAG_NOSTORE  // diagnostic: keep the work, drop the stores
+			if (zv[0] == 1234.5678)
+#endif
+#pragma unroll
+			for (int c = 0; c < 9; c++) XYZ_ST(c, offo, live ? zv[c] : 0.0);
+		}
+		buf ^= 1;
+#pragma unroll
+		for (int q = 0; q < NWY; q++)
+#pragma unroll
+			for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
+#pragma unroll
+		for (int k = 0; k < BS; k++)
+#pragma unroll
+			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
+		{  // X stage of row y+BS+1 (zero ghost rows give zero) -> window slot W-1
+			double xr[9];
+#if GCMX_XYZ_GROUPED
+			sched_fence();
+			x_stage_grouped(clamp_row(y + BS + 1), xr);
+			push(xr, W - 1);
+			sched_fence();
+#else
+#if GCMX_XYZ_SCHED_BARRIER  // keep the next row's loads behind this row's stores
+			__builtin_amdgcn_sched_barrier(0);
+#endif
+			x_stage(nxt_in, xr);
+			push(xr, W - 1);
+#if GCMX_XYZ_SCHED_BARRIER
+			__builtin_amdgcn_sched_barrier(0);
+#endif
+			x_load(nxt_in, clamp_row(y + BS + 2));
+#endif
+		}
+	}
+#else
+	// prologue: X results of rows yb-BS .. yb+BS-1
+#pragma unroll
+	for (int k = 0; k < W - 1; k++) {
+		const int r = yb - BS + k;
+		double xr[9];
+		if (in_rows(r)) {
+			XIn v;
+			x_load(v, r);
+			x_stage(v, xr);
+		} else {
+#pragma unroll
+			for (int j = 0; j < 9; j++) xr[j] = 0.0;
+		}
+		push(xr, k);
+	}
+#if GCMX_XYZ_PREFETCH
+	XIn nxt_in;
+	if (in_rows(yb + BS)) x_load(nxt_in, yb + BS);
+#endif
+
+	int buf = 0;
+	for (int y = yb; y < ye; y++) {
+		{  // X stage of row y+BS -> window slot W-1
+			const int r = y + BS;
+			double xr[9];
+			if (in_rows(r)) {
+#if GCMX_XYZ_PREFETCH
+				x_stage(nxt_in, xr);
+#else
+				XIn v;
+				x_load(v, r);
+				x_stage(v, xr);
+#endif
+			} else {
+#pragma unroll
+				for (int j = 0; j < 9; j++) xr[j] = 0.0;
+			}
+			push(xr, W - 1);
+#if GCMX_XYZ_PREFETCH
+			if (y + 1 < ye && in_rows(r + 1)) x_load(nxt_in, r + 1);
+#endif
+		}
+		double yv[9];
+		node_update<1, BS, KF0>(
+		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
+		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : cen[0][wslot(CMY, j)]; },
+		    yv);
+		if (live) {
+#pragma unroll
+			for (int j = 0; j < 9; j++)
+				if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = yv[j];
+		}
+#if !GCMX_DIAG_NOBAR
+		__syncthreads();
+#endif
+		if (live) {
+			double zv[9];
+			node_update<2, BS, KF0>(
+			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
+			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
+			const unsigned offo = plane + (unsigned)y * sty + z;
+#if GCMX_DIAG_NOSTORE  // diagnostic: keep the work, drop the stores
+			if (zv[0] == 1234.5678)
+#endif
+#pragma unroll
+			for (int c = 0; c < 9; c++) XYZ_ST(c, offo, zv[c]);
+		}
+		buf ^= 1;
+#pragma unroll
+		for (int q = 0; q < NWY; q++)
+#pragma unroll
+			for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
+#pragma unroll
+		for (int k = 0; k < BS; k++)
+#pragma unroll
+			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
+	}
+#endif
+}
+
+// ------------------------------------------------------------- launchers --
+
+static int xyz_chunk(int Y) { return Y <= GCMX_XYZ_CHUNK ? Y : GCMX_XYZ_CHUNK; }
+
+template <int BS, int ZT>
+static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                         int x1, hipStream_t st) {
+	const int chunk = xyz_chunk(g.sizes[1]);
+	dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0);
+	bool kf0 = true;
+	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
+	if (kf0)
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk);
+	else
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, false>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk);
+}
+
+template <int BS>
+static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                          int x1, hipStream_t st) {
+	const int Z = g.sizes[2];
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st);
+	return true;
+}
+
+bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                      int x1, hipStream_t st) {
+	if (!fused_yz_supported(g) || x1 <= x0) return false;
+#ifdef GCMX_TUNE_FAST  // tuning builds: the bench configuration only
+	if (g.bs != 2 || g.sizes[2] <= 256 || g.sizes[2] > 512) return false;
+#if GCMX_DIAG_HALFZ
+	{
+		const int chunk = xyz_chunk(g.sizes[1]);
+		dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0, 2);
+		hipLaunchKernelGGL((k_fused_xyz<2, 256, true>), grid, dim3(256), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk);
+		return true;
+	}
+#endif
+	launch_xyz_t<2, 512>(in, out, g, a, x0, x1, st);
+	return true;
+#endif
+	switch (g.bs) {
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st);
+	default: return false;
+	}
+}
+
+
+}  // namespace gcmx

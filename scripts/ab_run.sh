@@ -6,6 +6,11 @@ mkdir -p gpurun_out/ab
 for rep in 1 2; do
 for d in gcm_amd/lib/tune/*/; do
   name=$(basename "$d")
+  if [ $rep = 1 ]; then
+    GCMX_LIB="$d/libgcmx.so" timeout -k 10 120 python scripts/ab_check.py > gpurun_out/ab/$name.check 2>&1
+    rc=$?; echo "$name: $(tail -1 gpurun_out/ab/$name.check)"
+    [ $rc -le 1 ] || exit $rc
+  fi
   GCMX_LIB="$d/libgcmx.so" timeout -k 10 300 python bench.py --n ${N:-512} --steps ${STEPS:-20} \
     --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab/$name.$rep.json 2> gpurun_out/ab/$name.$rep.err
   rc=$?
