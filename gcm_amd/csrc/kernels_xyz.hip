@@ -21,6 +21,14 @@ namespace gcmx {
 //   * hands the Y result to the Z stage through double-buffered LDS.
 // HBM traffic: the input layer once, the output layer once (144 B/node/step).
 // Reads `in` (all components, x ghost planes valid), writes `outl`.
+//
+// Schedule (defaults below, measured A/B on MI355X): the loop is
+// rotated (Y, Z, stores, then the X stage of the row that enters the window);
+// the X stage loads one characteristic pair (10 values) at a time with the next
+// pair in flight, which keeps the kernel at 128 VGPRs (two 512-thread blocks per
+// CU); the first pair of the next row is issued before this row's stores, so
+// its vmcnt wait never includes the stores (loads and stores retire in order on
+// gfx950); the output is written with non-temporal stores.
 // Precondition as k_fused_yz: every y/z ghost of both layers is zero, so the
 // intermediate results at ghost rows / columns are the constant 0.0.
 #ifndef GCMX_XYZ_MINWAVES
@@ -36,7 +44,7 @@ namespace gcmx {
 #define GCMX_XYZ_UNROLL 1
 #endif
 #ifndef GCMX_XYZ_GROUPED
-#define GCMX_XYZ_GROUPED 1
+#define GCMX_XYZ_GROUPED 2
 #endif
 #ifndef GCMX_XYZ_SCHED_BARRIER
 #define GCMX_XYZ_SCHED_BARRIER 1
@@ -52,12 +60,15 @@ namespace gcmx {
 #define GCMX_DIAG_NOSTORE 0
 #endif
 #ifndef GCMX_XYZ_NT_STORE
-#define GCMX_XYZ_NT_STORE 0
+#define GCMX_XYZ_NT_STORE 1
 #endif
 #if GCMX_XYZ_NT_STORE
 #define XYZ_ST out_p.st_nt
 #else
 #define XYZ_ST out_p.st
+#endif
+#ifndef GCMX_DIAG_HOTSTORE
+#define GCMX_DIAG_HOTSTORE 0
 #endif
 #ifndef GCMX_DIAG_HALFZ
 #define GCMX_DIAG_HALFZ 0
@@ -163,15 +174,14 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		__builtin_amdgcn_sched_barrier(0);
 #endif
 	};
-	auto x_stage_grouped = [&](int r, double (&xr)[9]) {
+	// (split so that the first pair's loads can be issued ahead of the stores)
+	auto x_stage_grouped_rest = [&](PairWin& wa, int r, double (&xr)[9]) {
 		const unsigned o = base + (unsigned)r * sty;
 		using P0 = std::integral_constant<int, 0>;
 		using P1 = std::integral_constant<int, 1>;
 		using P2 = std::integral_constant<int, 2>;
 		double rr[9], n0[9], cv[9];
-		PairWin wa, wb;
-		pair_load(P0{}, wa, o);
-		sched_fence();
+		PairWin wb;
 		pair_load(P1{}, wb, o);
 		pair_update<0, BS, KF0, 0>(AX, pair_acc(P0{}, wa), rr[0], rr[1]);
 		n0[pair_vel(0, 0)] = wa[0][BS];
@@ -191,6 +201,15 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		sched_fence();
 		center_update<0>(AX, [&](int j) { return ((WMX >> j) & 1u) ? n0[j] : cv[j]; }, rr);
 		u1_apply<0>(AX, rr, xr);
+	};
+	auto x_load_a = [&](PairWin& wa, int r) {
+		pair_load(std::integral_constant<int, 0>{}, wa, base + (unsigned)r * sty);
+	};
+	auto x_stage_grouped = [&](int r, double (&xr)[9]) {
+		PairWin wa;
+		x_load_a(wa, r);
+		sched_fence();
+		x_stage_grouped_rest(wa, r, xr);
 	};
 
 	// Y window over X results of rows y-BS..y+BS; node-only components of rows
@@ -252,12 +271,24 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #if !GCMX_DIAG_NOBAR
 		__syncthreads();
 #endif
+#if GCMX_XYZ_GROUPED == 2
+		PairWin wa_next;
+#endif
 		{
 			double zv[9];
 			node_update<2, BS, KF0>(
 			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
 			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
+#if GCMX_DIAG_HOTSTORE  // diagnostic: every block stores into x plane 2 (L2-resident)
+			const unsigned offo = (unsigned)(g.origin + 2 * g.stride[0]) + zoff + (unsigned)y * sty + zo;
+#else
 			const unsigned offo = plane + (unsigned)y * sty + zo;
+#endif
+#if GCMX_XYZ_GROUPED == 2  // next row's first pair: loads older than this row's stores
+			sched_fence();
+			x_load_a(wa_next, clamp_row(y + BS + 1));
+			sched_fence();
+#endif
 #if GCMX_DIAG_NOSTORE  // diagnostic: keep the work, drop the stores
 			if (zv[0] == 1234.5678)
 #endif
@@ -275,7 +306,12 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
 		{  // X stage of row y+BS+1 (zero ghost rows give zero) -> window slot W-1
 			double xr[9];
-#if GCMX_XYZ_GROUPED
+#if GCMX_XYZ_GROUPED == 2
+			sched_fence();
+			x_stage_grouped_rest(wa_next, clamp_row(y + BS + 1), xr);
+			push(xr, W - 1);
+			sched_fence();
+#elif GCMX_XYZ_GROUPED
 			sched_fence();
 			x_stage_grouped(clamp_row(y + BS + 1), xr);
 			push(xr, W - 1);
