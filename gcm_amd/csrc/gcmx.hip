@@ -85,6 +85,7 @@ struct gcmx_ctx {
 	size_t nodes_cap = 0;
 	int* qs_d = nullptr;
 	double* vals_d = nullptr;
+	double* ode_d = nullptr;  // per-material ODE factors (256)
 };
 
 namespace {
@@ -445,6 +446,7 @@ void gcmx_destroy(gcmx_ctx* c) {
 	hipFree(c->nodes_d);
 	hipFree(c->qs_d);
 	hipFree(c->vals_d);
+	hipFree(c->ode_d);
 	if (c->ev_ready) hipEventDestroy(c->ev_ready);
 	if (c->ev_halo) hipEventDestroy(c->ev_halo);
 	if (c->stream) hipStreamDestroy(c->stream);
@@ -781,6 +783,30 @@ gcmx_status gcmx_border_fill(gcmx_ctx* c, int axis, int side, int n_nodes, const
 	}
 	launch_border_fill(c->cur, c->geo, axis, side > 0 ? -1 : 1, n_nodes, c->nodes_d, n_q, c->qs_d,
 	                   c->vals_d, c->stream);
+	HIP_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_ode_maxwell(gcmx_ctx* c, double tau, const double* tau0, int n_mat) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (c->n_mat == 0) return fail(GCMX_ERR_STATE, "materials not set");
+	if (!tau0 || n_mat != c->n_mat) return fail(GCMX_ERR_INVALID_ARG, "one tau0 per material expected");
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	s = halo_wait(c);
+	if (s) return s;
+	std::vector<double> f(n_mat);
+	for (int m = 0; m < n_mat; m++) f[m] = std::exp(-tau / tau0[m]);  // Ode.hpp:34-35
+	if (!c->mat_d) {
+		Timed t(c, "ode_maxwell", 2.0 * 8.0 * (c->M - c->D) * (double)c->geo.n_inner, c->stream);
+		launch_scale_stress(c->cur, c->geo, nullptr, nullptr, f[0], c->stream);
+	} else {
+		HIP_TRY(hipStreamSynchronize(c->stream));  // scratch reuse
+		if (!c->ode_d) HIP_TRY(hipMalloc(&c->ode_d, 256 * sizeof(double)));
+		HIP_TRY(hipMemcpy(c->ode_d, f.data(), n_mat * sizeof(double), hipMemcpyHostToDevice));
+		Timed t(c, "ode_maxwell", (2.0 * 8.0 * (c->M - c->D) + 1.0) * (double)c->geo.n_inner, c->stream);
+		launch_scale_stress(c->cur, c->geo, c->mat_d, c->ode_d, 0.0, c->stream);
+	}
 	HIP_TRY(hipGetLastError());
 	return GCMX_OK;
 }

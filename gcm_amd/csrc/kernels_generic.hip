@@ -231,6 +231,31 @@ void launch_copy_box(double* dst, const Geo& gd, const double* src, const Geo& g
 	                   ext[1], ext[2]);
 }
 
+// MaxwellViscosityOde::apply (rheology/ode/Ode.hpp:28-37): every stress
+// component of every inner node times exp(-tau / tau0) of the node's material
+// (the factor per material is computed on the host, once, like the reference
+// computes it per node: same libm call, same bits).  One thread per inner node.
+__global__ __launch_bounds__(256) void k_scale_stress(double* __restrict__ cur, Geo g,
+                                                      const uint8_t* __restrict__ mat,
+                                                      const double* __restrict__ f_d, double f0) {
+	const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= g.n_inner) return;
+	const int z = (int)(i % g.sizes[2]);
+	const long long t = i / g.sizes[2];
+	const int y = (int)(t % g.sizes[1]);
+	const int x = (int)(t / g.sizes[1]);
+	const long long off = g.origin + x * g.stride[0] + y * g.stride[1] + z * g.stride[2];
+	const double f = mat ? f_d[mat[i]] : f0;
+	for (int c = g.D; c < g.M; c++) cur[c * g.cs + off] = cur[c * g.cs + off] * f;
+}
+
+void launch_scale_stress(double* cur, const Geo& g, const uint8_t* mat_d, const double* f_d,
+                         double f0, hipStream_t st) {
+	if (g.n_inner <= 0) return;
+	hipLaunchKernelGGL(k_scale_stress, dim3((unsigned)((g.n_inner + 255) / 256)), dim3(256), 0, st,
+	                   cur, g, mat_d, f_d, f0);
+}
+
 void launch_border_fill(double* cur, const Geo& g, int axis, int inner_sign, int n_nodes,
                         const int* nodes_d, int n_q, const int* qs_d, const double* vals_d,
                         hipStream_t st) {

@@ -12,6 +12,8 @@ void launch_fill_random(double* cur, const Geo& g, const int gstart[3], long lon
                         long long GZ, uint64_t seed, hipStream_t st);
 void launch_copy_box(double* dst, const Geo& gd, const double* src, const Geo& gs,
                      const int dmin[3], const int smin[3], const int ext[3], hipStream_t st);
+void launch_scale_stress(double* cur, const Geo& g, const uint8_t* mat_d, const double* f_d,
+                         double f0, hipStream_t st);
 void launch_border_fill(double* cur, const Geo& g, int axis, int inner_sign, int n_nodes,
                         const int* nodes_d, int n_q, const int* qs_d, const double* vals_d,
                         hipStream_t st);

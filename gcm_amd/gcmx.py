@@ -33,6 +33,7 @@ SYMBOLS = [
     "gcmx_create", "gcmx_destroy", "gcmx_set_materials", "gcmx_set_material_ids",
     "gcmx_upload", "gcmx_download", "gcmx_fill_random", "gcmx_stage", "gcmx_step",
     "gcmx_set_kernel_path", "gcmx_effective_path", "gcmx_border_fill", "gcmx_copy_box",
+    "gcmx_ode_maxwell",
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_sync", "gcmx_stream",
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_inner_nodes",
@@ -89,6 +90,7 @@ def lib() -> ctypes.CDLL:
     L.gcmx_border_fill.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int,
                                    ip, dp]
     L.gcmx_copy_box.argtypes = [vp, ip, ip, vp, ip]
+    L.gcmx_ode_maxwell.argtypes = [vp, ctypes.c_double, dp, ctypes.c_int]
     L.gcmx_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
     L.gcmx_comm_init.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int]
@@ -228,6 +230,11 @@ class Context:
         pad = lambda s: list(s) + [0] * (3 - len(s))
         _check(lib().gcmx_copy_box(self._ptr, _ip(pad(dst_min)), _ip(pad(dst_max)), src._ptr,
                                    _ip(pad(src_min))))
+
+    def ode_maxwell(self, tau: float, tau0: Sequence[float]):
+        """MaxwellViscosityOde::apply: sigma *= exp(-tau / tau0[material])."""
+        t0 = np.ascontiguousarray(tau0, dtype=np.float64).reshape(-1)
+        _check(lib().gcmx_ode_maxwell(self._ptr, tau, _dp(t0), t0.shape[0]))
 
     def comm_init(self, unique_id: bytes, nranks: int, rank: int, left: int, right: int):
         buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)(*unique_id)

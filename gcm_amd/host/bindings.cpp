@@ -138,19 +138,32 @@ PYBIND11_MODULE(_gcm_host, m) {
 		         t.cubicGrid.cubics[id] = {sizes, start};
 	         })
 	    .def("set_default_material",
-	         [](Task& t, real rho, real lam, real mu) {
+	         [](Task& t, real rho, real lam, real mu, real tau0) {
 		         t.materialConditions.type = Task::MaterialCondition::Type::BY_AREAS;
-		         t.materialConditions.byAreas.defaultMaterial = std::make_shared<IsotropicMaterial>(rho, lam, mu);
-	         })
+		         t.materialConditions.byAreas.defaultMaterial =
+		             std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, 0, tau0);
+	         },
+	         py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0)
 	    .def("add_material",
-	         [](Task& t, py::tuple area, real rho, real lam, real mu) {
+	         [](Task& t, py::tuple area, real rho, real lam, real mu, real tau0) {
 		         t.materialConditions.byAreas.materials.push_back(
-		             {makeArea(area), std::make_shared<IsotropicMaterial>(rho, lam, mu)});
-	         })
+		             {makeArea(area), std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, 0, tau0)});
+	         },
+	         py::arg("area"), py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0)
 	    .def("set_body_material",
-	         [](Task& t, size_t id, real rho, real lam, real mu) {
+	         [](Task& t, size_t id, real rho, real lam, real mu, real tau0) {
 		         t.materialConditions.type = Task::MaterialCondition::Type::BY_BODIES;
-		         t.materialConditions.byBodies.bodyMaterialMap[id] = std::make_shared<IsotropicMaterial>(rho, lam, mu);
+		         t.materialConditions.byBodies.bodyMaterialMap[id] =
+		             std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, 0, tau0);
+	         },
+	         py::arg("id"), py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0)
+	    .def("add_ode",
+	         [](Task& t, size_t id, const std::string& name) {
+		         if (!t.bodies.count(id)) throw Exception("add_ode: no such body");
+		         if (name == "MAXWELL_VISCOSITY") t.bodies[id].odes.push_back(Odes::T::MAXWELL_VISCOSITY);
+		         else if (name == "CONTINUAL_DAMAGE") t.bodies[id].odes.push_back(Odes::T::CONTINUAL_DAMAGE);
+		         else if (name == "IDEAL_PLASTIC_FLOW") t.bodies[id].odes.push_back(Odes::T::IDEAL_PLASTIC_FLOW);
+		         else throw Exception("unknown ODE type " + name);
 	         })
 	    .def("add_initial_vector",
 	         [](Task& t, py::tuple area, std::vector<real> v) {

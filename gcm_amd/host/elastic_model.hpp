@@ -23,8 +23,16 @@ constexpr int pdeSize(int D) { return D + D * (D + 1) / 2; }
 /// Isotropic material (rheology/materials/IsotropicMaterial.hpp:7-27).
 struct IsotropicMaterial {
 	real rho = 0, lambda = 0, mu = 0;
+	real yieldStrength = 0;             ///< plasticity parameter
+	real continualDamageParameter = 0;  ///< parameter in the continual damage equation
+	int materialNumber = 0;
+	real tau0 = 0;                      ///< viscosity parameter (decay time), MaxwellViscosityOde
 	IsotropicMaterial() = default;
-	IsotropicMaterial(real rho_, real lambda_, real mu_) : rho(rho_), lambda(lambda_), mu(mu_) {}
+	IsotropicMaterial(real rho_, real lambda_, real mu_, real yieldStrength_ = 0,
+	                  real continualDamageParameter_ = 0, int materialNumber_ = 0, real tau0_ = 0)
+	    : rho(rho_), lambda(lambda_), mu(mu_), yieldStrength(yieldStrength_),
+	      continualDamageParameter(continualDamageParameter_), materialNumber(materialNumber_),
+	      tau0(tau0_) {}
 };
 
 /// GcmMatrices<M,D>::GcmMatrix (util/math/GridCharacteristicMethod.hpp:40-52), row-major.

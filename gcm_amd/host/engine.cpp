@@ -175,9 +175,11 @@ HostState<D> buildHostState(const Task& task, const CubicGrid<D>& grid) {
 	}
 	if (conds.size() > 255) throw Exception("at most 255 material conditions per body");
 	matrices.assign(conds.size(), GcmMatrices<D>());
+	st.tau0.assign(conds.size(), 0);
 	for (size_t c = 0; c < conds.size(); c++) {
 		if (!conds[c].second) throw Exception("material condition without a material");
 		ElasticModel<D>::constructGcmMatrices(matrices[c], *conds[c].second);
+		st.tau0[c] = conds[c].second->tau0;
 	}
 	forEachInner<D>(grid.sizes, [&](const std::array<int, D>& it) {
 		const Real3 x = grid.coords(it);
@@ -244,8 +246,10 @@ void HipMesh<D>::setUpPde(const Task& task) {
 	for (size_t c = 0; c < matrices.size(); c++)
 		if (used[c]) remap[c] = nUsed++;
 	std::vector<real> U((size_t)nUsed * D * M * M), U1(U.size()), L((size_t)nUsed * D * M);
+	deviceTau0_.assign(nUsed, 0);
 	for (size_t c = 0; c < matrices.size(); c++) {
 		if (remap[c] < 0) continue;
+		deviceTau0_[remap[c]] = st.tau0[c];
 		for (int s = 0; s < D; s++) {
 			const size_t o = ((size_t)remap[c] * D + s);
 			std::copy(matrices[c].m[s].U.begin(), matrices[c].m[s].U.end(), U.begin() + o * M * M);
@@ -352,10 +356,10 @@ Engine<D>::Engine(const Task& task, int device_) : AbstractEngine(task), device(
 	createGridsAndContacts(task);
 	for (const auto& tb : task.bodies) {
 		Body& body = getBody(tb.first);
-		if (!tb.second.odes.empty()) throw Exception("ODE correctors are not on this path");
 		body.mesh->setUpPde(task);
 		body.gcm = body.factory->createGcm(task);
 		body.border = body.factory->createBorder(task, body.mesh);
+		for (const Odes::T odeType : tb.second.odes) body.odes.push_back(body.factory->createOde(odeType));
 	}
 	afterConstruction(task);
 }
@@ -444,6 +448,7 @@ void Engine<D>::nextTimeStep() {
 		for (Body& b : bodies)
 			std::static_pointer_cast<HipGridCharacteristicMethod<D>>(b.gcm)->step(
 			    Clock::TimeStep(), dynamic_cast<HipMesh<D>&>(*b.mesh));
+		applyOdes();
 		return;
 	}
 	for (int stage = 0; stage < D; stage++) {
@@ -458,6 +463,22 @@ void Engine<D>::nextTimeStep() {
 			body.mesh->swapCurrAndNextPdeTimeLayer(0);
 		}
 	}
+	applyOdes();
+}
+
+// Engine.cpp:115-119: ODEs after all stages of the step.
+template <int D>
+void Engine<D>::applyOdes() {
+	for (Body& body : bodies)
+		for (auto& ode : body.odes) ode->apply(*body.mesh, Clock::TimeStep());
+}
+
+template <int D>
+void HipMaxwellViscosityOde<D>::apply(AbstractGrid& mesh_, const real timeStep) {
+	HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(mesh_);
+	const auto& tau0 = mesh.deviceTau0();
+	gcmxCheck(gcmx_ode_maxwell(mesh.ctx(), timeStep, tau0.data(), (int)tau0.size()),
+	          "gcmx_ode_maxwell");
 }
 
 // Engine.cpp:124-140
@@ -488,6 +509,9 @@ template class HipBorderConditions<3>;
 template class HipContactCopier<1>;
 template class HipContactCopier<2>;
 template class HipContactCopier<3>;
+template class HipMaxwellViscosityOde<1>;
+template class HipMaxwellViscosityOde<2>;
+template class HipMaxwellViscosityOde<3>;
 template CubicGrid<1>::ConstructionPack constructionPack<1>(const Task&, size_t);
 template CubicGrid<2>::ConstructionPack constructionPack<2>(const Task&, size_t);
 template CubicGrid<3>::ConstructionPack constructionPack<3>(const Task&, size_t);

@@ -124,6 +124,7 @@ struct HostState {
 	std::vector<real> pde;
 	std::vector<uint8_t> matId;
 	std::vector<GcmMatrices<D>> matrices;
+	std::vector<real> tau0;  // IsotropicMaterial::tau0 per material condition
 	real maximalEigenvalue = 0;
 };
 
@@ -156,12 +157,15 @@ public:
 	/// One node's PDE vector (downloads the layer; for tests and snapshots).
 	std::array<real, M> pde(const IntD& it) const;
 	int numberOfMaterials() const { return (int)matrices.size(); }
+	/// tau0 of the materials in the device table order (gcmx_set_materials).
+	const std::vector<real>& deviceTau0() const { return deviceTau0_; }
 
 private:
 	gcmx_ctx* ctx_ = nullptr;
 	int device;
 	real maximalEigenvalue = 0;
 	std::vector<GcmMatrices<D>> matrices;  // one per material condition
+	std::vector<real> deviceTau0_;
 	bool pdeIsSetUp = false;
 };
 
@@ -221,6 +225,21 @@ private:
 	std::array<int, 3> dmin, dmax, smin;
 };
 
+/// rheology/ode/Ode.hpp:16-19
+class AbstractOde {
+public:
+	virtual ~AbstractOde() = default;
+	virtual void apply(AbstractGrid& mesh, const real timeStep) = 0;
+};
+
+/// MaxwellViscosityOde<Mesh> (rheology/ode/Ode.hpp:24-38) on the device:
+/// sigma *= exp(-timeStep / tau0) per node (gcmx_ode_maxwell).
+template <int D>
+class HipMaxwellViscosityOde : public AbstractOde {
+public:
+	void apply(AbstractGrid& mesh, const real timeStep) override;
+};
+
 /// engine/cubic/AbstractFactory.hpp:22-54
 template <int D>
 class AbstractFactoryBase {
@@ -232,6 +251,7 @@ public:
 	virtual std::shared_ptr<GridCharacteristicMethodBase> createGcm(const Task& task) = 0;
 	virtual std::shared_ptr<AbstractBorderConditions> createBorder(
 	    const Task& task, std::shared_ptr<AbstractMesh<D>> mesh) = 0;
+	virtual std::shared_ptr<AbstractOde> createOde(const Odes::T type) = 0;
 };
 
 /// AbstractFactory<ElasticModel<D>, CubicGrid<D>, IsotropicMaterial, HipMesh>
@@ -251,6 +271,14 @@ public:
 	    const Task& task, std::shared_ptr<AbstractMesh<D>> mesh) override {
 		return std::make_shared<HipBorderConditions<D>>(
 		    task, dynamic_cast<const HipMesh<D>&>(*mesh));
+	}
+	/// AbstractFactory.hpp:90-93: every ODE type maps to MaxwellViscosityOde there;
+	/// the other two do not compile in the reference (Ode.hpp:50, 75), so they are
+	/// refused here.
+	std::shared_ptr<AbstractOde> createOde(const Odes::T type) override {
+		if (type != Odes::T::MAXWELL_VISCOSITY)
+			throw Exception("only the Maxwell viscosity ODE is on this path");
+		return std::make_shared<HipMaxwellViscosityOde<D>>();
 	}
 
 private:
@@ -281,12 +309,14 @@ private:
 			std::shared_ptr<HipContactCopier<D>> copier;
 		};
 		std::vector<Contact> contacts;
+		std::vector<std::shared_ptr<AbstractOde>> odes;
 	};
 	std::vector<Body> bodies;
 	int device;
 	Body& getBody(size_t id);
 	const Body& getBody(size_t id) const;
 	void createGridsAndContacts(const Task& task);
+	void applyOdes();
 };
 
 }  // namespace cubic

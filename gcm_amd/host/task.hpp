@@ -40,6 +40,10 @@ struct Materials {
 struct Models {
 	enum class T { ELASTIC, ACOUSTIC };
 };
+/// util/Enum.hpp:153-163
+struct Odes {
+	enum class T { MAXWELL_VISCOSITY, CONTINUAL_DAMAGE, IDEAL_PLASTIC_FLOW };
+};
 struct Grids {
 	enum class T { CUBIC, SIMPLEX };
 };
@@ -152,7 +156,7 @@ struct Task {
 	struct Body {
 		Materials::T materialId = Materials::T::ISOTROPIC;
 		Models::T modelId = Models::T::ELASTIC;
-		std::vector<int> odes;  // Odes::T; none supported on this path
+		std::vector<Odes::T> odes;  // only MAXWELL_VISCOSITY on this path (Ode.hpp:28-37)
 	};
 	std::map<size_t, Body> bodies;
 

@@ -134,6 +134,14 @@ gcmx_status gcmx_border_fill(gcmx_ctx* ctx, int axis, int side, int n_nodes,
 gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dst_min[3], const int dst_max[3],
                           gcmx_ctx* src, const int src_min[3]);
 
+/* Replaces MaxwellViscosityOde<Mesh>::apply (rheology/ode/Ode.hpp:28-37), which
+ * cubic::Engine::nextTimeStep runs after the stages (engine/cubic/Engine.cpp:115-119):
+ * every stress component of every inner node of the current layer is multiplied
+ * by exp(-tau / tau0[m]), m = the node's material (gcmx_set_material_ids).
+ * `tau0`: one decay time per material set with gcmx_set_materials (n_mat of
+ * them).  The factor is computed on the host with the C library's exp. */
+gcmx_status gcmx_ode_maxwell(gcmx_ctx* ctx, double tau, const double* tau0, int n_mat);
+
 /* ---- multi-GPU X-slab halo (replaces the dead MPI slab design,
  * src/test/TestMPI.cpp:33-50, 92-155, and the in-process ContactCopier for
  * bodies split along X) ---------------------------------------------------------*/

@@ -230,6 +230,7 @@ class Material:
     rho: float
     lam: float
     mu: float
+    tau0: float = 0.0  # IsotropicMaterial::tau0 (rheology/materials/IsotropicMaterial.hpp:17)
 
 
 @dataclass
@@ -257,6 +258,7 @@ class Task:
     ic_waves: List[Tuple[tuple, str, int, str, float]] = field(default_factory=list)
     ic_quantities: List[Tuple[tuple, str, float]] = field(default_factory=list)
     border_conditions: Dict[int, List[BorderCondition]] = field(default_factory=dict)
+    odes: Dict[int, List[str]] = field(default_factory=dict)  # Task::Body::odes (Task.hpp:33)
 
 
 class Body:
@@ -320,6 +322,11 @@ class Body:
         if len(conds) > 255:
             raise ValueError("too many material conditions")
         self.tables = [isotropic_elastic_matrices(D, m.rho, m.lam, m.mu) for _, m in conds]
+        self.tau0 = [m.tau0 for _, m in conds]
+        self.odes = list(task.odes.get(self.id, []))
+        for o in self.odes:
+            if o != "MAXWELL_VISCOSITY":
+                raise ValueError("only MaxwellViscosityOde compiles in the reference (Ode.hpp:50, 75)")
         mid = np.zeros(len(its), dtype=np.uint8)
         for ci, (area, _) in enumerate(conds):
             mid[area_contains(area, X, Y, Z)] = ci
@@ -413,6 +420,17 @@ class Body:
             raise ValueError("stage: interpolation out of range (reference assert)")
         self.pde, self.pde_new = self.pde_new, self.pde
 
+    def apply_odes(self, tau: float):
+        """MaxwellViscosityOde::apply (rheology/ode/Ode.hpp:28-37) over the inner nodes:
+        setSigma(getSigma() * exp(-timeStep / tau0)); the factor is the C library's exp of
+        the IEEE quotient, per material (one value per node in the reference, same bits)."""
+        for _ in self.odes:
+            with np.errstate(divide="ignore", invalid="ignore"):
+                f = [math.exp(float(np.float64(-tau) / np.float64(t0))) for t0 in self.tau0]
+            flat = self.flat_index(self.inner_indices())
+            fac = np.array(f)[self.mat_id[flat]]
+            self.pde[flat, self.D:] = self.pde[flat, self.D:] * fac[:, None]
+
     def aabb(self):
         mn = np.array(self.start[:self.D])
         return mn, mn + np.array(self.sizes[:self.D]) - 1
@@ -427,7 +445,7 @@ class Body:
 
 class Engine:
     """cubic::Engine<D> + AbstractEngine (engine/cubic/Engine.cpp:12-140,
-    engine/AbstractEngine.cpp:9-46) without snapshotters and ODEs."""
+    engine/AbstractEngine.cpp:9-46) without snapshotters."""
 
     def __init__(self, task: Task):
         self.task = task
@@ -497,6 +515,8 @@ class Engine:
                     body.pde[fa] = other.pde[fb]
             for b in self.bodies:
                 b.stage(s, tau, nthreads)
+        for b in self.bodies:  # Engine.cpp:115-119
+            b.apply_odes(tau)
 
     def run(self, nthreads: int = 0, max_steps: Optional[int] = None):
         """AbstractEngine::run (AbstractEngine.cpp:30-46)."""

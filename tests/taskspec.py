@@ -4,11 +4,12 @@ from oracle import oracle as O
 
 
 def spec(D, bs, h, cubics, courant, material, inhomogeneities=(), snaps=0, steps_per_snap=1,
-         required_time=0.0, vectors=(), waves=(), quantities=(), borders=None):
+         required_time=0.0, vectors=(), waves=(), quantities=(), borders=None, odes=None):
+    """material tuples: (rho, lambda, mu[, tau0]); odes: {body: ["MAXWELL_VISCOSITY", ..]}."""
     return dict(D=D, bs=bs, h=list(h), cubics=dict(cubics), courant=courant, material=material,
                 inhomogeneities=list(inhomogeneities), snaps=snaps, steps_per_snap=steps_per_snap,
                 required_time=required_time, vectors=list(vectors), waves=list(waves),
-                quantities=list(quantities), borders=borders or {})
+                quantities=list(quantities), borders=borders or {}, odes=odes or {})
 
 
 def oracle_task(s):
@@ -19,7 +20,8 @@ def oracle_task(s):
                   required_time=s["required_time"], ic_vectors=s["vectors"], ic_waves=s["waves"],
                   ic_quantities=s["quantities"],
                   border_conditions={b: [O.BorderCondition(d, a, v) for d, a, v in lst]
-                                     for b, lst in s["borders"].items()})
+                                     for b, lst in s["borders"].items()},
+                  odes={b: list(v) for b, v in s["odes"].items()})
 
 
 def host_task(s):
@@ -46,4 +48,7 @@ def host_task(s):
     for b, lst in s["borders"].items():
         for d, a, v in lst:
             t.add_border_condition(b, d, a, v)
+    for b, lst in s["odes"].items():
+        for o in lst:
+            t.add_ode(b, o)
     return t

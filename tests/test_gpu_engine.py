@@ -181,3 +181,24 @@ def test_engine_bad_courant_raises(H):
     he = H.Engine(host_task(s))
     with pytest.raises(H.GcmException):
         he.run()
+
+
+@pytest.mark.parametrize("D,tau0_b,path", [(3, None, "fused"), (2, 7.0, "generic"), (1, None, "generic"),
+                                           (3, 0.0, "generic")])
+def test_engine_maxwell_ode(H, D, tau0_b, path):
+    """Task bodies with MAXWELL_VISCOSITY (Engine.cpp:28-31, 115-119; Ode.hpp:24-38):
+    Task -> Engine::run on the GPU == the oracle engine, bitwise."""
+    from tests.test_oracle import _maxwell_spec
+    s = _maxwell_spec(D, 3.0, tau0_b)
+    he = H.Engine(host_task(s))
+    assert he.path(0) == path
+    oe, he = run_both(H, s)
+    assert_bodies_equal(oe, he, s)
+
+
+def test_engine_rejects_uncompilable_odes(H):
+    """Only MaxwellViscosityOde compiles in the reference (Ode.hpp:50, 75)."""
+    s = spec(2, 2, [1, 1], {0: ([8, 8], [0, 0])}, 0.9, (4, 2, 1), snaps=1,
+             odes={0: ["CONTINUAL_DAMAGE"]})
+    with pytest.raises(Exception):
+        H.Engine(host_task(s))

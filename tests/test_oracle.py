@@ -363,3 +363,43 @@ def test_random_field_is_splitmix():
     assert -1.0 <= v < 1.0
     assert O.splitmix_uniform(0x5EED, 0) == v
     assert O.splitmix_uniform(0x5EED, 1) != v
+
+
+# ------------------------------------------------------------ Maxwell ODE --
+# MaxwellViscosityOde (rheology/ode/Ode.hpp:24-38), applied by cubic::Engine after
+# the stages of every step (engine/cubic/Engine.cpp:115-119).  The reference has
+# no test of its own for it: parity unpinned beyond the defining identity below.
+
+def _maxwell_spec(D, tau0_a, tau0_b=None):
+    from tests.taskspec import spec
+    N = [12] * D
+    inh = []
+    if tau0_b is not None:
+        inh = [(("box", (-1, -1, -1), (5.5, 100, 100)), (4, 2, 1, tau0_b))]
+    return spec(D, 2, [1.0] * D, {0: (N, [0] * D)}, 0.9, (4, 2, 1, tau0_a), inhomogeneities=inh,
+                snaps=3, quantities=[(("sphere", 3.0, (6.0,) * 3), "PRESSURE", 2.0)],
+                vectors=[(("box", (2, 2, 2), (9, 9, 9)), [0.5] * O.pde_size(D))],
+                odes={0: ["MAXWELL_VISCOSITY"]})
+
+
+@pytest.mark.parametrize("D,tau0_b", [(1, None), (2, 7.0), (3, None), (3, 0.0)])
+def test_maxwell_ode_scales_stress_after_each_step(D, tau0_b):
+    """One step with the ODE == the same step without it, then every stress component
+    of every inner node times exp(-tau / tau0[material]) (tau0 = 0 gives 0)."""
+    from tests.taskspec import oracle_task
+    s = _maxwell_spec(D, 3.0, tau0_b)
+    with_ode = O.Engine(oracle_task(s))
+    s2 = dict(s); s2["odes"] = {}
+    plain = O.Engine(oracle_task(s2))
+    for _ in range(2):
+        with_ode.run(max_steps=with_ode.steps_done + 1)
+        plain.run(max_steps=plain.steps_done + 1)
+        b, p = with_ode.bodies[0], plain.bodies[0]
+        tau = with_ode.time_step
+        flat = b.flat_index(b.inner_indices())
+        for node in flat[:: max(1, len(flat) // 97)]:
+            t0 = b.tau0[b.mat_id[node]]
+            f = math.exp(-tau / t0) if t0 != 0 else 0.0
+            assert np.array_equal(b.pde[node, :D], p.pde[node, :D])
+            assert np.array_equal(b.pde[node, D:], p.pde[node, D:] * f)
+        p.pde[:] = b.pde  # continue both from the same state
