@@ -110,6 +110,24 @@ py::dict hostState(const Task& task, size_t id) {
 	return d;
 }
 
+/// VtkSnapshotter's file for body `id` without a GPU: the set-up layer of the
+/// task, or `pde` (all nodes incl. ghosts, [..., M]) when given.
+template <int D>
+void writeVtkHost(const Task& task, size_t id, const std::string& fileName, py::object pde) {
+	cubic::CubicGrid<D> grid(id, cubic::constructionPack<D>(task, id));
+	auto st = cubic::buildHostState<D>(task, grid);
+	std::vector<real> layer = st.pde;
+	if (!pde.is_none()) {
+		auto a = pde.cast<py::array_t<real, py::array::c_style | py::array::forcecast>>();
+		if ((size_t)a.size() != layer.size()) throw Exception("write_vtk: pde has the wrong size");
+		std::copy(a.data(), a.data() + a.size(), layer.begin());
+	}
+	makeParentDirectories(fileName);
+	cubic::writeVtkSnapshot<D>(fileName, grid.sizes, grid.start, grid.h, grid.borderSize,
+	                           layer.data(), st.matId.data(), st.materialNumber,
+	                           task.vtkSnapshotter.quantitiesToSnap);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_gcm_host, m) {
@@ -138,18 +156,20 @@ PYBIND11_MODULE(_gcm_host, m) {
 		         t.cubicGrid.cubics[id] = {sizes, start};
 	         })
 	    .def("set_default_material",
-	         [](Task& t, real rho, real lam, real mu, real tau0) {
+	         [](Task& t, real rho, real lam, real mu, real tau0, int number) {
 		         t.materialConditions.type = Task::MaterialCondition::Type::BY_AREAS;
 		         t.materialConditions.byAreas.defaultMaterial =
-		             std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, 0, tau0);
+		             std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, number, tau0);
 	         },
-	         py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0)
+	         py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0,
+	         py::arg("number") = 0)
 	    .def("add_material",
-	         [](Task& t, py::tuple area, real rho, real lam, real mu, real tau0) {
+	         [](Task& t, py::tuple area, real rho, real lam, real mu, real tau0, int number) {
 		         t.materialConditions.byAreas.materials.push_back(
-		             {makeArea(area), std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, 0, tau0)});
+		             {makeArea(area), std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, number, tau0)});
 	         },
-	         py::arg("area"), py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0)
+	         py::arg("area"), py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0,
+	         py::arg("number") = 0)
 	    .def("set_body_material",
 	         [](Task& t, size_t id, real rho, real lam, real mu, real tau0) {
 		         t.materialConditions.type = Task::MaterialCondition::Type::BY_BODIES;
@@ -157,6 +177,27 @@ PYBIND11_MODULE(_gcm_host, m) {
 		             std::make_shared<IsotropicMaterial>(rho, lam, mu, 0, 0, 0, tau0);
 	         },
 	         py::arg("id"), py::arg("rho"), py::arg("lam"), py::arg("mu"), py::arg("tau0") = 0.0)
+	    .def_property("output_directory", [](Task& t) { return t.globalSettings.outputDirectory; },
+	                  [](Task& t, const std::string& d) { t.globalSettings.outputDirectory = d; })
+	    .def("add_snapshotter",
+	         [](Task& t, const std::string& name) {
+		         if (name == "VTK") t.globalSettings.snapshottersId.push_back(Snapshotters::T::VTK);
+		         else if (name == "SLICESNAP") t.globalSettings.snapshottersId.push_back(Snapshotters::T::SLICESNAP);
+		         else if (name == "DETECTOR") t.globalSettings.snapshottersId.push_back(Snapshotters::T::DETECTOR);
+		         else throw Exception("unknown snapshotter " + name);
+	         })
+	    .def("set_vtk_quantities",
+	         [](Task& t, std::vector<std::string> qs) {
+		         t.vtkSnapshotter.quantitiesToSnap.clear();
+		         for (auto& q : qs) t.vtkSnapshotter.quantitiesToSnap.push_back(quantity(q));
+	         })
+	    .def("set_detector",
+	         [](Task& t, std::vector<std::string> qs, py::tuple area, size_t gridId) {
+		         t.detector.quantities.clear();
+		         for (auto& q : qs) t.detector.quantities.push_back(quantity(q));
+		         t.detector.area = makeArea(area);
+		         t.detector.gridId = gridId;
+	         })
 	    .def("add_ode",
 	         [](Task& t, size_t id, const std::string& name) {
 		         if (!t.bodies.count(id)) throw Exception("add_ode: no such body");
@@ -198,6 +239,18 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    },
 	    "GPU-free MaterialsCondition + InitialCondition set-up of one body", py::arg("task"),
 	    py::arg("body_id"));
+
+	m.def(
+	    "write_vtk",
+	    [](const Task& t, size_t id, const std::string& fileName, py::object pde) {
+		    const int D = t.globalSettings.dimensionality;
+		    if (D == 1) return writeVtkHost<1>(t, id, fileName, pde);
+		    if (D == 2) return writeVtkHost<2>(t, id, fileName, pde);
+		    if (D == 3) return writeVtkHost<3>(t, id, fileName, pde);
+		    throw Exception("dimensionality must be 1, 2 or 3");
+	    },
+	    "GPU-free VtkSnapshotter file of one body (set-up layer, or `pde`)", py::arg("task"),
+	    py::arg("body_id"), py::arg("file_name"), py::arg("pde") = py::none());
 
 	py::class_<PyEngine>(m, "Engine")
 	    .def(py::init([](const Task& t, int device) {

@@ -31,13 +31,17 @@ void AbstractEngine::afterConstruction(const Task& task) {
 	if (!(requiredTime > 0)) throw Exception("requiredTime must be > 0");
 }
 
-// AbstractEngine.cpp:30-46 (snapshots are out of scope on this path)
+// AbstractEngine.cpp:30-46
 void AbstractEngine::run() {
+	int step = 0;
+	writeSnapshots(step);
 	while (Clock::Time() < requiredTime) {
 		Clock::timeStep = estimateTimeStep();
 		nextTimeStep();
+		step++;
 		steps++;
 		Clock::tickTack();
+		writeSnapshots(step);
 	}
 }
 
@@ -180,6 +184,7 @@ HostState<D> buildHostState(const Task& task, const CubicGrid<D>& grid) {
 		if (!conds[c].second) throw Exception("material condition without a material");
 		ElasticModel<D>::constructGcmMatrices(matrices[c], *conds[c].second);
 		st.tau0[c] = conds[c].second->tau0;
+		st.materialNumber.push_back(conds[c].second->materialNumber);
 	}
 	forEachInner<D>(grid.sizes, [&](const std::array<int, D>& it) {
 		const Real3 x = grid.coords(it);
@@ -237,6 +242,8 @@ void HipMesh<D>::setUpPde(const Task& task) {
 	matrices = st.matrices;
 	maximalEigenvalue = st.maximalEigenvalue;
 	auto& matId = st.matId;
+	materialNumbers_ = st.materialNumber;
+	if (matrices.size() > 1) matIdAll_ = matId;  // before the device remap below
 
 	// ---- device tables: only the materials the nodes actually use
 	std::vector<int> used(matrices.size(), 0);
@@ -359,6 +366,8 @@ Engine<D>::Engine(const Task& task, int device_) : AbstractEngine(task), device(
 		body.mesh->setUpPde(task);
 		body.gcm = body.factory->createGcm(task);
 		body.border = body.factory->createBorder(task, body.mesh);
+		for (const Snapshotters::T snapType : task.globalSettings.snapshottersId)
+			body.snapshotters.push_back(body.factory->createSnapshotter(task, snapType));
 		for (const Odes::T odeType : tb.second.odes) body.odes.push_back(body.factory->createOde(odeType));
 	}
 	afterConstruction(task);
@@ -474,6 +483,73 @@ void Engine<D>::applyOdes() {
 }
 
 template <int D>
+void Engine<D>::writeSnapshots(const int step) {
+	for (Body& body : bodies)
+		for (auto& snap : body.snapshotters) snap->snapshot(body.mesh.get(), step);
+}
+
+// ------------------------------------------------------------- snapshotters --
+
+template <int D>
+void VtkSnapshotter<D>::snapshotImpl(const AbstractGrid* mesh_, const int step) {
+	const HipMesh<D>* mesh = dynamic_cast<const HipMesh<D>*>(mesh_);
+	if (!mesh) throw Exception("VtkSnapshotter: not a cubic mesh");
+	const std::vector<real> pde = mesh->pdeAll();  // the one device -> host copy
+	const auto& ids = mesh->materialIdsAll();
+	writeVtkSnapshot<D>(makeFileNameForSnapshot(std::to_string(mesh->id), step, "vts", "vtk"),
+	                    mesh->sizes, mesh->start, mesh->h, mesh->borderSize, pde.data(),
+	                    ids.empty() ? nullptr : ids.data(), mesh->materialNumbers(),
+	                    quantitiesToSnap);
+}
+
+template <int D>
+SliceSnapshotter<D>::SliceSnapshotter(const Task& task) : Snapshotter(task) {
+	if (task.detector.quantities.size() != 1)  // SliceSnapshotter.hpp:31
+		throw Exception("SliceSnapshotter: exactly one detector quantity is supported");
+	quantityToWrite = task.detector.quantities[0];
+	detectionArea = task.detector.area;
+	gridId = task.detector.gridId;
+	if (!detectionArea) throw Exception("SliceSnapshotter: detector area missing");
+}
+
+template <int D>
+void SliceSnapshotter<D>::snapshotImpl(const AbstractGrid* mesh_, const int step) {
+	const HipMesh<D>* mesh = dynamic_cast<const HipMesh<D>*>(mesh_);
+	if (!mesh) throw Exception("SliceSnapshotter: not a cubic mesh");
+	constexpr int M = pdeSize(D);
+	const int direction = D - 1;
+	const std::vector<real> pde = mesh->pdeAll();
+	auto at = [&](const std::array<int, D>& it) { return &pde[(size_t)mesh->getIndex(it) * M]; };
+	// along the last axis through sizes / 2 (SliceSnapshotter.hpp:45-63)
+	std::array<int, D> it;
+	for (int i = 0; i < D; i++) it[i] = mesh->sizes[i] / 2;
+	std::vector<real> coordZ, Vz;
+	for (int k = 0; k < mesh->sizes[direction]; k++) {
+		it[direction] = k;
+		coordZ.push_back(mesh->coords(it)[direction]);
+		Vz.push_back(at(it)[direction]);
+	}
+	writeColumns(makeFileNameForSnapshot(std::to_string(mesh->id), step, "txt", "zaxis"),
+	             {coordZ, Vz});
+	if (mesh->id != gridId) return;
+	// upper detector: mean over the right border of the last axis (hpp:65-88)
+	std::vector<real> valuesInArea;
+	forEachInner<D>(mesh->sizes, [&](const std::array<int, D>& j) {
+		if (j[direction] != mesh->sizes[direction] - 1) return;
+		if (detectionArea->contains(mesh->coords(j)))
+			valuesInArea.push_back(getQuantity(D, quantityToWrite, at(j)));
+	});
+	if (valuesInArea.empty()) throw Exception("SliceSnapshotter: no node in the detection area");
+	real sum = 0;
+	for (real v : valuesInArea) sum += v;  // std::accumulate order
+	const real valueToWrite = sum / (real)valuesInArea.size();
+	times.push_back(Clock::Time());
+	seismo.push_back((precision)valueToWrite);
+	writeColumns(makeFileNameForSnapshot(std::to_string(mesh->id), step, "txt", "detector"),
+	             {times, seismo});
+}
+
+template <int D>
 void HipMaxwellViscosityOde<D>::apply(AbstractGrid& mesh_, const real timeStep) {
 	HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(mesh_);
 	const auto& tau0 = mesh.deviceTau0();
@@ -509,6 +585,12 @@ template class HipBorderConditions<3>;
 template class HipContactCopier<1>;
 template class HipContactCopier<2>;
 template class HipContactCopier<3>;
+template class VtkSnapshotter<1>;
+template class VtkSnapshotter<2>;
+template class VtkSnapshotter<3>;
+template class SliceSnapshotter<1>;
+template class SliceSnapshotter<2>;
+template class SliceSnapshotter<3>;
 template class HipMaxwellViscosityOde<1>;
 template class HipMaxwellViscosityOde<2>;
 template class HipMaxwellViscosityOde<3>;

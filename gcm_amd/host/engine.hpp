@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/gcmx.h"
+#include "snapshot.hpp"
 #include "task.hpp"
 
 namespace gcm {
@@ -58,6 +59,7 @@ protected:
 	void afterConstruction(const Task& task);
 	virtual void nextTimeStep() = 0;
 	virtual real estimateTimeStep() = 0;
+	virtual void writeSnapshots(const int step) = 0;
 };
 
 /// grid/AbstractGrid.hpp -- what stage()/apply() receive and downcast.
@@ -125,6 +127,7 @@ struct HostState {
 	std::vector<uint8_t> matId;
 	std::vector<GcmMatrices<D>> matrices;
 	std::vector<real> tau0;  // IsotropicMaterial::tau0 per material condition
+	std::vector<int> materialNumber;  // IsotropicMaterial::materialNumber per condition
 	real maximalEigenvalue = 0;
 };
 
@@ -159,6 +162,10 @@ public:
 	int numberOfMaterials() const { return (int)matrices.size(); }
 	/// tau0 of the materials in the device table order (gcmx_set_materials).
 	const std::vector<real>& deviceTau0() const { return deviceTau0_; }
+	/// Material-condition index per node (all-nodes order) and the conditions'
+	/// IsotropicMaterial::materialNumber (DefaultMesh::material(it), for snapshots).
+	const std::vector<uint8_t>& materialIdsAll() const { return matIdAll_; }
+	const std::vector<int>& materialNumbers() const { return materialNumbers_; }
 
 private:
 	gcmx_ctx* ctx_ = nullptr;
@@ -166,6 +173,8 @@ private:
 	real maximalEigenvalue = 0;
 	std::vector<GcmMatrices<D>> matrices;  // one per material condition
 	std::vector<real> deviceTau0_;
+	std::vector<uint8_t> matIdAll_;
+	std::vector<int> materialNumbers_;
 	bool pdeIsSetUp = false;
 };
 
@@ -240,6 +249,39 @@ public:
 	void apply(AbstractGrid& mesh, const real timeStep) override;
 };
 
+/// VtkSnapshotter<Mesh> (util/snapshot/VtkSnapshotter.hpp:12-86): one .vts per
+/// snapshot under snapshots[/outDir]/vtk/.
+template <int D>
+class VtkSnapshotter : public Snapshotter {
+public:
+	explicit VtkSnapshotter(const Task& task)
+	    : Snapshotter(task), quantitiesToSnap(task.vtkSnapshotter.quantitiesToSnap) {}
+
+protected:
+	void snapshotImpl(const AbstractGrid* mesh, const int step) override;
+
+private:
+	const std::vector<PhysicalQuantities::T> quantitiesToSnap;
+};
+
+/// SliceSnapshotter<Mesh> (util/snapshot/SliceSnapshotter.hpp:12-118): velocity
+/// along the last axis through the centre into snapshots/../zaxis/*.txt, and the
+/// mean detector quantity over the top face (last axis) into ../detector/*.txt.
+template <int D>
+class SliceSnapshotter : public Snapshotter {
+public:
+	explicit SliceSnapshotter(const Task& task);
+
+protected:
+	void snapshotImpl(const AbstractGrid* mesh, const int step) override;
+
+private:
+	size_t gridId;
+	std::vector<real> times, seismo;
+	std::shared_ptr<Area> detectionArea;
+	PhysicalQuantities::T quantityToWrite;
+};
+
 /// engine/cubic/AbstractFactory.hpp:22-54
 template <int D>
 class AbstractFactoryBase {
@@ -252,6 +294,8 @@ public:
 	virtual std::shared_ptr<AbstractBorderConditions> createBorder(
 	    const Task& task, std::shared_ptr<AbstractMesh<D>> mesh) = 0;
 	virtual std::shared_ptr<AbstractOde> createOde(const Odes::T type) = 0;
+	virtual std::shared_ptr<Snapshotter> createSnapshotter(const Task& task,
+	                                                       const Snapshotters::T type) = 0;
 };
 
 /// AbstractFactory<ElasticModel<D>, CubicGrid<D>, IsotropicMaterial, HipMesh>
@@ -280,6 +324,15 @@ public:
 			throw Exception("only the Maxwell viscosity ODE is on this path");
 		return std::make_shared<HipMaxwellViscosityOde<D>>();
 	}
+	/// AbstractFactory.hpp:95-105
+	std::shared_ptr<Snapshotter> createSnapshotter(const Task& task,
+	                                               const Snapshotters::T type) override {
+		switch (type) {
+		case Snapshotters::T::VTK: return std::make_shared<VtkSnapshotter<D>>(task);
+		case Snapshotters::T::SLICESNAP: return std::make_shared<SliceSnapshotter<D>>(task);
+		default: throw Exception("Unknown or unsupported snapshotter");
+		}
+	}
 
 private:
 	int device;
@@ -296,6 +349,7 @@ public:
 protected:
 	void nextTimeStep() override;
 	real estimateTimeStep() override;
+	void writeSnapshots(const int step) override;
 
 private:
 	struct Body {
@@ -310,6 +364,7 @@ private:
 		};
 		std::vector<Contact> contacts;
 		std::vector<std::shared_ptr<AbstractOde>> odes;
+		std::vector<std::shared_ptr<Snapshotter>> snapshotters;
 	};
 	std::vector<Body> bodies;
 	int device;

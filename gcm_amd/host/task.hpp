@@ -40,6 +40,10 @@ struct Materials {
 struct Models {
 	enum class T { ELASTIC, ACOUSTIC };
 };
+/// util/Enum.hpp:136-147
+struct Snapshotters {
+	enum class T { VTK, DETECTOR, SLICESNAP };
+};
 /// util/Enum.hpp:153-163
 struct Odes {
 	enum class T { MAXWELL_VISCOSITY, CONTINUAL_DAMAGE, IDEAL_PLASTIC_FLOW };
@@ -168,6 +172,8 @@ struct Task {
 		int stepsPerSnap = 1;
 		real requiredTime = 0;
 		bool verboseTimeSteps = false;
+		std::vector<Snapshotters::T> snapshottersId;
+		std::string outputDirectory = "";
 	} globalSettings;
 
 	struct CubicGrid {
@@ -225,6 +231,17 @@ struct Task {
 		Values values;
 	};
 	std::map<size_t, std::vector<CubicBorderCondition>> cubicBorderConditions;
+
+	struct VtkSnapshotter {
+		/// list of physical quantities to write to vtk
+		std::vector<PhysicalQuantities::T> quantitiesToSnap;
+	} vtkSnapshotter;
+
+	struct Detector {
+		std::vector<PhysicalQuantities::T> quantities;
+		std::shared_ptr<Area> area;
+		size_t gridId = 0;
+	} detector;
 };
 
 }  // namespace gcm

@@ -68,3 +68,26 @@ def seq_sum(a):
     for x in np.asarray(a).reshape(-1).tolist():
         s += x
     return s
+
+
+def read_vts(path):
+    """Parse a VTK XML StructuredGrid file with appended raw data (UInt64 headers,
+    Float32 arrays) as gcm_amd's VtkSnapshotter writes it.  Returns
+    (dims, {name: array [n, components]}, points [n, 3]); points in VTK order."""
+    import re
+    raw = open(path, "rb").read()
+    head, _, rest = raw.partition(b"<AppendedData encoding=\"raw\">")
+    text = head.decode()
+    m = re.search(r'WholeExtent="([^"]+)"', text)
+    ext = [int(v) for v in m.group(1).split()]
+    dims = (ext[1] + 1, ext[3] + 1, ext[5] + 1)
+    data = rest[rest.index(b"_") + 1:]
+    arrays = {}
+    for name, comps, off in re.findall(
+            r'<DataArray type="Float32" Name="([^"]+)" NumberOfComponents="(\d+)" '
+            r'format="appended" offset="(\d+)"/>', text):
+        off = int(off)
+        nbytes = int(np.frombuffer(data[off:off + 8], dtype="<u8")[0])
+        arrays[name] = np.frombuffer(data[off + 8:off + 8 + nbytes], dtype="<f4").reshape(-1, int(comps))
+    points = arrays.pop("Points")
+    return dims, arrays, points

@@ -202,3 +202,51 @@ def test_engine_rejects_uncompilable_odes(H):
              odes={0: ["CONTINUAL_DAMAGE"]})
     with pytest.raises(Exception):
         H.Engine(host_task(s))
+
+
+def test_engine_snapshotters(H, tmp_path, monkeypatch):
+    """AbstractEngine::run with VTK and SLICESNAP snapshotters (AbstractEngine.cpp:30-46,
+    Snapshotter.hpp:46-77, VtkSnapshotter.hpp:26-77, SliceSnapshotter.hpp:37-90):
+    file set, .vts contents, z-axis slice and detector series == the oracle's states."""
+    from tests.helpers import read_vts
+    from tests.test_snapshot_cpu import _expected
+    monkeypatch.chdir(tmp_path)
+    N = 12
+    s = spec(3, 2, [1, 1, 1], {0: ([N] * 3, [0] * 3)}, 0.9, (4, 2, 1), snaps=3, steps_per_snap=2,
+             quantities=[(("sphere", 3.0, (6.0, 6.0, 6.0)), "PRESSURE", 10.0)])
+    t = host_task(s)
+    t.add_snapshotter("VTK")
+    t.add_snapshotter("SLICESNAP")
+    t.set_vtk_quantities(["PRESSURE"])
+    t.set_detector(["Szz"], ("box", (-1, -1, -1), (7.5, 100, 100)), 0)
+    t.output_directory = "out"
+    he = H.Engine(t)
+    he.run()
+    assert he.steps == 6
+    oe = O.Engine(oracle_task(s))
+    times, seismo, time = [], [], 0.0
+    for step in range(7):
+        if step:
+            oe.run(max_steps=step)
+            time += oe.time_step
+        if step % 2:
+            continue
+        b = oe.bodies[0]
+        stem = f"snapshots/out/%s/mesh0core00snap{step:04d}"
+        dims, arrays, points = read_vts(stem % "vtk" + ".vts")
+        vel, pts, q, _ = _expected(b, [("PRESSURE", "pressure")])
+        assert np.array_equal(arrays["Velocity"], vel) and np.array_equal(points, pts)
+        assert np.array_equal(arrays["pressure"][:, 0], q["pressure"])
+        inn = b.inner_view()
+        col = inn[N // 2, N // 2, :, 2]
+        want = "".join(f"{float(z):g}\t{float(v):g}\t\n" for z, v in zip(range(N), col))
+        assert open(stem % "zaxis" + ".txt").read() == want
+        face = inn[:, :, N - 1, 8]  # Szz on the top face, x < 7.5
+        vals = [float(face[x, y]) for x in range(N) for y in range(N) if x < 7.5]
+        acc = 0.0
+        for v in vals:
+            acc += v
+        times.append(time)
+        seismo.append(float(np.float32(acc / len(vals))))
+        want = "".join(f"{a:g}\t{c:g}\t\n" for a, c in zip(times, seismo))
+        assert open(stem % "detector" + ".txt").read() == want
