@@ -4,6 +4,7 @@
 // (engine/cubic/GridCharacteristicMethod.hpp:42-52) through node_update (iso.hpp).
 #include "iso.hpp"
 
+#include <cstring>
 #include <type_traits>
 
 namespace gcmx {
@@ -35,7 +36,7 @@ namespace gcmx {
 #define GCMX_XYZ_MINWAVES 4
 #endif
 #ifndef GCMX_XYZ_CHUNK
-#define GCMX_XYZ_CHUNK 64
+#define GCMX_XYZ_CHUNK 128
 #endif
 #ifndef GCMX_XYZ_ROTATE
 #define GCMX_XYZ_ROTATE 1
@@ -45,6 +46,12 @@ namespace gcmx {
 #endif
 #ifndef GCMX_XYZ_GROUPED
 #define GCMX_XYZ_GROUPED 2
+#endif
+#ifndef GCMX_XYZ_UNI
+#define GCMX_XYZ_UNI 1
+#endif
+#ifndef GCMX_XYZ_SWIZZLE
+#define GCMX_XYZ_SWIZZLE 1
 #endif
 #ifndef GCMX_XYZ_SCHED_BARRIER
 #define GCMX_XYZ_SCHED_BARRIER 1
@@ -77,10 +84,15 @@ namespace gcmx {
 #define GCMX_DIAG_NOBAR 0
 #endif
 
-template <int BS, int ZT, bool KF0>
+// UNI: the launch has Z == ZT (no idle lanes) and the three axes' tables are
+// identical (isotropic medium, equal h): one IsoAxis in scalar registers for all
+// three stages and no idle-lane selects.
+template <int BS, int ZT, bool KF0, bool UNI>
 __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
-    const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY,
-    IsoAxis AZ, int x0, int chunk) {
+    const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY_,
+    IsoAxis AZ_, int x0, int chunk, int nplanes) {
+	const IsoAxis& AY = UNI ? AX : AY_;
+	const IsoAxis& AZ = UNI ? AX : AZ_;
 	constexpr unsigned WMX = iso_window(0);
 	constexpr unsigned CMX = iso_center_only(0);
 	constexpr int NWX = popc9(WMX);
@@ -95,9 +107,24 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 	__shared__ double lds[2][NWZ][LW];
 
 	const int z = threadIdx.x;
-	const int x = x0 + blockIdx.y;
 	const int Y = g.sizes[1], Z = g.sizes[2];
+#if GCMX_XYZ_SWIZZLE && !GCMX_DIAG_HALFZ
+	// 1-D grid of nchunks * nplanes blocks.  Blocks are dealt round-robin over
+	// the 8 XCDs (b % 8 share one, MI355X_MICROARCH.md §Workgroup dispatch): give
+	// each XCD a contiguous run of (chunk, plane) pairs in chunk-major order, so
+	// the 2*BS+1 x-neighbour planes a block re-reads were loaded by blocks of the
+	// same XCD, i.e. hit its L2.  Placement only; any mapping is correct.
+	int x, yb;
+	{
+		const int nx = (int)nplanes, T = (int)gridDim.x, b = (int)blockIdx.x;
+		const int p = (T % 8 == 0) ? (b % 8) * (T / 8) + b / 8 : b;
+		x = x0 + p % nx;
+		yb = (p / nx) * chunk;
+	}
+#else
+	const int x = x0 + blockIdx.y;
 	const int yb = blockIdx.x * chunk;
+#endif
 	const int ye = min(yb + chunk, Y);
 #if GCMX_DIAG_HALFZ  // diagnostic: ZT-wide z tiles, no halo (wrong at tile edges)
 	const unsigned zoff = blockIdx.z * ZT;
@@ -106,7 +133,7 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 	const unsigned zoff = 0;
 	const int ZL = Z;
 #endif
-	const bool live = z < ZL;
+	const bool live = UNI || z < ZL;
 	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
 	const unsigned stx = (unsigned)g.stride[0];
 	const unsigned sty = (unsigned)g.stride[1];
@@ -175,14 +202,12 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #endif
 	};
 	// (split so that the first pair's loads can be issued ahead of the stores)
-	auto x_stage_grouped_rest = [&](PairWin& wa, int r, double (&xr)[9]) {
+	auto x_stage_grouped_ab = [&](PairWin& wa, PairWin& wb, int r, double (&xr)[9]) {
 		const unsigned o = base + (unsigned)r * sty;
 		using P0 = std::integral_constant<int, 0>;
 		using P1 = std::integral_constant<int, 1>;
 		using P2 = std::integral_constant<int, 2>;
 		double rr[9], n0[9], cv[9];
-		PairWin wb;
-		pair_load(P1{}, wb, o);
 		pair_update<0, BS, KF0, 0>(AX, pair_acc(P0{}, wa), rr[0], rr[1]);
 		n0[pair_vel(0, 0)] = wa[0][BS];
 		n0[pair_sig(0, 0)] = wa[1][BS];
@@ -201,6 +226,11 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		sched_fence();
 		center_update<0>(AX, [&](int j) { return ((WMX >> j) & 1u) ? n0[j] : cv[j]; }, rr);
 		u1_apply<0>(AX, rr, xr);
+	};
+	auto x_stage_grouped_rest = [&](PairWin& wa, int r, double (&xr)[9]) {
+		PairWin wb;
+		pair_load(std::integral_constant<int, 1>{}, wb, base + (unsigned)r * sty);
+		x_stage_grouped_ab(wa, wb, r, xr);
 	};
 	auto x_load_a = [&](PairWin& wa, int r) {
 		pair_load(std::integral_constant<int, 0>{}, wa, base + (unsigned)r * sty);
@@ -271,8 +301,11 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #if !GCMX_DIAG_NOBAR
 		__syncthreads();
 #endif
-#if GCMX_XYZ_GROUPED == 2
+#if GCMX_XYZ_GROUPED >= 2
 		PairWin wa_next;
+#endif
+#if GCMX_XYZ_GROUPED == 3
+		PairWin wb_next;
 #endif
 		{
 			double zv[9];
@@ -287,6 +320,12 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #if GCMX_XYZ_GROUPED == 2  // next row's first pair: loads older than this row's stores
 			sched_fence();
 			x_load_a(wa_next, clamp_row(y + BS + 1));
+			sched_fence();
+#elif GCMX_XYZ_GROUPED == 3  // first two pairs ahead of the stores
+			sched_fence();
+			x_load_a(wa_next, clamp_row(y + BS + 1));
+			pair_load(std::integral_constant<int, 1>{}, wb_next,
+			          base + (unsigned)clamp_row(y + BS + 1) * sty);
 			sched_fence();
 #endif
 #if GCMX_DIAG_NOSTORE  // diagnostic: keep the work, drop the stores
@@ -306,7 +345,12 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
 		{  // X stage of row y+BS+1 (zero ghost rows give zero) -> window slot W-1
 			double xr[9];
-#if GCMX_XYZ_GROUPED == 2
+#if GCMX_XYZ_GROUPED == 3
+			sched_fence();
+			x_stage_grouped_ab(wa_next, wb_next, clamp_row(y + BS + 1), xr);
+			push(xr, W - 1);
+			sched_fence();
+#elif GCMX_XYZ_GROUPED == 2
 			sched_fence();
 			x_stage_grouped_rest(wa_next, clamp_row(y + BS + 1), xr);
 			push(xr, W - 1);
@@ -412,21 +456,35 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 
 // ------------------------------------------------------------- launchers --
 
+static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
+	static_assert(sizeof(IsoAxis) == 12 * 8 + 2 * 4, "IsoAxis has padding");
+	return std::memcmp(&p, &q, sizeof(IsoAxis)) == 0;
+}
+
 static int xyz_chunk(int Y) { return Y <= GCMX_XYZ_CHUNK ? Y : GCMX_XYZ_CHUNK; }
 
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                          int x1, hipStream_t st) {
 	const int chunk = xyz_chunk(g.sizes[1]);
-	dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0);
+	const int nchunks = (g.sizes[1] + chunk - 1) / chunk;
+#if GCMX_XYZ_SWIZZLE && !GCMX_DIAG_HALFZ
+	dim3 grid(nchunks * (x1 - x0));
+#else
+	dim3 grid(nchunks, x1 - x0);
+#endif
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
-	if (kf0)
-		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
-		                   a[2], x0, chunk);
+	const bool uni = GCMX_XYZ_UNI && kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
+	if (uni)
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true, true>), grid, dim3(ZT), 0, st, in, out, g, a[0],
+		                   a[1], a[2], x0, chunk, x1 - x0);
+	else if (kf0)
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true, false>), grid, dim3(ZT), 0, st, in, out, g, a[0],
+		                   a[1], a[2], x0, chunk, x1 - x0);
 	else
-		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, false>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
-		                   a[2], x0, chunk);
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, false, false>), grid, dim3(ZT), 0, st, in, out, g,
+		                   a[0], a[1], a[2], x0, chunk, x1 - x0);
 }
 
 template <int BS>
@@ -450,8 +508,8 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	{
 		const int chunk = xyz_chunk(g.sizes[1]);
 		dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0, 2);
-		hipLaunchKernelGGL((k_fused_xyz<2, 256, true>), grid, dim3(256), 0, st, in, out, g, a[0], a[1],
-		                   a[2], x0, chunk);
+		hipLaunchKernelGGL((k_fused_xyz<2, 256, true, false>), grid, dim3(256), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk, x1 - x0);
 		return true;
 	}
 #endif
