@@ -26,6 +26,14 @@ gcmx_status fail(gcmx_status s, const std::string& msg) {
 	return s;
 }
 
+}  // namespace
+
+namespace gcmx {
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace gcmx
+
+namespace {
+
 #define HIP_TRY(expr)                                                                   \
 	do {                                                                                \
 		hipError_t e_ = (expr);                                                         \

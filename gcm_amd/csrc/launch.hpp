@@ -3,7 +3,12 @@
 
 #include "common.hpp"
 
+#include <string>
+
 namespace gcmx {
+
+// gcmx.hip: gcmx_last_error() of the calling thread (shared by every ABI file).
+void set_last_error(const std::string& msg);
 
 // kernels_generic.hip
 bool launch_stage_generic(const double* cur, double* nxt, const Geo& g, int s,

@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include "engine.hpp"
+#include "simplex.hpp"
 
 namespace py = pybind11;
 using namespace gcm;
@@ -128,6 +129,67 @@ void writeVtkHost(const Task& task, size_t id, const std::string& fileName, py::
 	                           task.vtkSnapshotter.quantitiesToSnap);
 }
 
+/// GPU-free simplex set-up (simplex::buildHostPlans) as numpy arrays.
+py::dict simplexPlans(const Task& task) {
+	using namespace simplex;
+	const HostPlans p = buildHostPlans(task);
+	const ssize_t nv = p.mesh.nVertices(), nc = (ssize_t)p.mesh.cells.size();
+	py::array_t<double> coords({nv, (ssize_t)3});
+	for (ssize_t i = 0; i < nv; i++)
+		for (int c = 0; c < 3; c++) coords.mutable_at(i, c) = p.mesh.v[i][c];
+	py::array_t<int> cells({nc, (ssize_t)4});
+	for (ssize_t i = 0; i < nc; i++)
+		for (int c = 0; c < 4; c++) cells.mutable_at(i, c) = p.mesh.cells[i][c];
+	py::array_t<double> U({(ssize_t)3, (ssize_t)9, (ssize_t)9}), U1({(ssize_t)3, (ssize_t)9, (ssize_t)9});
+	for (int s = 0; s < 3; s++)
+		for (int i = 0; i < 81; i++) {
+			U.mutable_data()[s * 81 + i] = p.matrices.m[s].U[i];
+			U1.mutable_data()[s * 81 + i] = p.matrices.m[s].U1[i];
+		}
+	py::array_t<double> pde({nv, (ssize_t)9});
+	std::copy(p.pde.begin(), p.pde.end(), pde.mutable_data());
+	py::list stages;
+	for (int s = 0; s < 3; s++) {
+		const auto& st = p.stages[s];
+		py::array_t<int> kind({nv, (ssize_t)6}), v({nv, (ssize_t)6, (ssize_t)4}),
+		    slot({nv, (ssize_t)6, (ssize_t)4});
+		py::array_t<double> lam({nv, (ssize_t)6, (ssize_t)4}), q({nv, (ssize_t)6, (ssize_t)3});
+		for (ssize_t e = 0; e < nv * 6; e++) {
+			const gsx_foot& f = st.feet[(size_t)e];
+			kind.mutable_data()[e] = f.kind;
+			for (int i = 0; i < 4; i++) {
+				v.mutable_data()[e * 4 + i] = f.v[i];
+				slot.mutable_data()[e * 4 + i] = f.slot[i];
+				lam.mutable_data()[e * 4 + i] = f.lam[i];
+			}
+			for (int i = 0; i < 3; i++) q.mutable_data()[e * 3 + i] = f.q[i];
+		}
+		py::dict d;
+		d["kind"] = kind; d["v"] = v; d["slot"] = slot; d["lam"] = lam; d["q"] = q;
+		stages.append(d);
+	}
+	py::dict d;
+	d["coords"] = coords; d["cells"] = cells; d["U"] = U; d["U1"] = U1; d["pde"] = pde;
+	d["tau"] = p.tau; d["average_height"] = p.averageHeight;
+	d["maximal_eigenvalue"] = p.maximalEigenvalue;
+	d["border"] = p.borderIdx; d["inner"] = p.innerIdx;
+	d["grad_offsets"] = p.gradient.offsets; d["grad_neighbors"] = p.gradient.neighbors;
+	d["grad_rows"] = p.gradient.rows; d["grad_weights"] = p.gradient.weights;
+	d["grad_M"] = p.gradient.M; d["grad_det"] = p.gradient.det;
+	d["stages"] = stages;
+	return d;
+}
+
+struct PySimplexEngine {
+	std::shared_ptr<simplex::Engine> e;
+	py::array_t<double> pde() const {
+		const std::vector<double> v = e->pde();
+		py::array_t<double> out({(ssize_t)(v.size() / 9), (ssize_t)9});
+		std::copy(v.begin(), v.end(), out.mutable_data());
+		return out;
+	}
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_gcm_host, m) {
@@ -198,6 +260,28 @@ PYBIND11_MODULE(_gcm_host, m) {
 		         t.detector.area = makeArea(area);
 		         t.detector.gridId = gridId;
 	         })
+	    .def_property("grid", [](Task& t) {
+		                  return std::string(t.globalSettings.gridId == Grids::T::SIMPLEX ? "SIMPLEX" : "CUBIC");
+	                  },
+	                  [](Task& t, const std::string& g) {
+		                  if (g == "SIMPLEX") t.globalSettings.gridId = Grids::T::SIMPLEX;
+		                  else if (g == "CUBIC") t.globalSettings.gridId = Grids::T::CUBIC;
+		                  else throw Exception("unknown grid " + g);
+	                  })
+	    .def_property("calculation_basis", [](Task& t) { return t.calculationBasis; },
+	                  [](Task& t, std::vector<real> b) { t.calculationBasis = b; })
+	    .def("set_simplex_box",
+	         [](Task& t, std::array<int, 3> cells, std::vector<real> lo, std::vector<real> hi,
+	            real jitter, uint64_t seed) {
+		         if (lo.size() != 3 || hi.size() != 3) throw Exception("set_simplex_box: 3-D box");
+		         t.simplexGrid.cells = cells;
+		         t.simplexGrid.lo = {lo[0], lo[1], lo[2]};
+		         t.simplexGrid.hi = {hi[0], hi[1], hi[2]};
+		         t.simplexGrid.jitter = jitter;
+		         t.simplexGrid.seed = seed;
+	         },
+	         py::arg("cells"), py::arg("lo"), py::arg("hi"), py::arg("jitter") = 0.0,
+	         py::arg("seed") = 0)
 	    .def("add_ode",
 	         [](Task& t, size_t id, const std::string& name) {
 		         if (!t.bodies.count(id)) throw Exception("add_ode: no such body");
@@ -251,6 +335,23 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    },
 	    "GPU-free VtkSnapshotter file of one body (set-up layer, or `pde`)", py::arg("task"),
 	    py::arg("body_id"), py::arg("file_name"), py::arg("pde") = py::none());
+
+	m.def("simplex_plans", &simplexPlans,
+	      "GPU-free simplex set-up: mesh, time step, gradient and stage plans", py::arg("task"));
+
+	py::class_<PySimplexEngine>(m, "SimplexEngine")
+	    .def(py::init([](const Task& t, int device) {
+		         PySimplexEngine p;
+		         p.e = std::make_shared<simplex::Engine>(t, device);
+		         return p;
+	         }),
+	         py::arg("task"), py::arg("device") = 0)
+	    .def("run", [](PySimplexEngine& p) { p.e->run(); })
+	    .def("run_steps", [](PySimplexEngine& p, int n) { p.e->runSteps(n); })
+	    .def("pde", &PySimplexEngine::pde, "current layer [n_vertices, 9]")
+	    .def_property_readonly("steps", [](PySimplexEngine& p) { return p.e->stepsDone(); })
+	    .def_property_readonly("time_step", [](PySimplexEngine& p) { return p.e->timeStepValue(); })
+	    .def_property_readonly("required_time", [](PySimplexEngine& p) { return p.e->getRequiredTime(); });
 
 	py::class_<PyEngine>(m, "Engine")
 	    .def(py::init([](const Task& t, int device) {

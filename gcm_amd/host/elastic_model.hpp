@@ -148,12 +148,12 @@ struct PdeVec {
 	}
 };
 
-/// linal::createLocalBasis(e_axis) (linal/basis.hpp:49-65) with
+/// linal::createLocalBasis(n) (linal/basis.hpp:49-65) with
 /// perpendicularClockwise (linal/geometry.hpp:35-52); columns (tau1, tau2, n).
 template <int D>
-void localBasis(int axis, real basis[D][D]) {
+void localBasisOf(const real nIn[D], real basis[D][D]) {
 	real n[3] = {0, 0, 0};
-	n[axis] = 1;
+	for (int i = 0; i < D; i++) n[i] = nIn[i];
 	if constexpr (D == 1) {
 		basis[0][0] = n[0];
 	} else if constexpr (D == 2) {
@@ -184,6 +184,14 @@ void localBasis(int axis, real basis[D][D]) {
 	}
 }
 
+/// createLocalBasis(e_axis)
+template <int D>
+void localBasis(int axis, real basis[D][D]) {
+	real n[D] = {};
+	n[axis] = 1;
+	localBasisOf<D>(n, basis);
+}
+
 }  // namespace detail
 
 /// ElasticModel<D> (rheology/models/ElasticModel.hpp) -- matrix construction only.
@@ -200,6 +208,20 @@ struct ElasticModel {
 		for (int i = 0; i < D; i++) {
 			real basis[D][D] = {};
 			detail::localBasis<D>(i, basis);
+			constructGcmMatrix(out.m[i], mat, basis);
+		}
+	}
+
+	/// constructGcmMatrices with an arbitrary calculation basis: stage i along
+	/// column i of `calc` (ElasticModel.hpp:57-65).
+	static void constructGcmMatrices(Matrices& out, const IsotropicMaterial& mat,
+	                                 const real calc[D][D]) {
+		if (!(mat.rho > 0) || !(mat.mu > 0))
+			throw std::invalid_argument("isotropic material needs rho > 0 and mu > 0");
+		for (int i = 0; i < D; i++) {
+			real n[D], basis[D][D] = {};
+			for (int r = 0; r < D; r++) n[r] = calc[r][i];
+			detail::localBasisOf<D>(n, basis);
 			constructGcmMatrix(out.m[i], mat, basis);
 		}
 	}

@@ -1,0 +1,736 @@
+// simplex.cpp -- mesh, triangulation queries and static plans of the simplex
+// path (see simplex.hpp).  Every geometric predicate restates the reference's
+// linal code operation by operation (paths relative to src/libgcm).
+#include "simplex.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <memory>
+#include <set>
+
+namespace gcm {
+namespace simplex {
+
+// ----------------------------------------------------------------- linal --
+namespace {
+
+inline Real3 sub(const Real3& a, const Real3& b) { return {a[0] - b[0], a[1] - b[1], a[2] - b[2]}; }
+inline Real3 add(const Real3& a, const Real3& b) { return {a[0] + b[0], a[1] + b[1], a[2] + b[2]}; }
+inline Real3 mul(const Real3& a, real x) { return {a[0] * x, a[1] * x, a[2] * x}; }
+inline real dot(const Real3& a, const Real3& b) {  // functions.hpp:327-334
+	real r = a[0] * b[0];
+	r += a[1] * b[1];
+	r += a[2] * b[2];
+	return r;
+}
+inline real length(const Real3& a) { return std::sqrt(dot(a, a)); }
+inline Real3 cross(const Real3& a, const Real3& b) {  // geometry.hpp:13-17
+	return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+}
+inline Real3 normalize(const Real3& a) {
+	const real l = length(a);
+	return {a[0] / l, a[1] / l, a[2] / l};
+}
+/// determinants.hpp:40-53 (arbitrary-type 3x3) and :25-30 (2x2)
+inline real det3(real m11, real m12, real m13, real m21, real m22, real m23, real m31, real m32,
+                 real m33) {
+	return m11 * (m22 * m33 - m23 * m32) - m12 * (m21 * m33 - m23 * m31) +
+	       m13 * (m21 * m32 - m22 * m31);
+}
+inline real det2(real m11, real m12, real m21, real m22) { return m11 * m22 - m12 * m21; }
+/// linearSystems.hpp:104-129 (Cramer); throws like THROW_INVALID_ARG
+Real3 solve3(const real A[3][3], const Real3& b) {
+	const real det = det3(A[0][0], A[0][1], A[0][2], A[1][0], A[1][1], A[1][2], A[2][0], A[2][1],
+	                      A[2][2]);
+	if (det == 0) throw Exception("SLE determinant is zero");
+	const real d1 = det3(b[0], A[0][1], A[0][2], b[1], A[1][1], A[1][2], b[2], A[2][1], A[2][2]);
+	const real d2 = det3(A[0][0], b[0], A[0][2], A[1][0], b[1], A[1][2], A[2][0], b[2], A[2][2]);
+	const real d3 = det3(A[0][0], A[0][1], b[0], A[1][0], A[1][1], b[1], A[2][0], A[2][1], b[2]);
+	return {d1 / det, d2 / det, d3 / det};
+}
+/// linearLeastSquares (linearSystems.hpp:150-158) for a 3x2 system, W = I:
+/// solve(A^T (W A), A^T (W b)) with transposeMultiply's summation order.
+std::array<real, 2> lls32(const Real3& c0, const Real3& c1, const Real3& b) {
+	const Real3* col[2] = {&c0, &c1};
+	real M[2][2], r[2];
+	for (int i = 0; i < 2; i++) {
+		for (int j = 0; j < 2; j++) {
+			real s = (*col[i])[0] * (*col[j])[0];
+			for (int n = 1; n < 3; n++) s += (*col[i])[n] * (*col[j])[n];
+			M[i][j] = s;
+		}
+		real s = (*col[i])[0] * b[0];
+		for (int n = 1; n < 3; n++) s += (*col[i])[n] * b[n];
+		r[i] = s;
+	}
+	const real det = det2(M[0][0], M[0][1], M[1][0], M[1][1]);  // linearSystems.hpp:71-90
+	if (det == 0) throw Exception("SLE determinant is zero");
+	return {det2(r[0], M[0][1], r[1], M[1][1]) / det, det2(M[0][0], r[0], M[1][0], r[1]) / det};
+}
+/// 3x1 system (segment barycentrics): (A^T A)^-1 A^T b, 1x1 solve
+real lls31(const Real3& c0, const Real3& b) {
+	real m = c0[0] * c0[0];
+	for (int n = 1; n < 3; n++) m += c0[n] * c0[n];
+	real r = c0[0] * b[0];
+	for (int n = 1; n < 3; n++) r += c0[n] * b[n];
+	if (m == 0) throw Exception("SLE determinant is zero");
+	return r / m;
+}
+/// geometry.hpp:142-151
+std::array<real, 4> barycentric(const Real3& a, const Real3& b, const Real3& c, const Real3& d,
+                                const Real3& q) {
+	const real T[3][3] = {{a[0] - d[0], b[0] - d[0], c[0] - d[0]},
+	                      {a[1] - d[1], b[1] - d[1], c[1] - d[1]},
+	                      {a[2] - d[2], b[2] - d[2], c[2] - d[2]}};
+	const Real3 l = solve3(T, sub(q, d));
+	return {l[0], l[1], l[2], 1 - l[0] - l[1] - l[2]};
+}
+/// geometry.hpp:124-137 (triangle in 3-D)
+Real3 barycentric3(const Real3& a, const Real3& b, const Real3& c, const Real3& q) {
+	const auto l = lls32(sub(a, c), sub(b, c), sub(q, c));
+	return {l[0], l[1], 1 - l[0] - l[1]};
+}
+/// geometry.hpp:88-103 (segment in 3-D)
+std::array<real, 2> barycentric2(const Real3& a, const Real3& b, const Real3& q) {
+	const real l = lls31(sub(a, b), sub(q, b));
+	return {l, 1 - l};
+}
+/// geometry.hpp:248-261
+real orientedVolume(const Real3& a, const Real3& b, const Real3& c, const Real3& d) {
+	const Real3 ba = sub(b, a), ca = sub(c, a), da = sub(d, a);
+	return det3(ba[0], ba[1], ba[2], ca[0], ca[1], ca[2], da[0], da[1], da[2]) / 6;
+}
+real volume(const Real3& a, const Real3& b, const Real3& c, const Real3& d) {
+	return std::fabs(orientedVolume(a, b, c, d));
+}
+real area(const Real3& a, const Real3& b, const Real3& c) {  // geometry.hpp:238-240
+	return length(cross(sub(b, a), sub(c, a))) / 2;
+}
+real minimalHeight3(const Real3& a, const Real3& b, const Real3& c) {  // geometry.hpp:263-270
+	const real S = area(a, b, c);
+	const real ab = length(sub(a, b)), ac = length(sub(a, c)), bc = length(sub(b, c));
+	return 2 * S / std::fmax(ab, std::fmax(ac, bc));
+}
+real minimalHeight4(const Real3& a, const Real3& b, const Real3& c, const Real3& d) {  // :274-284
+	const real V = volume(a, b, c, d);
+	const real A = area(b, c, d), B = area(c, d, a), C = area(d, a, b), D = area(a, b, c);
+	return 3 * V / std::fmax(A, std::fmax(B, std::fmax(C, D)));
+}
+bool isDegenerate3(const Real3& a, const Real3& b, const Real3& c, real eps) {  // :291-297
+	const real h = minimalHeight3(a, b, c);
+	const real l = (length(sub(a, b)) + length(sub(a, c)) + length(sub(b, c))) / 3;
+	return h <= eps * l;
+}
+bool isDegenerate4(const Real3& a, const Real3& b, const Real3& c, const Real3& d, real eps) {
+	const real h = minimalHeight4(a, b, c, d);  // :304-310
+	const real l = (length(sub(a, b)) + length(sub(a, c)) + length(sub(a, d)) + length(sub(d, b)) +
+	                length(sub(d, c)) + length(sub(b, c))) /
+	               6;
+	return h <= eps * l;
+}
+bool segmentContains(const Real3& a, const Real3& b, const Real3& q, real eps, real degEps) {
+	if (!isDegenerate3(a, b, q, degEps)) return false;  // :338-343
+	const auto l = barycentric2(a, b, q);
+	return l[0] >= -eps && l[1] >= -eps;
+}
+bool triangleContains(const Real3& a, const Real3& b, const Real3& c, const Real3& q, real eps,
+                      real degEps) {  // :359-364
+	if (!isDegenerate4(a, b, c, q, degEps)) return false;
+	const Real3 l = barycentric3(a, b, c, q);
+	return l[0] >= -eps && l[1] >= -eps && l[2] >= -eps;
+}
+bool tetrahedronContains(const Real3& a, const Real3& b, const Real3& c, const Real3& d,
+                         const Real3& q, real eps) {  // :370-376
+	const auto l = barycentric(a, b, c, d, q);
+	return l[0] >= -eps && l[1] >= -eps && l[2] >= -eps && l[3] >= -eps;
+}
+bool solidAngleContains(const Real3& a, const Real3& b, const Real3& c, const Real3& d,
+                        const Real3& q, real eps) {  // :410-416
+	const auto l = barycentric(a, b, c, d, q);
+	return l[0] <= 1 + eps && l[1] >= -eps && l[2] >= -eps && l[3] >= -eps;
+}
+Real3 oppositeFaceNormal(const Real3& opposite, const Real3& a, const Real3& b, const Real3& c) {
+	const Real3 ans = normalize(cross(sub(a, b), sub(c, b)));  // :423-428
+	return (dot(ans, sub(a, opposite)) > 0) ? ans : mul(ans, -1);
+}
+/// geometry.hpp:201-217
+Real3 lineWithFlatIntersection(const Real3& f1, const Real3& f2, const Real3& f3, const Real3& l1,
+                               const Real3& l2) {
+	const Real3 tau = sub(l2, l1), p = sub(f2, f1), q = sub(f3, f1);
+	const real A[3][3] = {{tau[0], -p[0], -q[0]}, {tau[1], -p[1], -q[1]}, {tau[2], -p[2], -q[2]}};
+	const Real3 params = solve3(A, sub(f1, l1));
+	return add(l1, mul(tau, params[0]));
+}
+
+uint64_t splitmix(uint64_t x) {
+	x += 0x9E3779B97F4A7C15ull;
+	x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+	x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+	return x ^ (x >> 31);
+}
+real unitRandom(uint64_t seed, uint64_t n) {  // [-1, 1)
+	return (real)(splitmix(seed * 0x100000001B3ull + n) >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- mesh --
+
+void TetMesh::buildTopology() {
+	const int nc = (int)cells.size(), nv = (int)v.size();
+	nb.assign(nc, {-1, -1, -1, -1});
+	std::map<std::array<int, 3>, std::pair<int, int>> faces;
+	for (int c = 0; c < nc; c++)
+		for (int i = 0; i < 4; i++) {
+			std::array<int, 3> f = {cells[c][(i + 1) % 4], cells[c][(i + 2) % 4], cells[c][(i + 3) % 4]};
+			std::sort(f.begin(), f.end());
+			auto it = faces.find(f);
+			if (it == faces.end()) {
+				faces[f] = {c, i};
+			} else {
+				if (it->second.first < 0) throw Exception("face shared by more than two cells");
+				nb[c][i] = it->second.first;
+				nb[it->second.first][it->second.second] = c;
+				it->second.first = -2;
+			}
+		}
+	std::vector<int> cnt(nv + 1, 0);
+	for (const auto& c : cells)
+		for (int x : c) cnt[x + 1]++;
+	for (int i = 0; i < nv; i++) cnt[i + 1] += cnt[i];
+	incOff = cnt;
+	incCells.assign(cnt[nv], 0);
+	std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+	for (int c = 0; c < nc; c++)
+		for (int x : cells[c]) incCells[fill[x]++] = c;
+}
+
+TetMesh boxMesh(const std::array<int, 3>& n, const Real3& lo, const Real3& hi, real jitter,
+                uint64_t seed) {
+	for (int i = 0; i < 3; i++)
+		if (n[i] < 1 || !(hi[i] > lo[i])) throw Exception("boxMesh: bad box");
+	if (!(jitter >= 0 && jitter < 0.25)) throw Exception("boxMesh: jitter must be in [0, 0.25)");
+	TetMesh m;
+	const int nx = n[0] + 1, ny = n[1] + 1, nz = n[2] + 1;
+	auto id = [&](int i, int j, int k) { return (i * ny + j) * nz + k; };
+	m.v.resize((size_t)nx * ny * nz);
+	for (int i = 0; i < nx; i++)
+		for (int j = 0; j < ny; j++)
+			for (int k = 0; k < nz; k++) {
+				const int ijk[3] = {i, j, k}, nn[3] = {nx, ny, nz};
+				Real3 p;
+				for (int a = 0; a < 3; a++) {
+					const real h = (hi[a] - lo[a]) / n[a];
+					p[a] = (ijk[a] == n[a]) ? hi[a] : lo[a] + h * ijk[a];
+					const bool onBoundary = ijk[a] == 0 || ijk[a] == nn[a] - 1;
+					if (!onBoundary && jitter > 0)
+						p[a] += jitter * h * unitRandom(seed, (uint64_t)id(i, j, k) * 3 + a);
+				}
+				m.v[id(i, j, k)] = p;
+			}
+	static const int perms[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+	for (int i = 0; i < n[0]; i++)
+		for (int j = 0; j < n[1]; j++)
+			for (int k = 0; k < n[2]; k++)
+				for (const auto& pm : perms) {
+					int c[3] = {i, j, k};
+					std::array<int, 4> t;
+					t[0] = id(c[0], c[1], c[2]);
+					for (int s = 0; s < 3; s++) {
+						c[pm[s]]++;
+						t[s + 1] = id(c[0], c[1], c[2]);
+					}
+					const real vol = orientedVolume(m.v[t[0]], m.v[t[1]], m.v[t[2]], m.v[t[3]]);
+					if (vol < 0) std::swap(t[2], t[3]);
+					if (!(vol != 0)) throw Exception("boxMesh: degenerate cell");
+					m.cells.push_back(t);
+				}
+	for (const auto& t : m.cells)
+		if (!(orientedVolume(m.v[t[0]], m.v[t[1]], m.v[t[2]], m.v[t[3]]) > 0))
+			throw Exception("boxMesh: jitter inverted a cell");
+	m.buildTopology();
+	return m;
+}
+
+// ------------------------------------------------------------------- grid --
+
+Grid::Grid(const TetMesh& m) : mesh(m) {
+	const int nv = m.nVertices();
+	inner.assign(nv, 1);
+	for (size_t c = 0; c < m.cells.size(); c++)
+		for (int i = 0; i < 4; i++)
+			if (m.nb[c][i] < 0)
+				for (int k = 1; k < 4; k++) inner[m.cells[c][(i + k) % 4]] = 0;
+	for (int it = 0; it < nv; it++) (inner[it] ? innerIdx : borderIdx).push_back(it);
+	// collectCellHeightsStatistics (SimplexGrid.cpp:266-285): Histogram of 100 bins
+	std::vector<real> hs;
+	for (const auto& t : m.cells) hs.push_back(minimalHeight4(P(t[0]), P(t[1]), P(t[2]), P(t[3])));
+	const real mn = *std::min_element(hs.begin(), hs.end());
+	const real mx = *std::max_element(hs.begin(), hs.end());
+	const size_t nBins = 100;
+	std::vector<size_t> bins;
+	const real binSize0 = (mx - mn) / real(nBins);
+	if (mx == mn) {  // Histogram.hpp:13-33
+		bins.assign(nBins, 0);
+		bins[0] = hs.size();
+	} else {
+		bins.assign(nBins + 1, 0);
+		for (real h : hs) ++bins[(size_t)((h - mn) / binSize0)];
+		bins[nBins - 1] += bins.back();
+		bins.pop_back();
+	}
+	const real binSize = (mx - mn) / (real)bins.size();  // Histogram.hpp:44-58
+	real ip = 0, cnt = 0;
+	for (size_t i = 0; i < bins.size(); i++) {
+		ip = ip + (real)bins[i] * (mn + (real(i) + 0.5) * binSize);
+		cnt = cnt + (real)bins[i];
+	}
+	averageHeight = ip / cnt;
+	minimalHeight = mn;
+}
+
+Real3 Grid::borderNormal(int it) const {
+	Real3 sum = {0, 0, 0};
+	bool any = false;
+	for (int p = mesh.incOff[it]; p < mesh.incOff[it + 1]; p++) {
+		const int c = mesh.incCells[p];
+		for (int i = 0; i < 4; i++) {
+			if (mesh.nb[c][i] >= 0 || mesh.cells[c][i] == it) continue;  // face must contain it
+			const auto& t = mesh.cells[c];
+			sum = add(sum, oppositeFaceNormal(P(t[i]), P(t[(i + 1) % 4]), P(t[(i + 2) % 4]),
+			                                  P(t[(i + 3) % 4])));  // Cgal3DTriangulation.hpp:109-118
+			any = true;
+		}
+	}
+	if (!any) return {0, 0, 0};
+	return normalize(sum);
+}
+
+std::vector<int> Grid::neighborVertices(int it) const {
+	std::set<int> s;
+	for (int p = mesh.incOff[it]; p < mesh.incOff[it + 1]; p++)
+		for (int x : mesh.cells[mesh.incCells[p]]) s.insert(x);
+	s.erase(it);
+	return std::vector<int>(s.begin(), s.end());
+}
+
+int Grid::otherVertexIndex(int cell, int a, int b, int c) const {  // Cgal3DTriangulation.hpp:272-280
+	for (int i = 0; i < 4; i++) {
+		const int d = mesh.cells[cell][i];
+		if (d != a && d != b && d != c) return i;
+	}
+	throw Exception("Cell contains equal vertices");
+}
+
+int Grid::findCrossedIncidentCell(int vh, const Real3& query, real eps) const {  // :221-238
+	for (int p = mesh.incOff[vh]; p < mesh.incOff[vh + 1]; p++) {
+		const int cand = mesh.incCells[p];
+		const auto& t = mesh.cells[cand];
+		const int a = t[otherVertexIndex(cand, vh, vh, vh)];
+		const int b = t[otherVertexIndex(cand, vh, vh, a)];
+		const int c = t[otherVertexIndex(cand, vh, a, b)];
+		if (solidAngleContains(P(vh), P(a), P(b), P(c), query, eps)) return cand;
+	}
+	return -1;
+}
+
+void Grid::findCrossedInsideOutFacet(int t, const Real3& q, const Real3& p, int& a, int& b, int& c,
+                                     real eps) const {  // :247-259
+	a = b = c = -1;
+	for (int i = 0; i < 4; i++) {
+		const int a1 = mesh.cells[t][(i + 1) % 4], b1 = mesh.cells[t][(i + 2) % 4],
+		          c1 = mesh.cells[t][(i + 3) % 4];
+		if (solidAngleContains(q, P(a1), P(b1), P(c1), p, eps)) {
+			a = a1;
+			b = b1;
+			c = c1;
+			return;
+		}
+	}
+}
+
+// LineWalker<Triangulation, 3>::collectCells (LineWalker.hpp:25-52).  Leaving
+// the body is the step onto nb == -1; the face crossed then is {u, v, w}.
+std::vector<int> Grid::collectCells(const Real3& q, const Real3& p, int t, int u, int v, int w,
+                                    std::array<int, 3>& lastFace) const {
+	std::vector<int> ans;
+	ans.push_back(t);
+	auto orient = [&](const Real3& a, const Real3& b, const Real3& c, const Real3& d) {
+		return orientedVolume(a, b, c, d);
+	};
+	while (orient(P(u), P(v), P(w), p) < 0) {
+		const int nt = mesh.nb[t][otherVertexIndex(t, u, v, w)];  // neighborThrough
+		if (nt < 0) {
+			lastFace = {u, v, w};
+			ans.push_back(-1);
+			break;
+		}
+		t = nt;
+		ans.push_back(t);
+		const int s = mesh.cells[t][otherVertexIndex(t, u, v, w)];
+		if (orient(P(u), P(s), q, p) > 0) {
+			if (orient(P(v), P(s), q, p) > 0) u = s;
+			else w = s;
+		} else {
+			if (orient(P(w), P(s), q, p) > 0) v = s;
+			else u = s;
+		}
+	}
+	return ans;
+}
+
+std::vector<int> Grid::cellsAlongSegmentFromVertex(int q, const Real3& p,
+                                                   std::array<int, 3>& lastFace) const {
+	const int t = findCrossedIncidentCell(q, p, 0);  // LineWalker.hpp:54-69
+	if (t < 0) return {};
+	const auto& c = mesh.cells[t];
+	int u = c[otherVertexIndex(t, q, q, q)];
+	int v = c[otherVertexIndex(t, q, q, u)];
+	const int w = c[otherVertexIndex(t, q, u, v)];
+	if (orientedVolume(P(u), P(v), P(w), P(q)) < 0) std::swap(u, v);
+	return collectCells(P(q), p, t, u, v, w, lastFace);
+}
+
+std::vector<int> Grid::cellsAlongSegmentFromCell(int t, const Real3& q, const Real3& p,
+                                                 std::array<int, 3>& lastFace) const {
+	int u, v, w;  // LineWalker.hpp:71-88
+	findCrossedInsideOutFacet(t, q, p, u, v, w, 0);
+	if (u < 0) findCrossedInsideOutFacet(t, q, p, u, v, w, EQUALITY_TOLERANCE);
+	if (u < 0) return {};
+	if (orientedVolume(P(u), P(v), P(w), q) < 0) std::swap(u, v);
+	return collectCells(q, p, t, u, v, w, lastFace);
+}
+
+// SimplexGrid.cpp:115-164
+Grid::Cell Grid::checkLineWalkFoundCell(int it, const std::vector<int>& cells,
+                                        const std::array<int, 3>& lastFace, const Real3& start,
+                                        const Real3& query) const {
+	Cell none;
+	if (cells.empty()) return none;
+	auto contains = [&](int c) {
+		const auto& t = mesh.cells[c];
+		return tetrahedronContains(P(t[0]), P(t[1]), P(t[2]), P(t[3]), query, EQUALITY_TOLERANCE);
+	};
+	auto full = [&](int c) {
+		Cell r;
+		r.n = 4;
+		for (int i = 0; i < 4; i++) r.v[i] = mesh.cells[c][i];
+		return r;
+	};
+	const int last = cells.back();
+	if (last >= 0 && contains(last)) return full(last);
+	if (cells.size() == 1) {
+		if (isInner(it)) throw Exception("line walk: inner node with a one-cell walk");
+		return none;
+	}
+	const int prev = cells[cells.size() - 2];
+	if (contains(prev)) return full(prev);
+	if (!isInner(it)) return none;
+	if (last < 0) {
+		// Triangulation::commonVertices(prev, last): prev's vertices in cell order
+		std::vector<int> face;
+		for (int i = 0; i < 4; i++) {
+			const int x = mesh.cells[prev][i];
+			if (x == lastFace[0] || x == lastFace[1] || x == lastFace[2]) face.push_back(x);
+		}
+		// filterFaceNotCrossedByTheRay (Cgal3DTriangulation.hpp:183-213)
+		std::vector<int> f;
+		const Real3 p0 = P(face[0]), p1 = P(face[1]), p2 = P(face[2]);
+		const Real3 x = lineWithFlatIntersection(p0, p1, p2, start, query);
+		const Real3 ps[3] = {p0, p1, p2};
+		if (triangleContains(p0, p1, p2, x, EQUALITY_TOLERANCE, EQUALITY_TOLERANCE)) {
+			f = face;
+		} else {
+			for (int i = 0; i < 3 && f.empty(); i++)
+				for (int j = i + 1; j < 3 && f.empty(); j++)
+					if (segmentContains(ps[i], ps[j], x, EQUALITY_TOLERANCE, EQUALITY_TOLERANCE))
+						f = {face[i], face[j]};
+			for (int i = 0; i < 3 && f.empty(); i++)
+				if (segmentContains(start, query, ps[i], EQUALITY_TOLERANCE, EQUALITY_TOLERANCE))
+					f = {face[i]};
+		}
+		Cell r;
+		r.n = (int)f.size();
+		for (int i = 0; i < r.n; i++) r.v[i] = f[i];
+		return r;
+	}
+	return none;
+}
+
+// SimplexGrid.cpp:57-112
+Grid::Cell Grid::findCellCrossedByTheRay(int it, const Real3& shift) const {
+	const Real3 start = P(it);
+	const Real3 query = add(start, shift);
+	std::array<int, 3> lastFace = {-1, -1, -1};
+	std::vector<int> along = cellsAlongSegmentFromVertex(it, query, lastFace);
+	Cell found = checkLineWalkFoundCell(it, along, lastFace, start, query);
+	if (found.n > 0) return found;
+	int startCell = findCrossedIncidentCell(it, query, 0);
+	if (startCell < 0) startCell = findCrossedIncidentCell(it, query, EQUALITY_TOLERANCE);
+	if (startCell < 0) startCell = mesh.incCells[mesh.incOff[it]];
+	const auto& t = mesh.cells[startCell];
+	// Triangulation::center (Cgal3DTriangulation.hpp:263-269): (a + b + c + d) / 4
+	Real3 center = add(add(add(P(t[0]), P(t[1])), P(t[2])), P(t[3]));
+	center = {center[0] / 4, center[1] / 4, center[2] / 4};
+	constexpr real w = 1e-3;
+	const Real3 startPoint = add(mul(center, w), mul(start, 1 - w));
+	lastFace = {-1, -1, -1};
+	along = cellsAlongSegmentFromCell(startCell, startPoint, query, lastFace);
+	found = checkLineWalkFoundCell(it, along, lastFace, start, query);
+	if (found.n > 0) return found;
+	if (isInner(it)) throw Exception("line walk failed for an inner node");
+	return Cell();
+}
+
+// ------------------------------------------------------------------- plans --
+
+GradientPlan buildGradientPlan(const Grid& grid) {
+	const auto& m = grid.mesh;
+	const int nv = m.nVertices();
+	GradientPlan g;
+	g.offsets.push_back(0);
+	for (int it = 0; it < nv; it++) {
+		const std::vector<int> nbs = grid.neighborVertices(it);
+		const int K = std::min((int)nbs.size(), MAX_NUMBER_OF_NEIGHBOR_VERTICES);
+		real A[MAX_NUMBER_OF_NEIGHBOR_VERTICES][3] = {};
+		real W[MAX_NUMBER_OF_NEIGHBOR_VERTICES] = {};
+		for (int i = 0; i < K; i++) {
+			const Real3 d = sub(m.v[nbs[i]], m.v[it]);
+			for (int c = 0; c < 3; c++) A[i][c] = d[c];
+			W[i] = 1.0 / length(d);
+			g.neighbors.push_back(nbs[i]);
+			for (int c = 0; c < 3; c++) g.rows.push_back(d[c]);
+			g.weights.push_back(W[i]);
+		}
+		g.offsets.push_back((int)g.neighbors.size());
+		// transposeMultiply(A, W * A) over all MAX rows (functions.hpp:220-234)
+		real M[3][3];
+		for (int r = 0; r < 3; r++)
+			for (int c = 0; c < 3; c++) {
+				real s = A[0][r] * (W[0] * A[0][c]);
+				for (int n = 1; n < MAX_NUMBER_OF_NEIGHBOR_VERTICES; n++) s += A[n][r] * (W[n] * A[n][c]);
+				M[r][c] = s;
+				g.M.push_back(s);
+			}
+		const real det = det3(M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1],
+		                      M[2][2]);
+		if (det == 0) throw Exception("estimateGradient: SLE determinant is zero");
+		g.det.push_back(det);
+	}
+	return g;
+}
+
+StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[9], real tau) {
+	const auto& m = grid.mesh;
+	const int nv = m.nVertices();
+	StagePlan plan;
+	plan.feet.assign((size_t)nv * 6, gsx_foot{});
+	plan.borderNodes = grid.borderIdx;
+	plan.innerNodes = grid.innerIdx;
+	static const std::vector<int> RIGHT = {1, 3, 5}, LEFT = {0, 2, 4};  // Model.cpp:81-82
+	for (int it = 0; it < nv; it++) {
+		const bool innerNode = grid.isInner(it);
+		std::vector<int> outer;
+		for (int k = 0; k < 6; k++) {
+			gsx_foot& f = plan.feet[(size_t)it * 6 + k];
+			const real dx = -tau * L[k];  // crossingPoints (common.hpp:46-52)
+			if (dx == 0) throw Exception("zero crossing point for a wave invariant");
+			const Real3 shift = mul(direction, dx);
+			const Grid::Cell t = grid.findCellCrossedByTheRay(it, shift);
+			const Real3 q = add(m.v[it], shift);
+			if (t.n == 4) {
+				f.kind = GSX_FOOT_CELL;
+				const auto lam = barycentric(m.v[t.v[0]], m.v[t.v[1]], m.v[t.v[2]], m.v[t.v[3]], q);
+				for (int i = 0; i < 4; i++) {
+					// TetrahedronInterpolator::isInterpolation assert (hpp:15-20)
+					if (!(lam[i] > -EQUALITY_TOLERANCE)) throw Exception("foot outside its cell");
+					f.v[i] = t.v[i];
+					f.lam[i] = lam[i];
+				}
+				for (int c = 0; c < 3; c++) f.q[c] = q[c];
+			} else if (t.n == 0 || ((t.n == 3 || t.n == 2) && !innerNode)) {
+				f.kind = GSX_FOOT_OUTER;
+				outer.push_back(k);
+			} else if (t.n == 3) {
+				// interpolateInSpaceTime (common.hpp:102-129): the geometry is static
+				const Real3 r0 = m.v[it], r1 = m.v[t.v[0]], r2 = m.v[t.v[1]], r3 = m.v[t.v[2]];
+				const Real3 rc = lineWithFlatIntersection(r1, r2, r3, r0, add(r0, shift));
+				const auto w = lls32(sub(r2, r1), sub(r3, r1), sub(rc, r1));
+				const Real3 pts[6] = {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {0, 1, 1}};
+				const Real3 qst = {w[0], w[1], 1 - length(sub(rc, r0)) / length(shift)};
+				// TetrahedronInterpolator::interpolateInOwner (hpp:113-155)
+				static const int tries[15][4] = {{0, 1, 2, 3}, {0, 1, 2, 4}, {0, 1, 2, 5}, {0, 1, 3, 4},
+				                                 {0, 1, 3, 5}, {0, 1, 4, 5}, {0, 2, 3, 4}, {0, 2, 3, 5},
+				                                 {0, 2, 4, 5}, {0, 3, 4, 5}, {1, 2, 3, 4}, {1, 2, 3, 5},
+				                                 {1, 2, 4, 5}, {1, 3, 4, 5}, {2, 3, 4, 5}};
+				bool ok = false;
+				for (const auto& tr : tries) {
+					if (volume(pts[tr[0]], pts[tr[1]], pts[tr[2]], pts[tr[3]]) == 0) continue;
+					const auto lam = barycentric(pts[tr[0]], pts[tr[1]], pts[tr[2]], pts[tr[3]], qst);
+					if (lam[0] > -EQUALITY_TOLERANCE && lam[1] > -EQUALITY_TOLERANCE &&
+					    lam[2] > -EQUALITY_TOLERANCE && lam[3] > -EQUALITY_TOLERANCE) {
+						for (int i = 0; i < 4; i++) {
+							f.slot[i] = tr[i];
+							f.lam[i] = lam[i];
+						}
+						ok = true;
+						break;
+					}
+				}
+				if (!ok) throw Exception("Containing tetrahedron is not found");
+				f.kind = GSX_FOOT_SPACETIME;
+				for (int i = 0; i < 3; i++) f.v[i] = t.v[i];
+			} else if (t.n == 2) {
+				// interpolateInSpaceTime1D in 3-D (GridCharacteristicMethodInRiemannInvariants.hpp:296-303)
+				throw Exception("This did not occur ever before");
+			} else {
+				f.kind = GSX_FOOT_ZERO;  // n == 1: no branch assigns u (hpp:168-196)
+			}
+		}
+		if (innerNode) {
+			if (!outer.empty()) throw Exception("outer invariant at an inner node");  // hpp:119
+			continue;
+		}
+		// contactAndBorderStage's outer-invariant completion (hpp:71-86)
+		if (outer != RIGHT && outer != LEFT && outer.size() != 6 && !outer.empty()) {
+			auto inter = [](const std::vector<int>& a, const std::vector<int>& b) {
+				std::vector<int> r;
+				std::set_intersection(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(r));
+				return r;
+			};
+			auto uni = [](const std::vector<int>& a, const std::vector<int>& b) {
+				std::vector<int> r;
+				std::set_union(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(r));
+				return r;
+			};
+			if (!inter(outer, RIGHT).empty()) outer = uni(outer, RIGHT);
+			if (!inter(outer, LEFT).empty()) outer = uni(outer, LEFT);
+			for (int k : outer) plan.feet[(size_t)it * 6 + k].kind = GSX_FOOT_OUTER;
+		}
+	}
+	return plan;
+}
+
+}  // namespace simplex
+}  // namespace gcm
+
+// ------------------------------------------------------------------ engine --
+namespace gcm {
+namespace simplex {
+
+namespace {
+void calcBasis(const Task& task, real calc[3][3]) {
+	if (task.calculationBasis.size() != 9)  // Engine.hpp:186-197 (random basis: not on this path)
+		throw Exception("the simplex path needs a constant 3x3 calculation basis");
+	for (int r = 0; r < 3; r++)
+		for (int c = 0; c < 3; c++) calc[r][c] = task.calculationBasis[(size_t)r * 3 + c];
+}
+}  // namespace
+
+HostPlans buildHostPlans(const Task& task) {
+	if (task.globalSettings.dimensionality != 3) throw Exception("the simplex path is 3-D");
+	if (task.bodies.size() != 1) throw Exception("the simplex path takes one body");
+	const size_t id = task.bodies.begin()->first;
+	const auto& body = task.bodies.begin()->second;
+	if (body.materialId != Materials::T::ISOTROPIC || body.modelId != Models::T::ELASTIC)
+		throw Exception("only isotropic elastic bodies are on this path");
+	if (!body.odes.empty()) throw Exception("ODEs are not on the simplex path");
+	// DefaultMesh::applyMaterialsCondition asserts BY_BODIES (engine/simplex/DefaultMesh.hpp:229-230)
+	if (task.materialConditions.type != Task::MaterialCondition::Type::BY_BODIES)
+		throw Exception("simplex materials must be given BY_BODIES");
+	const auto mat = task.materialConditions.byBodies.bodyMaterialMap.at(id);
+	HostPlans p;
+	const auto& sg = task.simplexGrid;
+	p.mesh = boxMesh(sg.cells, sg.lo, sg.hi, sg.jitter, sg.seed);
+	Grid grid(p.mesh);
+	real calc[3][3];
+	calcBasis(task, calc);
+	ElasticModel<3>::constructGcmMatrices(p.matrices, *mat, calc);
+	p.maximalEigenvalue = p.matrices.getMaximalEigenvalue();
+	p.averageHeight = grid.averageHeight;
+	// simplex::Engine::estimateTimeStep (Engine.hpp:78-92)
+	p.tau = task.globalSettings.CourantNumber * grid.averageHeight / p.maximalEigenvalue;
+	p.gradient = buildGradientPlan(grid);
+	for (int s = 0; s < 3; s++) {
+		const Real3 dir = {calc[0][s], calc[1][s], calc[2][s]};
+		p.stages[s] = buildStagePlan(grid, dir, p.matrices.m[s].L.data(), p.tau);
+	}
+	p.borderIdx = grid.borderIdx;
+	p.innerIdx = grid.innerIdx;
+	// InitialCondition::apply (util/task/InitialCondition.hpp:23-88): vectors and quantities
+	if (!task.initialCondition.waves.empty())
+		throw Exception("wave initial conditions are not on the simplex path");
+	std::vector<std::pair<std::shared_ptr<Area>, std::array<real, 9>>> ics;
+	for (const auto& v : task.initialCondition.vectors) {
+		if (v.list.size() != 9) throw Exception("initial vector has the wrong size");
+		std::array<real, 9> a;
+		std::copy(v.list.begin(), v.list.end(), a.begin());
+		ics.push_back({v.area, a});
+	}
+	for (const auto& q : task.initialCondition.quantities) {
+		std::array<real, 9> a{};
+		setQuantity(3, q.physicalQuantity, q.value, a.data());
+		ics.push_back({q.area, a});
+	}
+	const int nv = p.mesh.nVertices();
+	p.pde.assign((size_t)nv * 9, 0.0);
+	for (int it = 0; it < nv; it++) {
+		real* v = &p.pde[(size_t)it * 9];
+		for (const auto& ic : ics)
+			if (ic.first->contains(p.mesh.v[it]))
+				for (int c = 0; c < 9; c++) v[c] += ic.second[c];
+	}
+	return p;
+}
+
+Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
+	HostPlans p = buildHostPlans(task);
+	mesh_ = std::move(p.mesh);
+	grid_ = std::make_unique<Grid>(mesh_);
+	maximalEigenvalue = p.maximalEigenvalue;
+	tau = p.tau;
+	const int nv = mesh_.nVertices();
+	std::vector<double> coords((size_t)nv * 3);
+	for (int i = 0; i < nv; i++)
+		for (int c = 0; c < 3; c++) coords[(size_t)i * 3 + c] = mesh_.v[i][c];
+	gcmxCheck(gsx_create(device, nv, coords.data(), &ctx), "gsx_create");
+	std::vector<double> U(3 * 81), U1(3 * 81);
+	for (int s = 0; s < 3; s++) {
+		std::copy(p.matrices.m[s].U.begin(), p.matrices.m[s].U.end(), U.begin() + s * 81);
+		std::copy(p.matrices.m[s].U1.begin(), p.matrices.m[s].U1.end(), U1.begin() + s * 81);
+	}
+	gcmxCheck(gsx_set_matrices(ctx, U.data(), U1.data()), "gsx_set_matrices");
+	const auto& g = p.gradient;
+	gcmxCheck(gsx_set_gradient_plan(ctx, g.offsets.data(), g.neighbors.data(), g.rows.data(),
+	                                g.weights.data(), g.M.data(), g.det.data()),
+	          "gsx_set_gradient_plan");
+	for (int s = 0; s < 3; s++) {
+		const auto& st = p.stages[s];
+		gcmxCheck(gsx_set_stage_plan(ctx, s, st.feet.data(), (int)st.borderNodes.size(),
+		                             st.borderNodes.data(), (int)st.innerNodes.size(),
+		                             st.innerNodes.data()),
+		          "gsx_set_stage_plan");
+	}
+	gcmxCheck(gsx_upload(ctx, p.pde.data()), "gsx_upload");
+	afterConstruction(task);
+}
+
+Engine::~Engine() { gsx_destroy(ctx); }
+
+real Engine::estimateTimeStep() { return tau; }
+
+// simplex::Engine::nextTimeStep (engine/simplex/Engine.cpp:82-100) with a
+// constant basis and no border / contact correctors: the three gcmStage calls.
+void Engine::nextTimeStep() {
+	for (int stage = 0; stage < 3; stage++) gcmxCheck(gsx_stage(ctx, stage), "gsx_stage");
+}
+
+std::vector<real> Engine::pde() const {
+	std::vector<real> out((size_t)mesh_.nVertices() * 9);
+	gcmxCheck(gsx_download(ctx, out.data()), "gsx_download");
+	return out;
+}
+
+}  // namespace simplex
+}  // namespace gcm

@@ -1,0 +1,161 @@
+// simplex.hpp -- host side of the simplex (tetrahedral) grid-characteristic path.
+//
+// The reference's simplex engine (engine/simplex/*, grid/simplex/*) runs the
+// grid-characteristic method in Riemann invariants
+// (GridCharacteristicMethodInRiemannInvariants.hpp:44-198) on a CGAL
+// triangulation.  CGAL is not in this image, so the mesh here is built by
+// boxMesh() (a jittered Kuhn tetrahedralisation of a box) and the triangulation
+// queries the method needs -- incident cells, face neighbours, the line walk
+// of LineWalker.hpp / SimplexGrid.cpp:57-164 -- are restated over it.
+//
+// The mesh is static and the calculation basis constant, so everything the
+// walk decides (the cell or border face each characteristic foot falls in,
+// barycentric weights, which invariants are outer at a border node) is found
+// once on the host (StagePlan).  The per-step work -- Riemann invariants, LSQ
+// gradients (Differentiation.hpp:33-63), hybrid interpolation
+// (TetrahedronInterpolator.hpp:93-104), space-time interpolation
+// (common.hpp:102-129), U1 back-transform -- runs on the GPU (gsx_* in
+// include/gcmx.h, gcm_amd/csrc/simplex.hip).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/gcmx.h"
+#include "elastic_model.hpp"
+#include "task.hpp"
+
+namespace gcm {
+namespace simplex {
+
+constexpr real EQUALITY_TOLERANCE = 1e-9;           // util/infrastructure/Types.hpp:10
+constexpr int MAX_NUMBER_OF_NEIGHBOR_VERTICES = 20;  // Cgal3DTriangulation.hpp:53
+
+/// Tetrahedral mesh of one body: vertex coordinates, positively oriented cells,
+/// face neighbours (nb[c][i] = cell across the face opposite vertex i, -1 =
+/// outside the body) and vertex -> incident cells (ascending cell index).
+struct TetMesh {
+	std::vector<Real3> v;
+	std::vector<std::array<int, 4>> cells;
+	std::vector<std::array<int, 4>> nb;
+	std::vector<int> incOff, incCells;
+	void buildTopology();
+	int nVertices() const { return (int)v.size(); }
+};
+
+/// Kuhn tetrahedralisation (6 tetrahedra per cube) of the box [lo, hi] with
+/// n cubes per axis.  Vertices are jittered by up to `jitter` * h with a
+/// SplitMix64 stream of `seed`: interior vertices in 3-D, face vertices within
+/// their face, edge vertices along their edge, corners fixed.
+TetMesh boxMesh(const std::array<int, 3>& n, const Real3& lo, const Real3& hi, real jitter,
+                uint64_t seed);
+
+/// SimplexGrid<3> (grid/simplex/SimplexGrid.{hpp,cpp}) over a TetMesh, one body.
+class Grid {
+public:
+	explicit Grid(const TetMesh& mesh);
+	const TetMesh& mesh;
+	/// Cell found by the ray walk: n = 4 (cell), 3 (border face), 2, 1, 0.
+	struct Cell {
+		int n = 0;
+		int v[4] = {-1, -1, -1, -1};
+	};
+	bool isInner(int it) const { return inner[it]; }
+	/// borderNormal (SimplexGrid.hpp:151-154, normal():426-444)
+	Real3 borderNormal(int it) const;
+	/// findNeighborVertices (SimplexGrid.hpp:249-259): ascending local indices
+	std::vector<int> neighborVertices(int it) const;
+	/// findCellCrossedByTheRay (SimplexGrid.cpp:57-112)
+	Cell findCellCrossedByTheRay(int it, const Real3& shift) const;
+	real averageHeight = 0, minimalHeight = 0;  // collectCellHeightsStatistics (Histogram)
+	std::vector<int> innerIdx, borderIdx;       // markInnersAndBorders order
+
+private:
+	std::vector<char> inner;
+	const Real3& P(int vtx) const { return mesh.v[vtx]; }
+	int otherVertexIndex(int cell, int a, int b, int c) const;
+	int findCrossedIncidentCell(int vh, const Real3& query, real eps) const;
+	void findCrossedInsideOutFacet(int t, const Real3& q, const Real3& p, int& a, int& b, int& c,
+	                               real eps) const;
+	std::vector<int> collectCells(const Real3& q, const Real3& p, int t, int u, int v, int w,
+	                              std::array<int, 3>& lastFace) const;
+	std::vector<int> cellsAlongSegmentFromVertex(int q, const Real3& p,
+	                                             std::array<int, 3>& lastFace) const;
+	std::vector<int> cellsAlongSegmentFromCell(int t, const Real3& q, const Real3& p,
+	                                           std::array<int, 3>& lastFace) const;
+	Cell checkLineWalkFoundCell(int it, const std::vector<int>& cells,
+	                            const std::array<int, 3>& lastFace, const Real3& start,
+	                            const Real3& query) const;
+};
+
+/// Static data of one stage for the device (gsx_set_stage_plan).
+struct StagePlan {
+	std::vector<gsx_foot> feet;  // [node][6] invariants 0..5 (6..8 have dx == 0)
+	std::vector<int> borderNodes, innerNodes;
+};
+
+/// The LSQ gradient operator of every node (gsx_set_gradient_plan).
+struct GradientPlan {
+	std::vector<int> offsets, neighbors;
+	std::vector<double> rows, weights, M, det;
+};
+
+/// Differentiation::estimateGradient's per-node matrices (Differentiation.hpp:33-63).
+GradientPlan buildGradientPlan(const Grid& grid);
+
+/// Feet of every node for stage s along `direction` with crossing points
+/// dx = -tau * L (common.hpp:46-52) -- GridCharacteristicMethodInRiemannInvariants
+/// ::interpolateValuesAround (:156-198) decided once, plus the outer-invariant
+/// bookkeeping of contactAndBorderStage (:57-95).
+StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[9], real tau);
+
+}  // namespace simplex
+}  // namespace gcm
+
+#include "engine.hpp"
+
+namespace gcm {
+namespace simplex {
+
+/// simplex::Engine<3, CgalTriangulation> (engine/simplex/Engine.{hpp,cpp}) for one
+/// isotropic-elastic body: GcmType ADVECT_RIEMANN_INVARIANTS, SplittingType
+/// PRODUCT, BorderCalcMode GLOBAL_BASIS, constant Task::calculationBasis, border
+/// nodes without border conditions (outer invariants zero, i.e. non-reflecting).
+class Engine : public AbstractEngine {
+public:
+	explicit Engine(const Task& task, int device = 0);
+	~Engine() override;
+	const Grid& grid() const { return *grid_; }
+	const TetMesh& mesh() const { return mesh_; }
+	/// current layer, 9 doubles per vertex (downloads)
+	std::vector<real> pde() const;
+	real timeStepValue() const { return tau; }
+
+protected:
+	void nextTimeStep() override;
+	real estimateTimeStep() override;
+	void writeSnapshots(const int) override {}
+
+private:
+	TetMesh mesh_;
+	std::unique_ptr<Grid> grid_;
+	gsx_ctx* ctx = nullptr;
+	real maximalEigenvalue = 0, tau = 0;
+};
+
+/// GPU-free set-up of the simplex path: mesh, the time step and the static plans
+/// the Engine uploads (for tests and tools).
+struct HostPlans {
+	TetMesh mesh;
+	real averageHeight = 0, maximalEigenvalue = 0, tau = 0;
+	GcmMatrices<3> matrices;
+	GradientPlan gradient;
+	StagePlan stages[3];
+	std::vector<real> pde;  // initial layer, 9 per vertex
+	std::vector<int> borderIdx, innerIdx;
+};
+HostPlans buildHostPlans(const Task& task);
+
+}  // namespace simplex
+}  // namespace gcm

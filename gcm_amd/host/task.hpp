@@ -9,6 +9,7 @@
 #include <map>
 #include <memory>
 #include <stdexcept>
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -231,6 +232,19 @@ struct Task {
 		Values values;
 	};
 	std::map<size_t, std::vector<CubicBorderCondition>> cubicBorderConditions;
+
+	/// The reference's Task::calculationBasis (Task.hpp:129): 9 numbers, column i =
+	/// direction of stage i.  Required (constant) on the simplex path here.
+	std::vector<real> calculationBasis;
+
+	/// Task::SimplexGrid (Task.hpp:84-127) -- CGAL is absent, so the mesh is the
+	/// jittered Kuhn tetrahedralisation of a box (simplex::boxMesh).
+	struct SimplexGrid {
+		std::array<int, 3> cells = {0, 0, 0};  // cubes per axis
+		Real3 lo = {0, 0, 0}, hi = {1, 1, 1};
+		real jitter = 0;
+		uint64_t seed = 0;
+	} simplexGrid;
 
 	struct VtkSnapshotter {
 		/// list of physical quantities to write to vtk

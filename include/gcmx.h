@@ -163,6 +163,57 @@ gcmx_status gcmx_halo_exchange(gcmx_ctx* ctx);
  * any slab.  Call it before each time step, like the RCCL exchange. */
 gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n);
 
+/* ---- simplex (tetrahedral) stage ----------------------------------------------
+ * The device half of simplex::GridCharacteristicMethodInRiemannInvariants
+ * (engine/simplex/GridCharacteristicMethodInRiemannInvariants.hpp:44-198) for one
+ * body with the global calculation basis (BorderCalcMode::GLOBAL_BASIS,
+ * SplittingType::PRODUCT, engine/simplex/Engine.cpp:117-148).  The mesh walk
+ * (SimplexGrid::findCellCrossedByTheRay, SimplexGrid.cpp:57-164) is static for a
+ * static mesh and basis, so the host resolves every characteristic foot once
+ * (gcm_amd/host/simplex.cpp) and hands the result over as gsx_foot records.
+ * Node arrays use the reference's per-vertex order (local vertex index), M = 9
+ * doubles per node (AoS) at the boundary, SoA on the device. */
+typedef struct gsx_ctx gsx_ctx;
+
+typedef enum gsx_foot_kind {
+	GSX_FOOT_CELL = 0,      /* foot inside a cell: hybridInterpolate (TetrahedronInterpolator.hpp:93-104) */
+	GSX_FOOT_OUTER = 1,     /* outer invariant of a border node: 0 (:160-198, :57-95)  */
+	GSX_FOOT_SPACETIME = 2, /* ray leaves through a border face: interpolateInSpaceTime
+	                           (common.hpp:102-129) over the face's current and new values */
+	GSX_FOOT_ZERO = 3       /* walk ended on a single vertex: u = 0 (:186-196, no branch) */
+} gsx_foot_kind;
+
+typedef struct gsx_foot {
+	int kind;       /* gsx_foot_kind                                                 */
+	int v[4];       /* CELL: the cell's vertices; SPACETIME: v[0..2] = the border face */
+	int slot[4];    /* SPACETIME: value each weight multiplies, 0..2 = current layer of
+	                   v[0..2], 3..5 = new layer of v[0..2] (interpolateInOwner order)  */
+	double lam[4];  /* barycentric weights                                            */
+	double q[3];    /* CELL: the foot (query point) for the gradient terms            */
+} gsx_foot;
+
+gcmx_status gsx_create(int device, int n_nodes, const double* coords /* [n][3] */, gsx_ctx** out);
+void        gsx_destroy(gsx_ctx* ctx);
+/* GcmMatrices of the inner basis: U, U1 [3 stages][9*9] row-major (ElasticModel<3>
+ * ::constructGcmMatrices with the calculation basis, ElasticModel.hpp:57-65). */
+gcmx_status gsx_set_matrices(gsx_ctx* ctx, const double* U, const double* U1);
+/* Differentiation::estimateGradient (util/math/Differentiation.hpp:33-63): per node
+ * its neighbours (CSR offsets[n+1], neighbors), the LSQ rows d (3 per entry), the
+ * weights 1/|d|, the normal matrix A^T W A [9] and its determinant. */
+gcmx_status gsx_set_gradient_plan(gsx_ctx* ctx, const int* offsets, const int* neighbors,
+                                  const double* rows, const double* weights, const double* M,
+                                  const double* det);
+/* Feet of stage `stage`: feet[n_nodes][6] (invariants 0..5), the border nodes
+ * (contactAndBorderStage) and the inner nodes (innerStage), in calculation order. */
+gcmx_status gsx_set_stage_plan(gsx_ctx* ctx, int stage, const gsx_foot* feet, int n_border,
+                               const int* border_nodes, int n_inner, const int* inner_nodes);
+gcmx_status gsx_upload(gsx_ctx* ctx, const double* aos /* [n][9] */);
+gcmx_status gsx_download(gsx_ctx* ctx, double* aos);
+/* One stage: beforeStage (invariants + gradients), contactAndBorderStage,
+ * innerStage, afterStage (U1) and the PRODUCT swap (engine/simplex/Engine.cpp:117-148). */
+gcmx_status gsx_stage(gsx_ctx* ctx, int stage);
+gcmx_status gsx_sync(gsx_ctx* ctx);
+
 /* ---- synchronisation and timing ------------------------------------------- */
 gcmx_status gcmx_sync(gcmx_ctx* ctx);
 /* The context's compute stream as a hipStream_t (for event timing by callers). */

@@ -1,0 +1,569 @@
+"""CPU oracle for the simplex (tetrahedral) grid-characteristic path.
+
+TEST INFRASTRUCTURE ONLY (see oracle/oracle.py for the rules: only tests/,
+``__graft_entry__.smoke()`` and bench.py's cpu_baseline may import this).
+
+A plain-Python restatement of the reference's simplex stage in Riemann
+invariants for one isotropic-elastic body with a constant calculation basis,
+GLOBAL_BASIS border mode, PRODUCT splitting and border nodes without border
+conditions (non-reflecting):
+
+* triangulation queries over a given tetrahedral mesh (the mesh is INPUT: CGAL,
+  the reference's mesher, is absent; tests take the product's boxMesh output as
+  the task's mesh, like a mesh file): incident cells in ascending cell order,
+  face neighbours, the line walk of grid/simplex/cgal/LineWalker.hpp:25-88 and
+  SimplexGrid::findCellCrossedByTheRay (grid/simplex/SimplexGrid.cpp:57-164);
+* Differentiation::estimateGradient (util/math/Differentiation.hpp:33-63);
+* GridCharacteristicMethodInRiemannInvariants (engine/simplex/
+  GridCharacteristicMethodInRiemannInvariants.hpp:44-198) with
+  TetrahedronInterpolator::hybridInterpolate / interpolateInOwner
+  (util/math/interpolation/TetrahedronInterpolator.hpp:93-155) and
+  interpolateInSpaceTime (engine/simplex/common.hpp:102-129);
+* simplex::Engine::nextTimeStep / gcmStage (engine/simplex/Engine.cpp:82-123).
+
+Every expression keeps the reference's operation order on Python floats (IEEE
+double), so results are bit-for-bit comparable.  Parity against the reference
+itself is UNPINNED: CGAL is absent, so neither the reference's meshes nor its
+simplex outputs can be produced here; the only in-repo pins are structural
+(TestSimplexGcm.cpp:29-67, zero state stays zero), checked in tests.
+Paths are relative to /root/reference/src/libgcm.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence, Tuple
+
+EQUALITY_TOLERANCE = 1e-9   # util/infrastructure/Types.hpp:10
+MAX_NB = 20                 # Cgal3DTriangulation.hpp:53
+RIGHT = [1, 3, 5]           # rheology/models/Model.cpp:81-82
+LEFT = [0, 2, 4]
+
+
+# -------------------------------------------------------------- linal --
+
+def _sub(a, b):
+    return (a[0] - b[0], a[1] - b[1], a[2] - b[2])
+
+
+def _add(a, b):
+    return (a[0] + b[0], a[1] + b[1], a[2] + b[2])
+
+
+def _mul(a, x):
+    return (a[0] * x, a[1] * x, a[2] * x)
+
+
+def _dot(a, b):  # linal/functions.hpp:327-334
+    r = a[0] * b[0]
+    r += a[1] * b[1]
+    r += a[2] * b[2]
+    return r
+
+
+def _length(a):
+    return math.sqrt(_dot(a, a))
+
+
+def _cross(a, b):  # linal/geometry.hpp:13-17
+    return (a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0])
+
+
+def _det3(m11, m12, m13, m21, m22, m23, m31, m32, m33):  # linal/determinants.hpp:40-53
+    return m11 * (m22 * m33 - m23 * m32) - m12 * (m21 * m33 - m23 * m31) + \
+        m13 * (m21 * m32 - m22 * m31)
+
+
+def _det2(m11, m12, m21, m22):
+    return m11 * m22 - m12 * m21
+
+
+def _solve3(A, b):  # linal/linearSystems.hpp:104-129
+    det = _det3(A[0][0], A[0][1], A[0][2], A[1][0], A[1][1], A[1][2], A[2][0], A[2][1], A[2][2])
+    if det == 0:
+        raise ValueError("SLE determinant is zero")
+    d1 = _det3(b[0], A[0][1], A[0][2], b[1], A[1][1], A[1][2], b[2], A[2][1], A[2][2])
+    d2 = _det3(A[0][0], b[0], A[0][2], A[1][0], b[1], A[1][2], A[2][0], b[2], A[2][2])
+    d3 = _det3(A[0][0], A[0][1], b[0], A[1][0], A[1][1], b[1], A[2][0], A[2][1], b[2])
+    return (d1 / det, d2 / det, d3 / det)
+
+
+def _tmul_cols(cols, b):
+    """transposeMultiply(A, b) for A given by columns (functions.hpp:220-234)."""
+    out = []
+    for c in cols:
+        s = c[0] * b[0]
+        for n in range(1, len(b)):
+            s += c[n] * b[n]
+        out.append(s)
+    return out
+
+
+def _lls32(c0, c1, b):  # linearLeastSquares 3x2, W = I (linearSystems.hpp:150-158)
+    cols = [c0, c1]
+    M = [[_tmul_cols([ci], cj)[0] for cj in cols] for ci in cols]
+    r = _tmul_cols(cols, b)
+    det = _det2(M[0][0], M[0][1], M[1][0], M[1][1])
+    if det == 0:
+        raise ValueError("SLE determinant is zero")
+    return (_det2(r[0], M[0][1], r[1], M[1][1]) / det, _det2(M[0][0], r[0], M[1][0], r[1]) / det)
+
+
+def _lls31(c0, b):
+    m = _tmul_cols([c0], c0)[0]
+    r = _tmul_cols([c0], b)[0]
+    if m == 0:
+        raise ValueError("SLE determinant is zero")
+    return r / m
+
+
+def barycentric4(a, b, c, d, q):  # geometry.hpp:142-151
+    T = [[a[0] - d[0], b[0] - d[0], c[0] - d[0]],
+         [a[1] - d[1], b[1] - d[1], c[1] - d[1]],
+         [a[2] - d[2], b[2] - d[2], c[2] - d[2]]]
+    l = _solve3(T, _sub(q, d))
+    return (l[0], l[1], l[2], 1 - l[0] - l[1] - l[2])
+
+
+def _barycentric3(a, b, c, q):  # geometry.hpp:124-137
+    l = _lls32(_sub(a, c), _sub(b, c), _sub(q, c))
+    return (l[0], l[1], 1 - l[0] - l[1])
+
+
+def _barycentric2(a, b, q):  # geometry.hpp:88-103
+    l = _lls31(_sub(a, b), _sub(q, b))
+    return (l, 1 - l)
+
+
+def oriented_volume(a, b, c, d):  # geometry.hpp:248-255
+    ba, ca, da = _sub(b, a), _sub(c, a), _sub(d, a)
+    return _det3(ba[0], ba[1], ba[2], ca[0], ca[1], ca[2], da[0], da[1], da[2]) / 6
+
+
+def _volume(a, b, c, d):
+    return abs(oriented_volume(a, b, c, d))
+
+
+def _area(a, b, c):
+    return _length(_cross(_sub(b, a), _sub(c, a))) / 2
+
+
+def _min_height3(a, b, c):
+    S = _area(a, b, c)
+    ab, ac, bc = _length(_sub(a, b)), _length(_sub(a, c)), _length(_sub(b, c))
+    return 2 * S / max(ab, max(ac, bc))
+
+
+def min_height4(a, b, c, d):  # geometry.hpp:274-284
+    V = _volume(a, b, c, d)
+    A, B, C, D = _area(b, c, d), _area(c, d, a), _area(d, a, b), _area(a, b, c)
+    return 3 * V / max(A, max(B, max(C, D)))
+
+
+def _degenerate3(a, b, c, eps):
+    h = _min_height3(a, b, c)
+    l = (_length(_sub(a, b)) + _length(_sub(a, c)) + _length(_sub(b, c))) / 3
+    return h <= eps * l
+
+
+def _degenerate4(a, b, c, d, eps):
+    h = min_height4(a, b, c, d)
+    l = (_length(_sub(a, b)) + _length(_sub(a, c)) + _length(_sub(a, d)) + _length(_sub(d, b)) +
+         _length(_sub(d, c)) + _length(_sub(b, c))) / 6
+    return h <= eps * l
+
+
+def _segment_contains(a, b, q, eps, deg):
+    if not _degenerate3(a, b, q, deg):
+        return False
+    l = _barycentric2(a, b, q)
+    return l[0] >= -eps and l[1] >= -eps
+
+
+def _triangle_contains(a, b, c, q, eps, deg):
+    if not _degenerate4(a, b, c, q, deg):
+        return False
+    l = _barycentric3(a, b, c, q)
+    return l[0] >= -eps and l[1] >= -eps and l[2] >= -eps
+
+
+def _tet_contains(a, b, c, d, q, eps):
+    l = barycentric4(a, b, c, d, q)
+    return l[0] >= -eps and l[1] >= -eps and l[2] >= -eps and l[3] >= -eps
+
+
+def _solid_angle_contains(a, b, c, d, q, eps):
+    l = barycentric4(a, b, c, d, q)
+    return l[0] <= 1 + eps and l[1] >= -eps and l[2] >= -eps and l[3] >= -eps
+
+
+def _line_flat(f1, f2, f3, l1, l2):  # geometry.hpp:201-217
+    tau, p, q = _sub(l2, l1), _sub(f2, f1), _sub(f3, f1)
+    A = [[tau[0], -p[0], -q[0]], [tau[1], -p[1], -q[1]], [tau[2], -p[2], -q[2]]]
+    params = _solve3(A, _sub(f1, l1))
+    return _add(l1, _mul(tau, params[0]))
+
+
+# --------------------------------------------------------------- grid --
+
+class Grid:
+    """SimplexGrid<3> over a given mesh (coords [n][3], cells [m][4])."""
+
+    def __init__(self, coords: Sequence[Sequence[float]], cells: Sequence[Sequence[int]]):
+        self.P = [tuple(float(x) for x in c) for c in coords]
+        self.cells = [tuple(int(x) for x in c) for c in cells]
+        nv = len(self.P)
+        faces = {}
+        self.nb = [[-1] * 4 for _ in self.cells]
+        for ci, c in enumerate(self.cells):
+            for i in range(4):
+                f = tuple(sorted((c[(i + 1) % 4], c[(i + 2) % 4], c[(i + 3) % 4])))
+                if f in faces:
+                    cj, j = faces.pop(f)
+                    self.nb[ci][i] = cj
+                    self.nb[cj][j] = ci
+                else:
+                    faces[f] = (ci, i)
+        self.inc = [[] for _ in range(nv)]
+        for ci, c in enumerate(self.cells):
+            for x in c:
+                self.inc[x].append(ci)
+        self.inner = [True] * nv
+        for ci, c in enumerate(self.cells):
+            for i in range(4):
+                if self.nb[ci][i] < 0:
+                    for k in range(1, 4):
+                        self.inner[c[(i + k) % 4]] = False
+        self.inner_idx = [i for i in range(nv) if self.inner[i]]
+        self.border_idx = [i for i in range(nv) if not self.inner[i]]
+        self.average_height = self._average_height()
+
+    def _average_height(self):  # SimplexGrid.cpp:266-285 + util/math/Histogram.hpp
+        hs = [min_height4(*[self.P[x] for x in c]) for c in self.cells]
+        mn, mx = min(hs), max(hs)
+        nbins = 100
+        bs0 = (mx - mn) / float(nbins)
+        if mx == mn:
+            bins = [0] * nbins
+            bins[0] = len(hs)
+        else:
+            bins = [0] * (nbins + 1)
+            for h in hs:
+                bins[int((h - mn) / bs0)] += 1
+            bins[nbins - 1] += bins[-1]
+            bins.pop()
+        bs = (mx - mn) / float(len(bins))
+        ip, cnt = 0.0, 0.0
+        for i, b in enumerate(bins):
+            ip = ip + float(b) * (mn + (float(i) + 0.5) * bs)
+            cnt = cnt + float(b)
+        return ip / cnt
+
+    def neighbors(self, it) -> List[int]:  # SimplexGrid.hpp:249-259
+        s = set()
+        for c in self.inc[it]:
+            s.update(self.cells[c])
+        s.discard(it)
+        return sorted(s)
+
+    def _other_index(self, cell, a, b, c):
+        for i in range(4):
+            d = self.cells[cell][i]
+            if d != a and d != b and d != c:
+                return i
+        raise ValueError("Cell contains equal vertices")
+
+    def _crossed_incident(self, vh, query, eps):  # Cgal3DTriangulation.hpp:221-238
+        for cand in self.inc[vh]:
+            t = self.cells[cand]
+            a = t[self._other_index(cand, vh, vh, vh)]
+            b = t[self._other_index(cand, vh, vh, a)]
+            c = t[self._other_index(cand, vh, a, b)]
+            if _solid_angle_contains(self.P[vh], self.P[a], self.P[b], self.P[c], query, eps):
+                return cand
+        return -1
+
+    def _inside_out_facet(self, t, q, p, eps):  # Cgal3DTriangulation.hpp:247-259
+        for i in range(4):
+            a, b, c = (self.cells[t][(i + k) % 4] for k in (1, 2, 3))
+            if _solid_angle_contains(q, self.P[a], self.P[b], self.P[c], p, eps):
+                return a, b, c
+        return None
+
+    def _collect(self, q, p, t, u, v, w):  # LineWalker.hpp:25-52
+        P = self.P
+        ans, last_face = [t], None
+        while oriented_volume(P[u], P[v], P[w], p) < 0:
+            nt = self.nb[t][self._other_index(t, u, v, w)]
+            if nt < 0:
+                ans.append(-1)
+                last_face = (u, v, w)
+                break
+            t = nt
+            ans.append(t)
+            s = self.cells[t][self._other_index(t, u, v, w)]
+            if oriented_volume(P[u], P[s], q, p) > 0:
+                if oriented_volume(P[v], P[s], q, p) > 0:
+                    u = s
+                else:
+                    w = s
+            else:
+                if oriented_volume(P[w], P[s], q, p) > 0:
+                    v = s
+                else:
+                    u = s
+        return ans, last_face
+
+    def _along_from_vertex(self, q, p):  # LineWalker.hpp:54-69
+        t = self._crossed_incident(q, p, 0.0)
+        if t < 0:
+            return [], None
+        c = self.cells[t]
+        u = c[self._other_index(t, q, q, q)]
+        v = c[self._other_index(t, q, q, u)]
+        w = c[self._other_index(t, q, u, v)]
+        if oriented_volume(self.P[u], self.P[v], self.P[w], self.P[q]) < 0:
+            u, v = v, u
+        return self._collect(self.P[q], p, t, u, v, w)
+
+    def _along_from_cell(self, t, q, p):  # LineWalker.hpp:71-88
+        f = self._inside_out_facet(t, q, p, 0.0)
+        if f is None:
+            f = self._inside_out_facet(t, q, p, EQUALITY_TOLERANCE)
+        if f is None:
+            return [], None
+        u, v, w = f
+        if oriented_volume(self.P[u], self.P[v], self.P[w], q) < 0:
+            u, v = v, u
+        return self._collect(q, p, t, u, v, w)
+
+    def _contains(self, c, q):
+        return _tet_contains(*[self.P[x] for x in self.cells[c]], q, EQUALITY_TOLERANCE)
+
+    def _check(self, it, along, last_face, start, query):  # SimplexGrid.cpp:115-164
+        if not along:
+            return []
+        last = along[-1]
+        if last >= 0 and self._contains(last, query):
+            return list(self.cells[last])
+        if len(along) == 1:
+            if self.inner[it]:
+                raise ValueError("one-cell walk from an inner node")
+            return []
+        prev = along[-2]
+        if self._contains(prev, query):
+            return list(self.cells[prev])
+        if not self.inner[it]:
+            return []
+        if last < 0:
+            face = [x for x in self.cells[prev] if x in last_face]
+            p = [self.P[x] for x in face]
+            x = _line_flat(p[0], p[1], p[2], start, query)
+            if _triangle_contains(p[0], p[1], p[2], x, EQUALITY_TOLERANCE, EQUALITY_TOLERANCE):
+                return face
+            for i in range(3):
+                for j in range(i + 1, 3):
+                    if _segment_contains(p[i], p[j], x, EQUALITY_TOLERANCE, EQUALITY_TOLERANCE):
+                        return [face[i], face[j]]
+            for i in range(3):
+                if _segment_contains(start, query, p[i], EQUALITY_TOLERANCE, EQUALITY_TOLERANCE):
+                    return [face[i]]
+            return []
+        return []
+
+    def find_cell(self, it, shift) -> List[int]:  # SimplexGrid.cpp:57-112
+        start = self.P[it]
+        query = _add(start, shift)
+        along, lf = self._along_from_vertex(it, query)
+        found = self._check(it, along, lf, start, query)
+        if found:
+            return found
+        sc = self._crossed_incident(it, query, 0.0)
+        if sc < 0:
+            sc = self._crossed_incident(it, query, EQUALITY_TOLERANCE)
+        if sc < 0:
+            sc = self.inc[it][0]
+        t = [self.P[x] for x in self.cells[sc]]
+        cen = _add(_add(_add(t[0], t[1]), t[2]), t[3])
+        cen = (cen[0] / 4, cen[1] / 4, cen[2] / 4)
+        w = 1e-3
+        start_point = _add(_mul(cen, w), _mul(start, 1 - w))
+        along, lf = self._along_from_cell(sc, start_point, query)
+        found = self._check(it, along, lf, start, query)
+        if found:
+            return found
+        if self.inner[it]:
+            raise ValueError("line walk failed for an inner node")
+        return []
+
+    # -- Differentiation::estimateGradient -----------------------------------
+    def gradients(self, w: List[List[float]]):
+        """w[node][k] -> grad[node][r][k] (Differentiation.hpp:33-63)."""
+        out = []
+        for it in range(len(self.P)):
+            nbs = self.neighbors(it)[:MAX_NB]
+            A = [[0.0] * 3 for _ in range(MAX_NB)]
+            W = [0.0] * MAX_NB
+            b = [[0.0] * 9 for _ in range(MAX_NB)]
+            for i, nb in enumerate(nbs):
+                d = _sub(self.P[nb], self.P[it])
+                A[i] = list(d)
+                W[i] = 1.0 / _length(d)
+                b[i] = [w[nb][k] - w[it][k] for k in range(9)]
+            WA = [[W[i] * A[i][c] for c in range(3)] for i in range(MAX_NB)]
+            M = [[None] * 3 for _ in range(3)]
+            for r in range(3):
+                for c in range(3):
+                    s = A[0][r] * WA[0][c]
+                    for n in range(1, MAX_NB):
+                        s += A[n][r] * WA[n][c]
+                    M[r][c] = s
+            g = [[0.0] * 9 for _ in range(3)]
+            for k in range(9):
+                Wb = [b[i][k] * W[i] for i in range(MAX_NB)]
+                rhs = []
+                for r in range(3):
+                    s = A[0][r] * Wb[0]
+                    for n in range(1, MAX_NB):
+                        s += A[n][r] * Wb[n]
+                    rhs.append(s)
+                x = _solve3(M, rhs)
+                for r in range(3):
+                    g[r][k] = x[r]
+            out.append(g)
+        return out
+
+
+def _std_min(a, b):
+    return b if b < a else a
+
+
+def _std_max(a, b):
+    return b if a < b else a
+
+
+class Engine:
+    """simplex::Engine<3> for one body (see module docstring)."""
+
+    TRIES = [(0, 1, 2, 3), (0, 1, 2, 4), (0, 1, 2, 5), (0, 1, 3, 4), (0, 1, 3, 5), (0, 1, 4, 5),
+             (0, 2, 3, 4), (0, 2, 3, 5), (0, 2, 4, 5), (0, 3, 4, 5), (1, 2, 3, 4), (1, 2, 3, 5),
+             (1, 2, 4, 5), (1, 3, 4, 5), (2, 3, 4, 5)]
+
+    def __init__(self, coords, cells, U, U1, L, basis, courant, pde0):
+        """U, U1: [3][9][9]; L: [3][9]; basis: 3x3 (column s = stage s); pde0 [n][9]."""
+        self.grid = Grid(coords, cells)
+        self.U = [[[float(x) for x in row] for row in U[s]] for s in range(3)]
+        self.U1 = [[[float(x) for x in row] for row in U1[s]] for s in range(3)]
+        self.L = [[float(x) for x in L[s]] for s in range(3)]
+        self.basis = [[float(basis[r][c]) for c in range(3)] for r in range(3)]
+        mx = 0.0
+        for s in range(3):
+            for k in range(9):
+                mx = max(mx, abs(self.L[s][k]))
+        self.tau = courant * self.grid.average_height / mx  # Engine.hpp:78-92
+        self.u = [[float(x) for x in row] for row in pde0]
+        self.feet = [self._plan(s) for s in range(3)]
+
+    def _plan(self, s):
+        """Per node and invariant 0..5: ('cell', verts, q) | ('outer',) | ('st', face, shift)
+        | ('zero',), as interpolateValuesAround would decide (hpp:156-198)."""
+        g = self.grid
+        direction = (self.basis[0][s], self.basis[1][s], self.basis[2][s])
+        plan = []
+        for it in range(len(g.P)):
+            row, outer = [], []
+            for k in range(6):
+                dx = -self.tau * self.L[s][k]
+                shift = _mul(direction, dx)
+                t = g.find_cell(it, shift)
+                if len(t) == 4:
+                    row.append(("cell", t, _add(g.P[it], shift)))
+                elif len(t) == 0 or (len(t) in (2, 3) and not g.inner[it]):
+                    row.append(("outer",))
+                    outer.append(k)
+                elif len(t) == 3:
+                    row.append(("st", t, shift))
+                elif len(t) == 2:
+                    raise ValueError("This did not occur ever before")
+                else:
+                    row.append(("zero",))
+            if g.inner[it]:
+                if outer:
+                    raise ValueError("outer invariant at an inner node")
+            elif outer != RIGHT and outer != LEFT and len(outer) != 6 and outer:
+                if set(outer) & set(RIGHT):
+                    outer = sorted(set(outer) | set(RIGHT))
+                if set(outer) & set(LEFT):
+                    outer = sorted(set(outer) | set(LEFT))
+                for k in outer:
+                    row[k] = ("outer",)
+            plan.append(row)
+        return plan
+
+    def _interp(self, it, k, foot, w, wn, grads):
+        g = self.grid
+        kind = foot[0]
+        if kind == "cell":
+            verts, q = foot[1], foot[2]
+            c = [g.P[x] for x in verts]
+            lam = barycentric4(c[0], c[1], c[2], c[3], q)
+            if not all(l > -EQUALITY_TOLERANCE for l in lam):
+                raise ValueError("isInterpolation")
+            v = [w[x][k] for x in verts]
+            terms = []
+            for i, x in enumerate(verts):
+                gr = (grads[x][0][k], grads[x][1][k], grads[x][2][k])
+                terms.append(v[i] + _dot(gr, _sub(q, c[i])) / 2.0)
+            quad = lam[0] * terms[0] + lam[1] * terms[1] + lam[2] * terms[2] + lam[3] * terms[3]
+            mn = _std_min(_std_min(_std_min(v[0], v[1]), v[2]), v[3])
+            mx = _std_max(_std_max(_std_max(v[0], v[1]), v[2]), v[3])
+            lim = _std_min(_std_max(quad, mn), mx)
+            if quad == lim:
+                return quad
+            return lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3]
+        if kind == "st":  # common.hpp:102-129
+            face, shift = foot[1], foot[2]
+            r0 = g.P[it]
+            r1, r2, r3 = (g.P[x] for x in face)
+            rc = _line_flat(r1, r2, r3, r0, _add(r0, shift))
+            ww = _lls32(_sub(r2, r1), _sub(r3, r1), _sub(rc, r1))
+            pts = [(0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 0, 1), (0, 1, 1)]
+            vals = [w[face[0]][k], w[face[1]][k], w[face[2]][k],
+                    wn[face[0]][k], wn[face[1]][k], wn[face[2]][k]]
+            qst = (ww[0], ww[1], 1 - _length(_sub(rc, r0)) / _length(shift))
+            for tr in self.TRIES:  # TetrahedronInterpolator::interpolateInOwner
+                if _volume(*[pts[i] for i in tr]) != 0:
+                    lam = barycentric4(*[pts[i] for i in tr], qst)
+                    if all(l > -EQUALITY_TOLERANCE for l in lam):
+                        return lam[0] * vals[tr[0]] + lam[1] * vals[tr[1]] + \
+                            lam[2] * vals[tr[2]] + lam[3] * vals[tr[3]]
+            raise ValueError("Containing tetrahedron is not found")
+        return 0.0
+
+    def _mat_vec(self, M, x):  # linal/operators.hpp:109-123
+        out = []
+        for c in range(9):
+            s = M[c][0] * x[0]
+            for j in range(1, 9):
+                s += M[c][j] * x[j]
+            out.append(s)
+        return out
+
+    def stage(self, s):
+        """gcmStage with PRODUCT splitting (engine/simplex/Engine.cpp:104-123)."""
+        g = self.grid
+        n = len(g.P)
+        w = [self._mat_vec(self.U[s], self.u[i]) for i in range(n)]     # beforeStage
+        grads = g.gradients(w)
+        wn = [[0.0] * 9 for _ in range(n)]
+        for order in (g.border_idx, g.inner_idx):  # contactAndBorderStage, innerStage
+            for it in order:
+                for k in range(9):
+                    if k >= 6:
+                        wn[it][k] = w[it][k]
+                    else:
+                        wn[it][k] = self._interp(it, k, self.feet[s][it][k], w, wn, grads)
+        self.u = [self._mat_vec(self.U1[s], wn[i]) for i in range(n)]   # afterStage + swap
+
+    def step(self):
+        for s in range(3):
+            self.stage(s)

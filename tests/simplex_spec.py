@@ -1,0 +1,29 @@
+"""Shared simplex task builder for the CPU and GPU simplex tests."""
+import numpy as np
+
+from oracle import oracle as O
+from oracle import simplex as S
+
+
+def host_task(n=4, courant=1.0, jitter=0.1, seed=7, snaps=3, pressure=1.0, vector=None):
+    from gcm_amd import _gcm_host as H
+    t = H.Task()
+    t.dimensionality = 3
+    t.grid = "SIMPLEX"
+    t.courant = courant
+    t.number_of_snaps = snaps
+    t.add_body(0, [1, 1, 1], [0, 0, 0])
+    t.set_body_material(0, 4, 2, 1)
+    t.calculation_basis = [1, 0, 0, 0, 1, 0, 0, 0, 1]
+    t.set_simplex_box([n, n, n], [0, 0, 0], [1, 1, 1], jitter, seed)
+    if pressure:
+        t.add_initial_quantity(("sphere", 0.3, (0.5, 0.5, 0.5)), "PRESSURE", pressure)
+    if vector is not None:
+        t.add_initial_vector(("infinite",), list(vector))
+    return t
+
+
+def oracle_engine(plans, courant):
+    """The oracle engine on the product's mesh (input data) with its own matrices."""
+    U, U1, L = O.isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
+    return S.Engine(plans["coords"], plans["cells"], U, U1, L, np.eye(3), courant, plans["pde"])

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_symbols():
     text = open(os.path.join(ROOT, "include", "gcmx.h")).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(gcmx_[a-z_0-9]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b((?:gcmx|gsx)_[a-z_0-9]+)\s*\(", text)))
 
 
 def test_header_declares_the_boundary():

@@ -1,0 +1,43 @@
+"""The simplex stage on the GPU (gsx_* through gcm_amd._gcm_host.SimplexEngine) against
+the oracle's restatement of the reference simplex engine, bitwise, on jittered Kuhn
+meshes of the unit cube -- including Courant numbers that send inner-node feet out
+through border faces (space-time interpolation, common.hpp:102-129) -- and the
+reference's own engine test TestSimplexGcm.ZeroInitialization (TestSimplexGcm.cpp:29-53)."""
+import numpy as np
+import pytest
+
+from tests.simplex_spec import host_task, oracle_engine
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    from gcm_amd import _gcm_host
+    return _gcm_host
+
+
+@pytest.mark.parametrize("n,courant,jitter,seed,steps", [(4, 1.0, 0.1, 7, 3), (4, 2.0, 0.1, 7, 2),
+                                                         (6, 1.3, 0.15, 9, 2)])
+def test_simplex_engine_matches_oracle(H, n, courant, jitter, seed, steps):
+    t = host_task(n, courant, jitter, seed, vector=[0.1 * i for i in range(9)])
+    p = H.simplex_plans(t)
+    e = H.SimplexEngine(t)
+    assert e.time_step == p["tau"]
+    o = oracle_engine(p, courant)
+    e.run_steps(steps)
+    for _ in range(steps):
+        o.step()
+    got = e.pde()
+    want = np.array(o.u)
+    assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"
+    assert np.abs(got).max() > 0
+
+
+def test_simplex_zero_state_stays_zero(H):
+    """TestSimplexGcm.ZeroInitialization: Engine::run from a zero state stays zero."""
+    t = host_task(4, pressure=0.0)
+    e = H.SimplexEngine(t)
+    e.run()
+    assert e.steps == 3
+    assert not np.any(e.pde())

