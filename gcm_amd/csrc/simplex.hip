@@ -6,6 +6,8 @@
 //                         (GridCharacteristicMethodInRiemannInvariants.hpp:44-56)
 //   k_sx_gradient         Differentiation::estimateGradient of w (Differentiation.hpp:33-63)
 //   k_sx_nodes(border)    contactAndBorderStage (hpp:57-95)
+//   k_sx_correct          border correctors, applyInGlobalBasis (BorderCorrector.hpp:118-165,
+//                         256-265), on the border nodes' new invariants
 //   k_sx_nodes(inner)     innerStage (hpp:98-112) -- space-time feet read the border
 //                         nodes' new invariants written by the previous launch
 //   k_sx_transform(U1_s)  afterStage: u_new = U1_s w_new (hpp:115-126), then swap.
@@ -37,6 +39,21 @@ gcmx_status fail(gcmx_status s, const std::string& msg) {
 			return fail(GCMX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
 	} while (0)
 
+struct BorderArgs {  // per-condition data passed by value with every launch
+	int type[GSX_MAX_BORDER_CONDITIONS];
+	double minDet[GSX_MAX_BORDER_CONDITIONS][3];
+	double b[GSX_MAX_BORDER_CONDITIONS][3];
+};
+
+struct BorderDev {
+	int n = 0, nCond = 0;
+	int *nodes = nullptr, *cond = nullptr;
+	double *B = nullptr, *S = nullptr;
+	signed char* outer = nullptr;
+	BorderArgs args{};
+	bool set = false, valuesSet = false;
+};
+
 struct StageDev {
 	gsx_foot* feet = nullptr;
 	int* border = nullptr;
@@ -58,6 +75,7 @@ struct gsx_ctx {
 	double *gRows = nullptr, *gW = nullptr, *gM = nullptr, *gDet = nullptr;
 	bool gradSet = false;
 	StageDev st[3];
+	BorderDev bd;
 };
 
 namespace {
@@ -187,6 +205,166 @@ __global__ __launch_bounds__(256) void k_sx_nodes(const int* __restrict__ nodes,
 	}
 }
 
+// Symmetric-storage slot of sigma(i, j) in the PDE vector (linal/Symmetry.hpp:38-46,
+// VelocitySigmaVariables.hpp:82-96): Vx Vy Vz Sxx Sxy Sxz Syy Syz Szz.
+__device__ __forceinline__ int sym(int i, int j) {
+	const int a = i < j ? i : j, b = i < j ? j : i;
+	return 3 + a * 3 - ((a - 1) * a) / 2 + b - a;
+}
+
+// ElasticModel::applyPlainBorderCorrection (ElasticModel.hpp:202-228) on one PDE vector.
+__device__ void plain_correction(double (&u)[kM], int type, const double* __restrict__ S,
+                                 const double (&b)[3]) {
+	if (type == GSX_FIXED_FORCE) {
+		double sg[3][3], t[3][3], sl[3][3];
+		for (int i = 0; i < 3; i++)
+			for (int j = 0; j < 3; j++) sg[i][j] = u[sym(i, j)];  // getSigmaFrom
+		for (int i = 0; i < 3; i++)  // S_T * sigmaGlobal
+			for (int j = 0; j < 3; j++) {
+				double x = S[0 * 3 + i] * sg[0][j];
+				x += S[1 * 3 + i] * sg[1][j];
+				x += S[2 * 3 + i] * sg[2][j];
+				t[i][j] = x;
+			}
+		for (int i = 0; i < 3; i++)  // (...) * S
+			for (int j = 0; j < 3; j++) {
+				double x = t[i][0] * S[0 * 3 + j];
+				x += t[i][1] * S[1 * 3 + j];
+				x += t[i][2] * S[2 * 3 + j];
+				sl[i][j] = x;
+			}
+		for (int i = 0; i < 3; i++) sl[i][2] = b[i];  // setColumn(D - 1, value)
+		for (int j = 0; j < 3; j++) sl[2][j] = b[j];  // setRow(D - 1, value)
+		for (int i = 0; i < 3; i++)  // S * sigmaLocal
+			for (int j = 0; j < 3; j++) {
+				double x = S[i * 3 + 0] * sl[0][j];
+				x += S[i * 3 + 1] * sl[1][j];
+				x += S[i * 3 + 2] * sl[2][j];
+				t[i][j] = x;
+			}
+		for (int i = 0; i < 3; i++)  // (...) * S_T, then setSigmaTo (row-major writes)
+			for (int j = 0; j < 3; j++) {
+				double x = t[i][0] * S[j * 3 + 0];
+				x += t[i][1] * S[j * 3 + 1];
+				x += t[i][2] * S[j * 3 + 2];
+				u[sym(i, j)] = x;
+			}
+	} else {
+		for (int i = 0; i < 3; i++) {  // velocity = S * value
+			double x = S[i * 3 + 0] * b[0];
+			x += S[i * 3 + 1] * b[1];
+			x += S[i * 3 + 2] * b[2];
+			u[i] = x;
+		}
+	}
+}
+
+// calculateOuterWaveCorrection (common.hpp:186-202) with Omega = the U1 columns
+// `cols` (getColumnsFromGcmMatrices, common.hpp:153-165).
+__device__ bool outer_wave_correction(const double (&u)[kM], const double* __restrict__ U1,
+                                      const int (&cols)[3], const double* __restrict__ B,
+                                      const double (&b)[3], double minValid, double (&value)[kM]) {
+	double M[3][3];
+	for (int i = 0; i < 3; i++)
+		for (int j = 0; j < 3; j++) {
+			double x = B[i * kM + 0] * U1[0 * kM + cols[j]];
+			for (int n = 1; n < kM; n++) x += B[i * kM + n] * U1[n * kM + cols[j]];
+			M[i][j] = x;
+		}
+	const double det = det3(M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1],
+	                        M[2][2]);
+	if (!(fabs(det) > minValid)) return false;
+	double r[3];
+	for (int i = 0; i < 3; i++) {
+		double x = B[i * kM + 0] * u[0];
+		for (int n = 1; n < kM; n++) x += B[i * kM + n] * u[n];
+		r[i] = b[i] - x;
+	}
+	// linal::solveLinearSystem 3x3 (linearSystems.hpp:104-129)
+	const double d1 = det3(r[0], M[0][1], M[0][2], r[1], M[1][1], M[1][2], r[2], M[2][1], M[2][2]);
+	const double d2 = det3(M[0][0], r[0], M[0][2], M[1][0], r[1], M[1][2], M[2][0], r[2], M[2][2]);
+	const double d3 = det3(M[0][0], M[0][1], r[0], M[1][0], M[1][1], r[1], M[2][0], M[2][1], r[2]);
+	const double alpha[3] = {d1 / det, d2 / det, d3 / det};
+	for (int i = 0; i < kM; i++) {
+		double x = U1[i * kM + cols[0]] * alpha[0];
+		x += U1[i * kM + cols[1]] * alpha[1];
+		x += U1[i * kM + cols[2]] * alpha[2];
+		value[i] = x;
+	}
+	return true;
+}
+
+__device__ __forceinline__ void mat_vec(const double* __restrict__ Mx, const double (&in)[kM],
+                                        double (&out)[kM]) {
+#pragma unroll
+	for (int c = 0; c < kM; c++) {
+		double s = Mx[c * kM + 0] * in[0];
+#pragma unroll
+		for (int j = 1; j < kM; j++) s += Mx[c * kM + j] * in[j];
+		out[c] = s;
+	}
+}
+
+// BorderCorrectorInRiemannInvariants::applyInGlobalBasis (BorderCorrector.hpp:256-265):
+// invariants -> PDE (U1), BorderCorrectorInPdeVectors::applyInGlobalBasis (:118-165),
+// PDE -> invariants (U).
+__global__ __launch_bounds__(256) void k_sx_correct(const int* __restrict__ nodes,
+                                                    const int* __restrict__ cond,
+                                                    const double* __restrict__ Bm,
+                                                    const double* __restrict__ Sm,
+                                                    const signed char* __restrict__ outer,
+                                                    const double* __restrict__ U,
+                                                    const double* __restrict__ U1, double* wn,
+                                                    int count, int stage, int N, BorderArgs args) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= count) return;
+	const int n = nodes[t], c = cond[t];
+	const int code = outer[(size_t)stage * count + t];
+	const double* B = Bm + 27 * (size_t)t;
+	const double b[3] = {args.b[c][0], args.b[c][1], args.b[c][2]};
+	const double minValid = args.minDet[c][stage];
+	double w[kM], u[kM];
+	for (int k = 0; k < kM; k++) w[k] = wn[k * N + n];
+	mat_vec(U1, w, u);
+	const int R[3] = {1, 3, 5}, L[3] = {0, 2, 4};  // Model.cpp:81-82
+	if (code == 1 || code == 2) {
+		double v[kM];
+		if (outer_wave_correction(u, U1, code == 1 ? R : L, B, b, minValid, v)) {
+			for (int k = 0; k < kM; k++) u[k] += v[k];
+		} else {
+			plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+		}
+	} else {
+		// double-outer or fully inner: average of both sides (:146-162)
+		double vr[kM], vl[kM];
+		const bool okR = outer_wave_correction(u, U1, R, B, b, minValid, vr);
+		const bool okL = outer_wave_correction(u, U1, L, B, b, minValid, vl);
+		if (okR && okL) {
+			for (int k = 0; k < kM; k++) u[k] += (vr[k] + vl[k]) / 2;
+		} else {
+			plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+		}
+	}
+	mat_vec(U, u, w);
+	for (int k = 0; k < kM; k++) wn[k * N + n] = w[k];
+}
+
+// BorderCorrectorInPdeVectors::applyPlainCorrection (BorderCorrector.hpp:167-178) on
+// the current layer.
+__global__ __launch_bounds__(256) void k_sx_plain(const int* __restrict__ nodes,
+                                                  const int* __restrict__ cond,
+                                                  const double* __restrict__ Sm, double* u_,
+                                                  int count, int N, BorderArgs args) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= count) return;
+	const int n = nodes[t], c = cond[t];
+	const double b[3] = {args.b[c][0], args.b[c][1], args.b[c][2]};
+	double u[kM];
+	for (int k = 0; k < kM; k++) u[k] = u_[k * N + n];
+	plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+	for (int k = 0; k < kM; k++) u_[k * N + n] = u[k];
+}
+
 gcmx_status check(gsx_ctx* c) {
 	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null simplex context");
 	SX_TRY(hipSetDevice(c->device));
@@ -244,6 +422,9 @@ void gsx_destroy(gsx_ctx* c) {
 	void* ptrs[] = {c->coords, c->u, c->un, c->w, c->wn, c->grad, c->mats, c->gOff, c->gNb,
 	                c->gRows, c->gW, c->gM, c->gDet};
 	for (void* p : ptrs)
+		if (p) (void)hipFree(p);
+	void* bptrs[] = {c->bd.nodes, c->bd.cond, c->bd.B, c->bd.S, c->bd.outer};
+	for (void* p : bptrs)
 		if (p) (void)hipFree(p);
 	for (auto& st : c->st) {
 		if (st.feet) (void)hipFree(st.feet);
@@ -349,6 +530,64 @@ gcmx_status gsx_download(gsx_ctx* c, double* aos) {
 	return GCMX_OK;
 }
 
+gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const double* min_det,
+                                int n, const int* nodes, const int* cond, const double* B,
+                                const double* S, const signed char* outer) {
+	gcmx_status s = check(c);
+	if (s) return s;
+	if (n_cond < 0 || n_cond > GSX_MAX_BORDER_CONDITIONS || n < 0 || (n_cond && (!type || !min_det)) ||
+	    (n && (!nodes || !cond || !B || !S || !outer)))
+		return fail(GCMX_ERR_INVALID_ARG, "bad border plan");
+	for (int i = 0; i < n_cond; i++)
+		if (type[i] != GSX_FIXED_FORCE && type[i] != GSX_FIXED_VELOCITY)
+			return fail(GCMX_ERR_INVALID_ARG, "unknown border condition type");
+	for (int i = 0; i < n; i++) {
+		if (nodes[i] < 0 || nodes[i] >= c->N) return fail(GCMX_ERR_INVALID_ARG, "node out of range");
+		if (cond[i] < 0 || cond[i] >= n_cond) return fail(GCMX_ERR_INVALID_ARG, "condition out of range");
+	}
+	for (int i = 0; i < 3 * n; i++)
+		if (outer[i] < 0 || outer[i] > 3) return fail(GCMX_ERR_INVALID_ARG, "bad outer code");
+	SX_TRY(hipStreamSynchronize(c->stream));
+	BorderDev& bd = c->bd;
+	if ((s = upload(&bd.nodes, nodes, (size_t)n)) || (s = upload(&bd.cond, cond, (size_t)n)) ||
+	    (s = upload(&bd.B, B, 27 * (size_t)n)) || (s = upload(&bd.S, S, 9 * (size_t)n)) ||
+	    (s = upload(&bd.outer, outer, 3 * (size_t)n)))
+		return s;
+	bd.n = n;
+	bd.nCond = n_cond;
+	bd.args = BorderArgs{};
+	for (int i = 0; i < n_cond; i++) {
+		bd.args.type[i] = type[i];
+		for (int st = 0; st < 3; st++) bd.args.minDet[i][st] = min_det[i * 3 + st];
+	}
+	bd.set = true;
+	bd.valuesSet = (n_cond == 0);
+	return GCMX_OK;
+}
+
+gcmx_status gsx_set_border_values(gsx_ctx* c, const double* b) {
+	gcmx_status s = check(c);
+	if (s) return s;
+	if (!c->bd.set) return fail(GCMX_ERR_STATE, "border plan not set");
+	if (c->bd.nCond && !b) return fail(GCMX_ERR_INVALID_ARG, "null border values");
+	for (int i = 0; i < c->bd.nCond; i++)
+		for (int k = 0; k < 3; k++) c->bd.args.b[i][k] = b[i * 3 + k];
+	c->bd.valuesSet = true;
+	return GCMX_OK;
+}
+
+gcmx_status gsx_plain_correction(gsx_ctx* c) {
+	gcmx_status s = check(c);
+	if (s) return s;
+	const BorderDev& bd = c->bd;
+	if (!bd.set || !bd.valuesSet) return fail(GCMX_ERR_STATE, "border plan / values not set");
+	if (bd.n)
+		hipLaunchKernelGGL(k_sx_plain, dim3((bd.n + 255) / 256), dim3(256), 0, c->stream, bd.nodes,
+		                   bd.cond, bd.S, c->u, bd.n, c->N, bd.args);
+	SX_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
 gcmx_status gsx_stage(gsx_ctx* c, int stage) {
 	gcmx_status s = check(c);
 	if (s) return s;
@@ -364,6 +603,13 @@ gcmx_status gsx_stage(gsx_ctx* c, int stage) {
 	if (st.nBorder)
 		hipLaunchKernelGGL(k_sx_nodes, dim3((st.nBorder + 255) / 256), blk, 0, c->stream, st.border,
 		                   st.nBorder, st.feet, c->coords, c->w, c->grad, c->wn, N);
+	const BorderDev& bd = c->bd;
+	if (bd.set && bd.n) {
+		if (!bd.valuesSet) return fail(GCMX_ERR_STATE, "border values not set");
+		hipLaunchKernelGGL(k_sx_correct, dim3((bd.n + 255) / 256), blk, 0, c->stream, bd.nodes,
+		                   bd.cond, bd.B, bd.S, bd.outer, c->mats + stage * 81,
+		                   c->mats + 3 * 81 + stage * 81, c->wn, bd.n, stage, N, bd.args);
+	}
 	if (st.nInner)
 		hipLaunchKernelGGL(k_sx_nodes, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
 		                   st.nInner, st.feet, c->coords, c->w, c->grad, c->wn, N);

@@ -39,7 +39,8 @@ SYMBOLS = [
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_inner_nodes",
     "gcmx_all_nodes", "gcmx_device_bytes",
     "gsx_create", "gsx_destroy", "gsx_set_matrices", "gsx_set_gradient_plan",
-    "gsx_set_stage_plan", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
+    "gsx_set_stage_plan", "gsx_set_border_plan", "gsx_set_border_values",
+    "gsx_plain_correction", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
 ]
 
 

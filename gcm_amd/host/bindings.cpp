@@ -177,6 +177,15 @@ py::dict simplexPlans(const Task& task) {
 	d["grad_rows"] = p.gradient.rows; d["grad_weights"] = p.gradient.weights;
 	d["grad_M"] = p.gradient.M; d["grad_det"] = p.gradient.det;
 	d["stages"] = stages;
+	py::list outer;
+	for (int s = 0; s < 3; s++) outer.append(std::vector<int>(p.stages[s].outerCode.begin(), p.stages[s].outerCode.end()));
+	d["outer_code"] = outer;
+	const auto& b = p.border;
+	py::dict bd;
+	bd["type"] = b.type; bd["min_det"] = b.minDet; bd["nodes"] = b.nodes; bd["cond"] = b.cond;
+	bd["normal"] = b.normal; bd["B"] = b.B; bd["S"] = b.S;
+	bd["outer"] = std::vector<int>(b.outer.begin(), b.outer.end());
+	d["border_plan"] = bd;
 	return d;
 }
 
@@ -310,7 +319,22 @@ PYBIND11_MODULE(_gcm_host, m) {
 		         bc.area = makeArea(area);
 		         for (auto& kv : values) bc.values[quantity(kv.first)] = kv.second;
 		         t.cubicBorderConditions[body].push_back(bc);
-	         });
+	         })
+	    .def("add_simplex_border_condition",
+	         [](Task& t, py::tuple area, const std::string& type,
+	            std::vector<std::function<real(real)>> values, bool useForMulticontactNodes) {
+		         // Task::borderConditions (Task.hpp:204-213)
+		         Task::BorderCondition bc;
+		         bc.area = makeArea(area);
+		         if (type == "FIXED_FORCE") bc.type = BorderConditions::T::FIXED_FORCE;
+		         else if (type == "FIXED_VELOCITY") bc.type = BorderConditions::T::FIXED_VELOCITY;
+		         else throw Exception("unknown border condition type " + type);
+		         bc.values = std::move(values);
+		         bc.useForMulticontactNodes = useForMulticontactNodes;
+		         t.borderConditions.push_back(bc);
+	         },
+	         py::arg("area"), py::arg("type"), py::arg("values"),
+	         py::arg("use_for_multicontact_nodes") = true);
 
 	m.def(
 	    "host_state",

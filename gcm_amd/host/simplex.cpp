@@ -526,6 +526,7 @@ StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[
 	const int nv = m.nVertices();
 	StagePlan plan;
 	plan.feet.assign((size_t)nv * 6, gsx_foot{});
+	plan.outerCode.assign((size_t)nv, 0);
 	plan.borderNodes = grid.borderIdx;
 	plan.innerNodes = grid.innerIdx;
 	static const std::vector<int> RIGHT = {1, 3, 5}, LEFT = {0, 2, 4};  // Model.cpp:81-82
@@ -608,8 +609,104 @@ StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[
 			if (!inter(outer, LEFT).empty()) outer = uni(outer, LEFT);
 			for (int k : outer) plan.feet[(size_t)it * 6 + k].kind = GSX_FOOT_OUTER;
 		}
+		if (outer == RIGHT) plan.outerCode[it] = 1;
+		else if (outer == LEFT) plan.outerCode[it] = 2;
+		else if (!outer.empty()) plan.outerCode[it] = 3;  // all six after the completion
 	}
 	return plan;
+}
+
+std::array<real, 27> borderMatrix(BorderConditions::T type, const Real3& normal) {
+	std::array<real, 27> B{};
+	real S[3][3];
+	detail::localBasisOf<3>(normal.data(), S);
+	if (type == BorderConditions::T::FIXED_FORCE) {
+		// G_k(i, j) += S(i, k) p(j) over a SymmetricMatrix (Symmetry.hpp:38-46), so
+		// an off-diagonal slot collects both (i, j) and (j, i); setSigma copies it.
+		for (int k = 0; k < 3; k++) {
+			real G[6] = {0, 0, 0, 0, 0, 0};
+			for (int i = 0; i < 3; i++)
+				for (int j = 0; j < 3; j++) {
+					const int a = std::min(i, j), b = std::max(i, j);
+					G[a * 3 - ((a - 1) * a) / 2 + b - a] += S[i][k] * normal[j];
+				}
+			for (int q = 0; q < 6; q++) B[(size_t)k * 9 + 3 + q] = G[q];
+		}
+	} else {
+		for (int i = 0; i < 3; i++)
+			for (int j = 0; j < 3; j++) B[(size_t)i * 9 + j] = S[j][i];  // setVelocity(S column i)
+	}
+	return B;
+}
+
+namespace {
+/// calculateOuterWaveCorrection's |det(B * Omega)| (common.hpp:186-202)
+real outerDeterminantFabs(const std::array<real, 27>& B, const std::array<real, 81>& U1,
+                          const int cols[3]) {
+	real M[3][3];
+	for (int i = 0; i < 3; i++)
+		for (int j = 0; j < 3; j++) {
+			real x = B[(size_t)i * 9 + 0] * U1[(size_t)0 * 9 + cols[j]];
+			for (int n = 1; n < 9; n++) x += B[(size_t)i * 9 + n] * U1[(size_t)n * 9 + cols[j]];
+			M[i][j] = x;
+		}
+	return std::fabs(det3(M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1],
+	                      M[2][2]));
+}
+}  // namespace
+
+BorderPlan buildBorderPlan(const Task& task, const Grid& grid, const GcmMatrices<3>& matrices,
+                           const real calc[3][3], const StagePlan stages[3]) {
+	BorderPlan bp;
+	const auto& conds = task.borderConditions;
+	if (conds.size() > GSX_MAX_BORDER_CONDITIONS) throw Exception("too many border conditions");
+	for (const auto& c : conds) {
+		if (!c.area) throw Exception("border condition without area");
+		if (c.values.size() != 3) throw Exception("border condition needs OUTER_NUMBER = 3 values");
+		bp.type.push_back(c.type == BorderConditions::T::FIXED_FORCE ? GSX_FIXED_FORCE
+		                                                             : GSX_FIXED_VELOCITY);
+	}
+	std::vector<int> count(conds.size(), 0);
+	for (int it : grid.borderIdx) {  // Engine::addBorderNode (Engine.cpp:292-309)
+		const Real3 bn = grid.borderNormal(it);
+		const bool isMulticontact = bn[0] == 0 && bn[1] == 0 && bn[2] == 0;
+		int chosen = -1;
+		for (size_t c = 0; c < conds.size(); c++)
+			if (conds[c].area->contains(grid.mesh.v[it]) &&
+			    (!isMulticontact || conds[c].useForMulticontactNodes))
+				chosen = (int)c;
+		if (chosen < 0) continue;
+		const Real3 n = bn;  // commonNormal == borderNormal for one body
+		if (isMulticontact) throw Exception("zero border normal at a border-condition node");
+		bp.nodes.push_back(it);
+		bp.cond.push_back(chosen);
+		count[(size_t)chosen]++;
+		for (int r = 0; r < 3; r++) bp.normal.push_back(n[r]);
+		const auto B = borderMatrix(conds[(size_t)chosen].type, n);
+		bp.B.insert(bp.B.end(), B.begin(), B.end());
+		real S[3][3];
+		detail::localBasisOf<3>(n.data(), S);
+		for (int r = 0; r < 3; r++)
+			for (int c = 0; c < 3; c++) bp.S.push_back(S[r][c]);
+	}
+	const size_t nn = bp.nodes.size();
+	bp.outer.assign(3 * nn, 0);
+	for (int s = 0; s < 3; s++)
+		for (size_t i = 0; i < nn; i++) bp.outer[s * nn + i] = stages[s].outerCode[(size_t)bp.nodes[i]];
+	// getMaximalPossibleDeterminant (BorderCorrector.hpp:198-214): B along the stage
+	// direction, RIGHT outer columns; the correction's threshold is 1e-3 of it.
+	static const int RIGHT[3] = {1, 3, 5};
+	bp.minDet.assign(3 * conds.size(), 0.0);
+	for (size_t c = 0; c < conds.size(); c++) {
+		if (!count[c]) continue;  // applyInGlobalBasis returns before (hpp:124)
+		for (int s = 0; s < 3; s++) {
+			const Real3 dir = {calc[0][s], calc[1][s], calc[2][s]};
+			const real det = outerDeterminantFabs(borderMatrix(conds[c].type, dir), matrices.m[s].U1, RIGHT);
+			if (!(det > 0)) throw Exception("degenerate outer-wave system along the stage direction");
+			bp.minDet[c * 3 + s] = 1e-3 * det;
+		}
+	}
+	return bp;
 }
 
 }  // namespace simplex
@@ -656,6 +753,7 @@ HostPlans buildHostPlans(const Task& task) {
 		const Real3 dir = {calc[0][s], calc[1][s], calc[2][s]};
 		p.stages[s] = buildStagePlan(grid, dir, p.matrices.m[s].L.data(), p.tau);
 	}
+	p.border = buildBorderPlan(task, grid, p.matrices, calc, p.stages);
 	p.borderIdx = grid.borderIdx;
 	p.innerIdx = grid.innerIdx;
 	// InitialCondition::apply (util/task/InitialCondition.hpp:23-88): vectors and quantities
@@ -713,16 +811,40 @@ Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
 		          "gsx_set_stage_plan");
 	}
 	gcmxCheck(gsx_upload(ctx, p.pde.data()), "gsx_upload");
+	conditions = task.borderConditions;
+	const auto& b = p.border;
+	if (!conditions.empty()) {
+		gcmxCheck(gsx_set_border_plan(ctx, (int)b.type.size(), b.type.data(), b.minDet.data(),
+		                              (int)b.nodes.size(), b.nodes.data(), b.cond.data(), b.B.data(),
+		                              b.S.data(), b.outer.data()),
+		          "gsx_set_border_plan");
+		hasBorderPlan = true;
+		// applyPlainBorderContactCorrection(Clock::Time()) (Engine.cpp:44)
+		setBorderValues(Clock::Time());
+		gcmxCheck(gsx_plain_correction(ctx), "gsx_plain_correction");
+	}
 	afterConstruction(task);
+}
+
+void Engine::setBorderValues(real time) {
+	std::vector<double> v;
+	for (const auto& c : conditions)
+		for (const auto& f : c.values) v.push_back(f(time));  // BorderCondition::b (:33-40)
+	gcmxCheck(gsx_set_border_values(ctx, v.data()), "gsx_set_border_values");
 }
 
 Engine::~Engine() { gsx_destroy(ctx); }
 
 real Engine::estimateTimeStep() { return tau; }
 
-// simplex::Engine::nextTimeStep (engine/simplex/Engine.cpp:82-100) with a
-// constant basis and no border / contact correctors: the three gcmStage calls.
+// simplex::Engine::nextTimeStep (engine/simplex/Engine.cpp:95-116) with a
+// constant basis: plain border correction at the next time layer, then the three
+// gcmStage calls (the border correctors run inside gsx_stage with b(t + tau)).
 void Engine::nextTimeStep() {
+	if (hasBorderPlan) {
+		setBorderValues(Clock::Time() + Clock::TimeStep());
+		gcmxCheck(gsx_plain_correction(ctx), "gsx_plain_correction");
+	}
 	for (int stage = 0; stage < 3; stage++) gcmxCheck(gsx_stage(ctx, stage), "gsx_stage");
 }
 

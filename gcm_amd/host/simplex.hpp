@@ -93,6 +93,21 @@ private:
 struct StagePlan {
 	std::vector<gsx_foot> feet;  // [node][6] invariants 0..5 (6..8 have dx == 0)
 	std::vector<int> borderNodes, innerNodes;
+	/// waveIndices of every node after contactAndBorderStage: 0 none, 1 RIGHT,
+	/// 2 LEFT, 3 both (gsx_set_border_plan's outer codes)
+	std::vector<signed char> outerCode;
+};
+
+/// Border correctors of the body: the Border list of Engine::createMeshes
+/// (engine/simplex/Engine.cpp:76-84) filled by addBorderNode (:292-309), with
+/// the per-node data BorderCorrectorInPdeVectors needs (gsx_set_border_plan).
+struct BorderPlan {
+	std::vector<int> type;           // per condition (gsx_border_type)
+	std::vector<double> minDet;      // [cond][3]
+	std::vector<int> nodes, cond;    // corrected nodes and their condition
+	std::vector<double> normal;      // [n][3] commonNormal
+	std::vector<double> B, S;        // [n][27] border matrix, [n][9] local basis
+	std::vector<signed char> outer;  // [3][n]
 };
 
 /// The LSQ gradient operator of every node (gsx_set_gradient_plan).
@@ -110,6 +125,13 @@ GradientPlan buildGradientPlan(const Grid& grid);
 /// bookkeeping of contactAndBorderStage (:57-95).
 StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[9], real tau);
 
+/// ElasticModel::borderMatrixFixedForce / borderMatrixFixedVelocity
+/// (rheology/models/ElasticModel.hpp:111-154), 3 x 9 row-major.
+std::array<real, 27> borderMatrix(BorderConditions::T type, const Real3& normal);
+
+BorderPlan buildBorderPlan(const Task& task, const Grid& grid, const GcmMatrices<3>& matrices,
+                           const real calc[3][3], const StagePlan stages[3]);
+
 }  // namespace simplex
 }  // namespace gcm
 
@@ -120,8 +142,9 @@ namespace simplex {
 
 /// simplex::Engine<3, CgalTriangulation> (engine/simplex/Engine.{hpp,cpp}) for one
 /// isotropic-elastic body: GcmType ADVECT_RIEMANN_INVARIANTS, SplittingType
-/// PRODUCT, BorderCalcMode GLOBAL_BASIS, constant Task::calculationBasis, border
-/// nodes without border conditions (outer invariants zero, i.e. non-reflecting).
+/// PRODUCT, BorderCalcMode GLOBAL_BASIS, constant Task::calculationBasis,
+/// Task::borderConditions through the border correctors (FIXED_FORCE,
+/// FIXED_VELOCITY); border nodes no condition covers keep zero outer invariants.
 class Engine : public AbstractEngine {
 public:
 	explicit Engine(const Task& task, int device = 0);
@@ -142,6 +165,9 @@ private:
 	std::unique_ptr<Grid> grid_;
 	gsx_ctx* ctx = nullptr;
 	real maximalEigenvalue = 0, tau = 0;
+	std::vector<Task::BorderCondition> conditions;
+	bool hasBorderPlan = false;
+	void setBorderValues(real time);
 };
 
 /// GPU-free set-up of the simplex path: mesh, the time step and the static plans
@@ -152,6 +178,7 @@ struct HostPlans {
 	GcmMatrices<3> matrices;
 	GradientPlan gradient;
 	StagePlan stages[3];
+	BorderPlan border;
 	std::vector<real> pde;  // initial layer, 9 per vertex
 	std::vector<int> borderIdx, innerIdx;
 };

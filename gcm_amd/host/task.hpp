@@ -49,6 +49,10 @@ struct Snapshotters {
 struct Odes {
 	enum class T { MAXWELL_VISCOSITY, CONTINUAL_DAMAGE, IDEAL_PLASTIC_FLOW };
 };
+/// util/Enum.hpp: BorderConditions::T (simplex border correctors)
+struct BorderConditions {
+	enum class T { FIXED_FORCE, FIXED_VELOCITY };
+};
 struct Grids {
 	enum class T { CUBIC, SIMPLEX };
 };
@@ -232,6 +236,17 @@ struct Task {
 		Values values;
 	};
 	std::map<size_t, std::vector<CubicBorderCondition>> cubicBorderConditions;
+
+	/// Task::BorderCondition (Task.hpp:204-213): simplex border correctors.
+	/// `values` are the OUTER_NUMBER = 3 components of b(t) in the border's
+	/// local basis (util/task/BorderCondition.hpp).
+	struct BorderCondition {
+		std::shared_ptr<Area> area;
+		bool useForMulticontactNodes = true;
+		BorderConditions::T type = BorderConditions::T::FIXED_FORCE;
+		std::vector<TimeDependency> values;
+	};
+	std::vector<BorderCondition> borderConditions;
 
 	/// The reference's Task::calculationBasis (Task.hpp:129): 9 numbers, column i =
 	/// direction of stage i.  Required (constant) on the simplex path here.

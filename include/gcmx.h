@@ -209,7 +209,33 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* ctx, int stage, const gsx_foot* feet, in
                                const int* border_nodes, int n_inner, const int* inner_nodes);
 gcmx_status gsx_upload(gsx_ctx* ctx, const double* aos /* [n][9] */);
 gcmx_status gsx_download(gsx_ctx* ctx, double* aos);
+/* Border correctors (engine/simplex/BorderCorrector.hpp:82-276, BorderCalcMode
+ * GLOBAL_BASIS; replaces Engine::createMeshes' Border list, Engine.cpp:76-84, and
+ * addBorderNode, :292-309).  Condition c has type[c] (gsx_border_type) and
+ * min_det[c][s] = 1e-3 * getMaximalPossibleDeterminant at stage s
+ * (BorderCorrector.hpp:131-133, 198-214).  Corrected node i is `nodes[i]` under
+ * condition cond[i], with the border matrix B[i] (3 x 9, row-major,
+ * ElasticModel::borderMatrixFixedForce / FixedVelocity of its normal,
+ * ElasticModel.hpp:111-154), the local basis S[i] (3 x 3 row-major,
+ * linal::createLocalBasis of the normal) and, per stage s, outer[s * n + i]:
+ * the node's wave indices after contactAndBorderStage -- 0 none, 1 RIGHT
+ * {1,3,5}, 2 LEFT {0,2,4}, 3 both (GridCharacteristicMethodInRiemannInvariants.hpp:71-88). */
+typedef enum gsx_border_type { GSX_FIXED_FORCE = 0, GSX_FIXED_VELOCITY = 1 } gsx_border_type;
+#define GSX_MAX_BORDER_CONDITIONS 16
+gcmx_status gsx_set_border_plan(gsx_ctx* ctx, int n_cond, const int* type,
+                                const double* min_det /* [n_cond][3] */, int n_nodes,
+                                const int* nodes, const int* cond,
+                                const double* B /* [n][27] */, const double* S /* [n][9] */,
+                                const signed char* outer /* [3][n] */);
+/* b(t) of every condition (BorderCondition::b, util/task/BorderCondition.hpp:33-40),
+ * [n_cond][3]; used by the following gsx_plain_correction / gsx_stage calls. */
+gcmx_status gsx_set_border_values(gsx_ctx* ctx, const double* b);
+/* applyPlainCorrection on the current layer (BorderCorrector.hpp:177-187 ->
+ * ElasticModel::applyPlainBorderCorrection, ElasticModel.hpp:202-228); the engine
+ * calls it at construction and at the start of every step (Engine.cpp:44,99). */
+gcmx_status gsx_plain_correction(gsx_ctx* ctx);
 /* One stage: beforeStage (invariants + gradients), contactAndBorderStage,
+ * the border correctors (applyInGlobalBasis, when a border plan is set),
  * innerStage, afterStage (U1) and the PRODUCT swap (engine/simplex/Engine.cpp:117-148). */
 gcmx_status gsx_stage(gsx_ctx* ctx, int stage);
 gcmx_status gsx_sync(gsx_ctx* ctx);

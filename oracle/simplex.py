@@ -5,8 +5,9 @@ TEST INFRASTRUCTURE ONLY (see oracle/oracle.py for the rules: only tests/,
 
 A plain-Python restatement of the reference's simplex stage in Riemann
 invariants for one isotropic-elastic body with a constant calculation basis,
-GLOBAL_BASIS border mode, PRODUCT splitting and border nodes without border
-conditions (non-reflecting):
+GLOBAL_BASIS border mode, PRODUCT splitting and the border correctors of
+Task::borderConditions (FIXED_FORCE / FIXED_VELOCITY; border nodes no condition
+covers keep zero outer invariants):
 
 * triangulation queries over a given tetrahedral mesh (the mesh is INPUT: CGAL,
   the reference's mesher, is absent; tests take the product's boxMesh output as
@@ -19,7 +20,13 @@ conditions (non-reflecting):
   TetrahedronInterpolator::hybridInterpolate / interpolateInOwner
   (util/math/interpolation/TetrahedronInterpolator.hpp:93-155) and
   interpolateInSpaceTime (engine/simplex/common.hpp:102-129);
-* simplex::Engine::nextTimeStep / gcmStage (engine/simplex/Engine.cpp:82-123).
+* BorderCorrectorInRiemannInvariants / BorderCorrectorInPdeVectors
+  (engine/simplex/BorderCorrector.hpp:82-276), calculateOuterWaveCorrection
+  (common.hpp:153-202), ElasticModel::borderMatrixFixedForce / FixedVelocity /
+  applyPlainBorderCorrection (rheology/models/ElasticModel.hpp:111-228), border
+  node selection (Engine::addBorderNode, Engine.cpp:292-309) with
+  SimplexGrid::normal (grid/simplex/SimplexGrid.hpp:426-444);
+* simplex::Engine::nextTimeStep / gcmStage (engine/simplex/Engine.cpp:95-135).
 
 Every expression keeps the reference's operation order on Python floats (IEEE
 double), so results are bit-for-bit comparable.  Parity against the reference
@@ -203,6 +210,110 @@ def _line_flat(f1, f2, f3, l1, l2):  # geometry.hpp:201-217
     return _add(l1, _mul(tau, params[0]))
 
 
+def _neg(a):
+    return (-a[0], -a[1], -a[2])
+
+
+def _normalize(a):  # linal/functions.hpp:375-379
+    l = _length(a)
+    return (a[0] / l, a[1] / l, a[2] / l)
+
+
+def _opposite_face_normal(opposite, a, b, c):  # geometry.hpp:423-428
+    ans = _normalize(_cross(_sub(a, b), _sub(c, b)))
+    return ans if _dot(ans, _sub(a, opposite)) > 0 else _neg(ans)
+
+
+def local_basis(n):  # linal/basis.hpp:59-65, perpendicularClockwise geometry.hpp:46-52
+    """Rows of the 3x3 matrix with columns (tau1, tau2, n)."""
+    ans = (n[1], -n[0], 0.0)
+    if n[0] == 0 and n[1] == 0:
+        ans = (n[2], 0.0, 0.0)
+    lv, la = _length(n), _length(ans)
+    t1 = tuple((x * lv) / la for x in ans)
+    t2 = _cross(n, t1)
+    return [[t1[r], t2[r], n[r]] for r in range(3)]
+
+
+def _sym(i, j):  # linal/Symmetry.hpp:38-46 + VelocitySigmaVariables.hpp:82-96
+    a, b = min(i, j), max(i, j)
+    return 3 + a * 3 - ((a - 1) * a) // 2 + b - a
+
+
+def border_matrix(kind, normal):  # ElasticModel.hpp:111-154, 3 x 9
+    S = local_basis(normal)
+    B = [[0.0] * 9 for _ in range(3)]
+    if kind == "FIXED_FORCE":
+        for k in range(3):
+            G = [0.0] * 6          # SymmetricMatrix::Zeros; (i, j) and (j, i) share a slot
+            for i in range(3):
+                for j in range(3):
+                    q = _sym(i, j) - 3
+                    G[q] = G[q] + S[i][k] * normal[j]
+            for q in range(6):
+                B[k][3 + q] = G[q]  # setSigma
+    elif kind == "FIXED_VELOCITY":
+        for i in range(3):
+            for j in range(3):
+                B[i][j] = S[j][i]   # setVelocity(S.getColumn(i))
+    else:
+        raise ValueError("Unknown type of border condition")
+    return B
+
+
+def _mat_mul(A, B):  # linal/operators.hpp:98-123
+    n, m, k = len(A), len(B), len(B[0])
+    out = []
+    for i in range(n):
+        row = []
+        for j in range(k):
+            x = A[i][0] * B[0][j]
+            for t in range(1, m):
+                x += A[i][t] * B[t][j]
+            row.append(x)
+        out.append(row)
+    return out
+
+
+def _det33(M):
+    return _det3(M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1], M[2][2])
+
+
+def outer_wave_correction(u, Omega, B, b, min_valid):  # common.hpp:186-202
+    """(determinant fabs, successful, value) -- Omega: 9 x 3, B: 3 x 9."""
+    M = _mat_mul(B, Omega)
+    det = abs(_det33(M))
+    if not det > min_valid:
+        return det, False, [0.0] * 9
+    Bu = _mat_mul(B, [[x] for x in u])
+    rhs = [b[i] - Bu[i][0] for i in range(3)]
+    alpha = _solve3(M, rhs)
+    value = _mat_mul(Omega, [[a] for a in alpha])
+    return det, True, [v[0] for v in value]
+
+
+def plain_border_correction(u, kind, normal, value):  # ElasticModel.hpp:202-228
+    u = list(u)
+    S = local_basis(normal)
+    if kind == "FIXED_FORCE":
+        sg = [[u[_sym(i, j)] for j in range(3)] for i in range(3)]   # getSigmaFrom
+        ST = [[S[j][i] for j in range(3)] for i in range(3)]
+        sl = _mat_mul(_mat_mul(ST, sg), S)
+        for i in range(3):
+            sl[i][2] = value[i]     # setColumn(D - 1)
+        for j in range(3):
+            sl[2][j] = value[j]     # setRow(D - 1)
+        sg = _mat_mul(_mat_mul(S, sl), ST)
+        for i in range(3):
+            for j in range(3):
+                u[_sym(i, j)] = sg[i][j]   # setSigmaTo: row-major, the later write wins
+    else:
+        v = _mat_mul(S, [[x] for x in value])
+        for i in range(3):
+            u[i] = v[i][0]
+    return u
+
+
 # --------------------------------------------------------------- grid --
 
 class Grid:
@@ -236,6 +347,22 @@ class Grid:
         self.inner_idx = [i for i in range(nv) if self.inner[i]]
         self.border_idx = [i for i in range(nv) if not self.inner[i]]
         self.average_height = self._average_height()
+
+    def border_normal(self, it):  # SimplexGrid.hpp:151-154, 426-444; Cgal3DTriangulation.hpp:109-118
+        normals = []
+        for ci in self.inc[it]:
+            c = self.cells[ci]
+            for i in range(4):
+                if self.nb[ci][i] < 0 and c[i] != it:
+                    normals.append(_opposite_face_normal(
+                        self.P[c[i]], self.P[c[(i + 1) % 4]], self.P[c[(i + 2) % 4]],
+                        self.P[c[(i + 3) % 4]]))
+        if not normals:
+            return (0.0, 0.0, 0.0)
+        acc = (0.0, 0.0, 0.0)
+        for n in normals:
+            acc = _add(acc, n)
+        return _normalize(acc)
 
     def _average_height(self):  # SimplexGrid.cpp:266-285 + util/math/Histogram.hpp
         hs = [min_height4(*[self.P[x] for x in c]) for c in self.cells]
@@ -448,8 +575,11 @@ class Engine:
              (0, 2, 3, 4), (0, 2, 3, 5), (0, 2, 4, 5), (0, 3, 4, 5), (1, 2, 3, 4), (1, 2, 3, 5),
              (1, 2, 4, 5), (1, 3, 4, 5), (2, 3, 4, 5)]
 
-    def __init__(self, coords, cells, U, U1, L, basis, courant, pde0):
-        """U, U1: [3][9][9]; L: [3][9]; basis: 3x3 (column s = stage s); pde0 [n][9]."""
+    def __init__(self, coords, cells, U, U1, L, basis, courant, pde0, border_conditions=()):
+        """U, U1: [3][9][9]; L: [3][9]; basis: 3x3 (column s = stage s); pde0 [n][9];
+        border_conditions: Task::borderConditions as dicts {"contains": point -> bool,
+        "type": "FIXED_FORCE" | "FIXED_VELOCITY", "values": [3 functions of t],
+        "multi": useForMulticontactNodes}."""
         self.grid = Grid(coords, cells)
         self.U = [[[float(x) for x in row] for row in U[s]] for s in range(3)]
         self.U1 = [[[float(x) for x in row] for row in U1[s]] for s in range(3)]
@@ -461,7 +591,75 @@ class Engine:
                 mx = max(mx, abs(self.L[s][k]))
         self.tau = courant * self.grid.average_height / mx  # Engine.hpp:78-92
         self.u = [[float(x) for x in row] for row in pde0]
+        self.outers = [{} for _ in range(3)]
         self.feet = [self._plan(s) for s in range(3)]
+        self.time = 0.0
+        self.conditions = list(border_conditions)
+        self._border_setup()
+        self._plain_correction(self.time)     # Engine.cpp:44
+
+    def _border_setup(self):
+        """Engine::createMeshes' Border list + addBorderNode (Engine.cpp:76-84, 292-309)."""
+        g = self.grid
+        self.corrected = []                   # (node, condition, normal)
+        for it in g.border_idx:
+            n = g.border_normal(it)
+            multi = n == (0.0, 0.0, 0.0)
+            chosen = None
+            for ci, c in enumerate(self.conditions):
+                if c["contains"](g.P[it]) and (not multi or c.get("multi", True)):
+                    chosen = ci
+            if chosen is None:
+                continue
+            if multi:
+                raise ValueError("zero common normal at a border node")
+            self.corrected.append((it, chosen, n))
+        self.min_det = {}
+        for ci, c in enumerate(self.conditions):   # getMaximalPossibleDeterminant (hpp:198-214)
+            if not any(x[1] == ci for x in self.corrected):
+                continue
+            for s in range(3):
+                direction = (self.basis[0][s], self.basis[1][s], self.basis[2][s])
+                det, ok, _ = outer_wave_correction([0.0] * 9, self._omega(s, RIGHT),
+                                                   border_matrix(c["type"], direction), [0.0] * 3, 0)
+                if not (ok and det > 0):
+                    raise ValueError("degenerate outer-wave system")
+                self.min_det[(ci, s)] = 1e-3 * det
+
+    def _omega(self, s, cols):  # getColumnsFromGcmMatrices (common.hpp:153-165)
+        return [[self.U1[s][i][c] for c in cols] for i in range(9)]
+
+    def _b(self, ci, t):
+        return [float(f(t)) for f in self.conditions[ci]["values"]]
+
+    def _plain_correction(self, t):  # applyPlainBorderContactCorrection (Engine.cpp:193-211)
+        for it, ci, n in self.corrected:
+            self.u[it] = plain_border_correction(self.u[it], self.conditions[ci]["type"], n,
+                                                 self._b(ci, t))
+
+    def _correct(self, s, wn, t):
+        """BorderCorrectorInRiemannInvariants::applyInGlobalBasis (hpp:256-265)."""
+        for it, ci, n in self.corrected:
+            kind = self.conditions[ci]["type"]
+            b = self._b(ci, t)
+            min_valid = self.min_det[(ci, s)]
+            B = border_matrix(kind, n)
+            u = self._mat_vec(self.U1[s], wn[it])
+            outers = self.outers[s].get(it, [])
+            if outers == RIGHT or outers == LEFT:
+                _, ok, v = outer_wave_correction(u, self._omega(s, outers), B, b, min_valid)
+                if ok:
+                    u = [u[i] + v[i] for i in range(9)]
+                else:
+                    u = plain_border_correction(u, kind, n, b)
+            else:
+                _, okr, vr = outer_wave_correction(u, self._omega(s, RIGHT), B, b, min_valid)
+                _, okl, vl = outer_wave_correction(u, self._omega(s, LEFT), B, b, min_valid)
+                if okr and okl:
+                    u = [u[i] + (vr[i] + vl[i]) / 2 for i in range(9)]
+                else:
+                    u = plain_border_correction(u, kind, n, b)
+            wn[it] = self._mat_vec(self.U[s], u)
 
     def _plan(self, s):
         """Per node and invariant 0..5: ('cell', verts, q) | ('outer',) | ('st', face, shift)
@@ -496,6 +694,8 @@ class Engine:
                     outer = sorted(set(outer) | set(LEFT))
                 for k in outer:
                     row[k] = ("outer",)
+            if not g.inner[it]:
+                self.outers[s][it] = list(outer)
             plan.append(row)
         return plan
 
@@ -548,14 +748,16 @@ class Engine:
             out.append(s)
         return out
 
-    def stage(self, s):
-        """gcmStage with PRODUCT splitting (engine/simplex/Engine.cpp:104-123)."""
+    def stage(self, s, t_next=None):
+        """gcmStage with PRODUCT splitting (engine/simplex/Engine.cpp:119-135)."""
         g = self.grid
         n = len(g.P)
         w = [self._mat_vec(self.U[s], self.u[i]) for i in range(n)]     # beforeStage
         grads = g.gradients(w)
         wn = [[0.0] * 9 for _ in range(n)]
         for order in (g.border_idx, g.inner_idx):  # contactAndBorderStage, innerStage
+            if order is g.inner_idx and self.corrected:   # correctContactsAndBorders
+                self._correct(s, wn, self.time + self.tau if t_next is None else t_next)
             for it in order:
                 for k in range(9):
                     if k >= 6:
@@ -565,5 +767,9 @@ class Engine:
         self.u = [self._mat_vec(self.U1[s], wn[i]) for i in range(n)]   # afterStage + swap
 
     def step(self):
+        """simplex::Engine::nextTimeStep (Engine.cpp:95-116) + the Clock tick."""
+        t_next = self.time + self.tau
+        self._plain_correction(t_next)
         for s in range(3):
-            self.stage(s)
+            self.stage(s, t_next)
+        self.time = self.time + self.tau

@@ -5,7 +5,9 @@ from oracle import oracle as O
 from oracle import simplex as S
 
 
-def host_task(n=4, courant=1.0, jitter=0.1, seed=7, snaps=3, pressure=1.0, vector=None):
+def host_task(n=4, courant=1.0, jitter=0.1, seed=7, snaps=3, pressure=1.0, vector=None, border=()):
+    """border: Task::borderConditions as (area tuple, "FIXED_FORCE" | "FIXED_VELOCITY",
+    [3 functions of t], useForMulticontactNodes)."""
     from gcm_amd import _gcm_host as H
     t = H.Task()
     t.dimensionality = 3
@@ -20,10 +22,33 @@ def host_task(n=4, courant=1.0, jitter=0.1, seed=7, snaps=3, pressure=1.0, vecto
         t.add_initial_quantity(("sphere", 0.3, (0.5, 0.5, 0.5)), "PRESSURE", pressure)
     if vector is not None:
         t.add_initial_vector(("infinite",), list(vector))
+    for area, kind, values, multi in border:
+        t.add_simplex_border_condition(area, kind, list(values), multi)
     return t
 
 
-def oracle_engine(plans, courant):
+def _contains(area):
+    def f(p):
+        return bool(O.area_contains(area, np.array([p[0]]), np.array([p[1]]), np.array([p[2]]))[0])
+    return f
+
+
+def oracle_conditions(border):
+    return [{"contains": _contains(a), "type": k, "values": list(v), "multi": m}
+            for a, k, v, m in border]
+
+
+def oracle_engine(plans, courant, border=()):
     """The oracle engine on the product's mesh (input data) with its own matrices."""
     U, U1, L = O.isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
-    return S.Engine(plans["coords"], plans["cells"], U, U1, L, np.eye(3), courant, plans["pde"])
+    return S.Engine(plans["coords"], plans["cells"], U, U1, L, np.eye(3), courant, plans["pde"],
+                    oracle_conditions(border))
+
+
+ZERO = (lambda t: 0.0,) * 3
+FREE_BORDER = [(("infinite",), "FIXED_FORCE", ZERO, True)]   # main.cpp:209-220 (cube task)
+# a time-dependent velocity on the x = 0 face, free surface elsewhere (the last
+# containing condition wins, Engine.cpp:298-303)
+MIXED_BORDER = [(("infinite",), "FIXED_FORCE", ZERO, True),
+                (("box", (-1.0, 0.2, 0.2), (0.05, 0.8, 0.8)), "FIXED_VELOCITY",
+                 (lambda t: 0.1 * t, lambda t: 0.0, lambda t: -0.05), True)]

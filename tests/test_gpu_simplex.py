@@ -41,3 +41,29 @@ def test_simplex_zero_state_stays_zero(H):
     e.run()
     assert e.steps == 3
     assert not np.any(e.pde())
+
+
+from tests.simplex_spec import FREE_BORDER, MIXED_BORDER  # noqa: E402
+
+
+@pytest.mark.parametrize("border,n,courant,steps", [(FREE_BORDER, 4, 1.0, 3), (MIXED_BORDER, 4, 1.3, 3),
+                                                    (FREE_BORDER, 5, 2.0, 2)],
+                         ids=["free-c1", "mixed-c1.3", "free-c2"])
+def test_simplex_border_correctors_match_oracle(H, border, n, courant, steps):
+    """BorderCorrectorInRiemannInvariants (GLOBAL_BASIS) + the plain correction at
+    the start of every step: GPU == oracle bitwise (the cube task's free surface,
+    main.cpp:209-220, and a time-dependent FIXED_VELOCITY patch)."""
+    t = host_task(n, courant, 0.1, 7, border=border)
+    p = H.simplex_plans(t)
+    e = H.SimplexEngine(t)
+    o = oracle_engine(p, courant, border)
+    assert len(o.corrected) == len(p["border_plan"]["nodes"]) > 0
+    e.run_steps(steps)
+    for _ in range(steps):
+        o.step()
+    got, want = e.pde(), np.array(o.u)
+    assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"
+    # the corrector changed the border values relative to no correction
+    e0 = H.SimplexEngine(host_task(n, courant, 0.1, 7))
+    e0.run_steps(steps)
+    assert not np.array_equal(e0.pde()[p["border"]], got[p["border"]])

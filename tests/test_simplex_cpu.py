@@ -93,3 +93,83 @@ def test_oracle_uniform_field_is_preserved_inside():
     for it in e.grid.inner_idx:
         for k in range(9):
             assert math.isclose(e.u[it][k], p["pde"][it][k], rel_tol=1e-12, abs_tol=1e-12)
+
+
+# ------------------------------------------------------------ border correctors --
+
+from tests.simplex_spec import FREE_BORDER, MIXED_BORDER  # noqa: E402
+
+CODE = {(1, 3, 5): 1, (0, 2, 4): 2}
+
+
+@pytest.mark.parametrize("border", [FREE_BORDER, MIXED_BORDER], ids=["free", "mixed"])
+@pytest.mark.parametrize("n,courant,jitter,seed", [(4, 1.0, 0.1, 7), (5, 1.7, 0.15, 3)])
+def test_border_plan_matches_oracle(H, border, n, courant, jitter, seed):
+    """Engine::addBorderNode's choice of nodes / conditions / normals, the border
+    matrices, local bases, thresholds and wave indices: host == oracle exactly."""
+    p = H.simplex_plans(host_task(n, courant, jitter, seed, border=border))
+    e = oracle_engine(p, courant, border)
+    b = p["border_plan"]
+    assert list(b["nodes"]) == [x[0] for x in e.corrected]
+    assert list(b["cond"]) == [x[1] for x in e.corrected]
+    kinds = [c[1] for c in border]
+    assert list(b["type"]) == [0 if k == "FIXED_FORCE" else 1 for k in kinds]
+    nn = len(e.corrected)
+    for i, (it, ci, nrm) in enumerate(e.corrected):
+        assert tuple(b["normal"][3 * i:3 * i + 3]) == nrm
+        B = S.border_matrix(kinds[ci], nrm)
+        assert list(b["B"][27 * i:27 * i + 27]) == [x for row in B for x in row]
+        Sb = S.local_basis(nrm)
+        assert list(b["S"][9 * i:9 * i + 9]) == [x for row in Sb for x in row]
+        for s in range(3):
+            outers = tuple(e.outers[s].get(it, []))
+            want = CODE.get(outers, 0 if not outers else 3)
+            assert b["outer"][s * nn + i] == want
+    for (ci, s), v in e.min_det.items():
+        assert b["min_det"][3 * ci + s] == v
+    if border is MIXED_BORDER:
+        assert 0 < sum(b["cond"]) < nn   # both conditions own nodes
+
+
+def test_outer_wave_correction_satisfies_the_condition():
+    """calculateOuterWaveCorrection's purpose (common.hpp:170-185): after adding
+    Omega * alpha the border condition B u = b holds (to rounding)."""
+    U, U1, _ = O.isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
+    rng = np.random.default_rng(5)
+    for kind in ("FIXED_FORCE", "FIXED_VELOCITY"):
+        for _ in range(20):
+            nrm = S._normalize(tuple(rng.normal(size=3)))
+            u = list(rng.uniform(-1, 1, 9))
+            b = list(rng.uniform(-1, 1, 3))
+            B = S.border_matrix(kind, nrm)
+            omega = [[U1[0][i][c] for c in S.RIGHT] for i in range(9)]
+            det, ok, v = S.outer_wave_correction(u, omega, B, b, 0.0)
+            assert ok and det > 0
+            uc = [u[i] + v[i] for i in range(9)]
+            Bu = [sum(B[r][k] * uc[k] for k in range(9)) for r in range(3)]
+            assert np.allclose(Bu, b, atol=1e-12)
+
+
+def test_plain_correction_sets_local_traction_and_velocity():
+    """applyPlainBorderCorrection (ElasticModel.hpp:202-228): sigma in the local
+    basis has the given last row / column; velocity = S * value."""
+    rng = np.random.default_rng(9)
+    nrm = S._normalize(tuple(rng.normal(size=3)))
+    Sb = np.array(S.local_basis(nrm))
+    u = list(rng.uniform(-1, 1, 9))
+    val = [0.3, -0.2, 0.7]
+    uf = S.plain_border_correction(u, "FIXED_FORCE", nrm, val)
+    sig = np.array([[uf[S._sym(i, j)] for j in range(3)] for i in range(3)])
+    loc = Sb.T @ sig @ Sb
+    assert np.allclose(loc[:, 2], val, atol=1e-12) and np.allclose(loc[2, :], val, atol=1e-12)
+    assert uf[:3] == u[:3]
+    uv = S.plain_border_correction(u, "FIXED_VELOCITY", nrm, val)
+    assert np.allclose(uv[:3], Sb @ np.array(val), atol=1e-15) and uv[3:] == u[3:]
+
+
+def test_border_condition_validation(H):
+    t = host_task(3, border=[(("infinite",), "FIXED_FORCE", (lambda t: 0.0,) * 2, True)])
+    with pytest.raises(Exception, match="OUTER_NUMBER"):
+        H.simplex_plans(t)
+    with pytest.raises(Exception, match="unknown border condition type"):
+        host_task(3, border=[(("infinite",), "FIXED_STRAIN", (lambda t: 0.0,) * 3, True)])
