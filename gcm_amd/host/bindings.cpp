@@ -334,7 +334,24 @@ PYBIND11_MODULE(_gcm_host, m) {
 		         t.borderConditions.push_back(bc);
 	         },
 	         py::arg("area"), py::arg("type"), py::arg("values"),
-	         py::arg("use_for_multicontact_nodes") = true);
+	         py::arg("use_for_multicontact_nodes") = true)
+	    .def("set_simplex_domain",
+	         [](Task& t, std::vector<std::array<real, 3>> points, std::vector<std::array<int, 3>> faces) {
+		         t.simplexGrid.offPoints.assign(points.begin(), points.end());
+		         t.simplexGrid.offFaces = std::move(faces);
+	         },
+	         py::arg("points"), py::arg("faces"),
+	         "Domain surface (closed triangles): cells whose centroid is outside are empty space")
+	    .def("set_simplex_domain_off",
+	         [](Task& t, const std::string& fileName) {
+		         simplex::readOff(fileName, t.simplexGrid.offPoints, t.simplexGrid.offFaces);
+	         },
+	         py::arg("file_name"))
+	    .def("add_simplex_body_area",
+	         [](Task& t, py::tuple area, size_t id) {
+		         t.simplexGrid.bodyAreas.push_back({makeArea(area), id});
+	         },
+	         py::arg("area"), py::arg("body"));
 
 	m.def(
 	    "host_state",

@@ -5,7 +5,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <fstream>
 #include <map>
+#include <sstream>
 #include <memory>
 #include <set>
 
@@ -253,16 +255,156 @@ TetMesh boxMesh(const std::array<int, 3>& n, const Real3& lo, const Real3& hi, r
 	return m;
 }
 
+// --------------------------------------------------------- triangulation --
+
+bool offContains(const std::vector<Real3>& points, const std::vector<std::array<int, 3>>& faces,
+                 const Real3& p) {
+	// generalized winding number: sum of the triangles' solid angles / 4 pi
+	// (Van Oosterom & Strackee); a point inside k nested closed surfaces gets |k|
+	real w = 0;
+	for (const auto& f : faces) {
+		const Real3 a = sub(points[(size_t)f[0]], p), b = sub(points[(size_t)f[1]], p),
+		            c = sub(points[(size_t)f[2]], p);
+		const real la = length(a), lb = length(b), lc = length(c);
+		const real num = dot(a, cross(b, c));
+		const real den = la * lb * lc + dot(a, b) * lc + dot(a, c) * lb + dot(b, c) * la;
+		w += 2 * std::atan2(num, den);
+	}
+	const long k = std::lround(std::fabs(w) / (4 * M_PI));
+	return (k % 2) == 1;
+}
+
+void readOff(const std::string& fileName, std::vector<Real3>& points,
+             std::vector<std::array<int, 3>>& faces) {
+	std::ifstream in(fileName);
+	if (!in) throw Exception("cannot open " + fileName);
+	std::vector<std::string> tokens;
+	std::string line;
+	while (std::getline(in, line)) {  // '#' starts a comment (meshes/layers_with_fracture.off)
+		const size_t h = line.find('#');
+		if (h != std::string::npos) line.resize(h);
+		std::istringstream ls(line);
+		std::string t;
+		while (ls >> t) tokens.push_back(t);
+	}
+	size_t i = 0;
+	auto next = [&]() -> const std::string& {
+		if (i >= tokens.size()) throw Exception("truncated .off file " + fileName);
+		return tokens[i++];
+	};
+	if (next() != "OFF") throw Exception(fileName + " is not an OFF file");
+	const long nv = std::stol(next()), nf = std::stol(next());
+	next();  // number of edges
+	if (nv < 4 || nf < 4) throw Exception("degenerate .off surface");
+	points.assign((size_t)nv, Real3{});
+	for (long v = 0; v < nv; v++)
+		for (int c = 0; c < 3; c++) points[(size_t)v][c] = std::stod(next());
+	faces.clear();
+	for (long f = 0; f < nf; f++) {
+		if (std::stol(next()) != 3) throw Exception("only triangles are supported in .off");
+		std::array<int, 3> t;
+		for (int c = 0; c < 3; c++) {
+			t[c] = std::stoi(next());
+			if (t[c] < 0 || t[c] >= nv) throw Exception("bad .off vertex index");
+		}
+		faces.push_back(t);
+	}
+}
+
+Triangulation buildTriangulation(const Task& task) {
+	const auto& sg = task.simplexGrid;
+	if (task.bodies.empty()) throw Exception("the simplex task has no bodies");
+	Triangulation tr;
+	tr.all = boxMesh(sg.cells, sg.lo, sg.hi, sg.jitter, sg.seed);
+	const int firstBody = (int)task.bodies.begin()->first;
+	tr.gridId.assign(tr.all.cells.size(), firstBody);
+	for (size_t c = 0; c < tr.all.cells.size(); c++) {
+		const auto& t = tr.all.cells[c];
+		Real3 ctr = add(add(add(tr.all.v[(size_t)t[0]], tr.all.v[(size_t)t[1]]), tr.all.v[(size_t)t[2]]),
+		                tr.all.v[(size_t)t[3]]);
+		ctr = mul(ctr, 0.25);
+		if (!sg.offFaces.empty() && !offContains(sg.offPoints, sg.offFaces, ctr)) {
+			tr.gridId[c] = EMPTY_SPACE;
+			continue;
+		}
+		for (const auto& rule : sg.bodyAreas) {
+			if (!task.bodies.count(rule.second)) throw Exception("body area names an unknown body");
+			if (rule.first->contains(ctr)) tr.gridId[c] = (int)rule.second;
+		}
+	}
+	return tr;
+}
+
+TetMesh bodyMesh(const Triangulation& tr, int id) {
+	const TetMesh& all = tr.all;
+	const int nvAll = all.nVertices();
+	// vertices on the box surface touch the (infinite) empty space
+	std::vector<char> onHull((size_t)nvAll, 0);
+	for (size_t c = 0; c < all.cells.size(); c++)
+		for (int i = 0; i < 4; i++)
+			if (all.nb[c][i] < 0)
+				for (int k = 1; k < 4; k++) onHull[(size_t)all.cells[c][(i + k) % 4]] = 1;
+	std::vector<int> cellsOf;
+	std::vector<int> local((size_t)nvAll, -1);
+	for (size_t c = 0; c < all.cells.size(); c++)
+		if (tr.gridId[c] == id) {
+			cellsOf.push_back((int)c);
+			for (int x : all.cells[c]) local[(size_t)x] = 0;
+		}
+	if (cellsOf.empty()) throw Exception("a body without cells");
+	TetMesh m;
+	for (int g = 0; g < nvAll; g++)
+		if (local[(size_t)g] == 0) {
+			local[(size_t)g] = (int)m.v.size();
+			m.v.push_back(all.v[(size_t)g]);
+			m.global.push_back(g);
+		}
+	for (int c : cellsOf) {
+		std::array<int, 4> t;
+		for (int i = 0; i < 4; i++) t[i] = local[(size_t)all.cells[(size_t)c][i]];
+		m.cells.push_back(t);
+	}
+	m.buildTopology();
+	m.nbGrid.assign(m.cells.size(), {id, id, id, id});
+	for (size_t lc = 0; lc < cellsOf.size(); lc++)
+		for (int i = 0; i < 4; i++)
+			if (m.nb[lc][i] < 0) {
+				const int gn = all.nb[(size_t)cellsOf[lc]][i];
+				m.nbGrid[lc][i] = gn < 0 ? EMPTY_SPACE : tr.gridId[(size_t)gn];
+				if (m.nbGrid[lc][i] == id) throw Exception("bodyMesh: lost a face neighbour");
+			}
+	m.otherGrids.assign(m.v.size(), {});
+	for (int lv = 0; lv < m.nVertices(); lv++) {
+		const int g = m.global[(size_t)lv];
+		std::set<int> s;
+		if (onHull[(size_t)g]) s.insert(EMPTY_SPACE);
+		for (int p = all.incOff[(size_t)g]; p < all.incOff[(size_t)g + 1]; p++) {
+			const int gid = tr.gridId[(size_t)all.incCells[(size_t)p]];
+			if (gid != id) s.insert(gid);
+		}
+		m.otherGrids[(size_t)lv].assign(s.begin(), s.end());
+	}
+	return m;
+}
+
 // ------------------------------------------------------------------- grid --
 
 Grid::Grid(const TetMesh& m) : mesh(m) {
 	const int nv = m.nVertices();
+	if (m.otherGrids.size() != (size_t)nv || m.nbGrid.size() != m.cells.size())
+		throw Exception("Grid: the mesh was not cut out of a triangulation (bodyMesh)");
 	inner.assign(nv, 1);
-	for (size_t c = 0; c < m.cells.size(); c++)
-		for (int i = 0; i < 4; i++)
-			if (m.nb[c][i] < 0)
-				for (int k = 1; k < 4; k++) inner[m.cells[c][(i + k) % 4]] = 0;
-	for (int it = 0; it < nv; it++) (inner[it] ? innerIdx : borderIdx).push_back(it);
+	// borderState (SimplexGrid.hpp:388-395) + markInnersAndBorders (SimplexGrid.cpp:216-252)
+	for (int it = 0; it < nv; it++) {
+		const auto& o = m.otherGrids[(size_t)it];
+		if (o.empty()) {
+			innerIdx.push_back(it);
+			continue;
+		}
+		inner[it] = 0;
+		if (o.size() == 1 && o[0] != EMPTY_SPACE) contactIdx.push_back(it);
+		else borderIdx.push_back(it);  // BORDER or MULTICONTACT
+	}
 	// collectCellHeightsStatistics (SimplexGrid.cpp:266-285): Histogram of 100 bins
 	std::vector<real> hs;
 	for (const auto& t : m.cells) hs.push_back(minimalHeight4(P(t[0]), P(t[1]), P(t[2]), P(t[3])));
@@ -290,13 +432,15 @@ Grid::Grid(const TetMesh& m) : mesh(m) {
 	minimalHeight = mn;
 }
 
-Real3 Grid::borderNormal(int it) const {
+template <typename Pred>
+Real3 Grid::normal(int it, Pred use) const {
 	Real3 sum = {0, 0, 0};
 	bool any = false;
 	for (int p = mesh.incOff[it]; p < mesh.incOff[it + 1]; p++) {
 		const int c = mesh.incCells[p];
 		for (int i = 0; i < 4; i++) {
 			if (mesh.nb[c][i] >= 0 || mesh.cells[c][i] == it) continue;  // face must contain it
+			if (!use(mesh.nbGrid[c][i])) continue;
 			const auto& t = mesh.cells[c];
 			sum = add(sum, oppositeFaceNormal(P(t[i]), P(t[(i + 1) % 4]), P(t[(i + 2) % 4]),
 			                                  P(t[(i + 3) % 4])));  // Cgal3DTriangulation.hpp:109-118
@@ -305,6 +449,15 @@ Real3 Grid::borderNormal(int it) const {
 	}
 	if (!any) return {0, 0, 0};
 	return normalize(sum);
+}
+Real3 Grid::borderNormal(int it) const {
+	return normal(it, [](int g) { return g == EMPTY_SPACE; });
+}
+Real3 Grid::contactNormal(int it, int other) const {
+	return normal(it, [other](int g) { return g == other; });
+}
+Real3 Grid::commonNormal(int it) const {
+	return normal(it, [](int) { return true; });
 }
 
 std::vector<int> Grid::neighborVertices(int it) const {
@@ -527,7 +680,9 @@ StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[
 	StagePlan plan;
 	plan.feet.assign((size_t)nv * 6, gsx_foot{});
 	plan.outerCode.assign((size_t)nv, 0);
-	plan.borderNodes = grid.borderIdx;
+	// contactAndBorderStage: contact nodes, then border nodes (hpp:90-95)
+	plan.borderNodes = grid.contactIdx;
+	plan.borderNodes.insert(plan.borderNodes.end(), grid.borderIdx.begin(), grid.borderIdx.end());
 	plan.innerNodes = grid.innerIdx;
 	static const std::vector<int> RIGHT = {1, 3, 5}, LEFT = {0, 2, 4};  // Model.cpp:81-82
 	for (int it = 0; it < nv; it++) {
@@ -676,8 +831,8 @@ BorderPlan buildBorderPlan(const Task& task, const Grid& grid, const GcmMatrices
 			    (!isMulticontact || conds[c].useForMulticontactNodes))
 				chosen = (int)c;
 		if (chosen < 0) continue;
-		const Real3 n = bn;  // commonNormal == borderNormal for one body
-		if (isMulticontact) throw Exception("zero border normal at a border-condition node");
+		const Real3 n = grid.commonNormal(it);
+		if (n[0] == 0 && n[1] == 0 && n[2] == 0) throw Exception("zero common normal at a border node");
 		bp.nodes.push_back(it);
 		bp.cond.push_back(chosen);
 		count[(size_t)chosen]++;
@@ -738,8 +893,7 @@ HostPlans buildHostPlans(const Task& task) {
 		throw Exception("simplex materials must be given BY_BODIES");
 	const auto mat = task.materialConditions.byBodies.bodyMaterialMap.at(id);
 	HostPlans p;
-	const auto& sg = task.simplexGrid;
-	p.mesh = boxMesh(sg.cells, sg.lo, sg.hi, sg.jitter, sg.seed);
+	p.mesh = bodyMesh(buildTriangulation(task), (int)id);
 	Grid grid(p.mesh);
 	real calc[3][3];
 	calcBasis(task, calc);

@@ -20,6 +20,7 @@
 
 #include <array>
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "../../include/gcmx.h"
@@ -32,17 +33,45 @@ namespace simplex {
 constexpr real EQUALITY_TOLERANCE = 1e-9;           // util/infrastructure/Types.hpp:10
 constexpr int MAX_NUMBER_OF_NEIGHBOR_VERTICES = 20;  // Cgal3DTriangulation.hpp:53
 
+/// Grid::EmptySpaceFlag (SimplexGrid.hpp): the grid id of cells outside every body.
+constexpr int EMPTY_SPACE = -1;
+
 /// Tetrahedral mesh of one body: vertex coordinates, positively oriented cells,
 /// face neighbours (nb[c][i] = cell across the face opposite vertex i, -1 =
 /// outside the body) and vertex -> incident cells (ascending cell index).
+/// A body cut out of a Triangulation also knows, for every face with nb < 0,
+/// the grid id on the other side (nbGrid: EMPTY_SPACE or another body) and, for
+/// every vertex, the other grid ids of the cells around it (otherGrids, sorted,
+/// EMPTY_SPACE for the box surface) -- SimplexGrid::gridsAroundVertex
+/// (SimplexGrid.hpp:415-423) minus the body's own id.
 struct TetMesh {
 	std::vector<Real3> v;
 	std::vector<std::array<int, 4>> cells;
 	std::vector<std::array<int, 4>> nb;
 	std::vector<int> incOff, incCells;
+	std::vector<std::array<int, 4>> nbGrid;
+	std::vector<std::vector<int>> otherGrids;
+	std::vector<int> global;  // local vertex -> vertex of the triangulation
 	void buildTopology();
 	int nVertices() const { return (int)v.size(); }
 };
+
+/// The global triangulation of the calculation space (the CgalTriangulation
+/// every SimplexGrid of the task shares, SimplexGrid.cpp:12-37): the box mesh and
+/// a grid id per cell (EMPTY_SPACE outside the domain surface).
+struct Triangulation {
+	TetMesh all;
+	std::vector<int> gridId;
+};
+
+/// Odd-parity inside test of a closed triangulated surface (the .off domain):
+/// the generalized winding number rounded to an integer, inside when odd.
+bool offContains(const std::vector<Real3>& points, const std::vector<std::array<int, 3>>& faces,
+                 const Real3& p);
+
+/// Read the vertices and triangles of an .off file (the reference meshes/*.off).
+void readOff(const std::string& fileName, std::vector<Real3>& points,
+             std::vector<std::array<int, 3>>& faces);
 
 /// Kuhn tetrahedralisation (6 tetrahedra per cube) of the box [lo, hi] with
 /// n cubes per axis.  Vertices are jittered by up to `jitter` * h with a
@@ -51,7 +80,16 @@ struct TetMesh {
 TetMesh boxMesh(const std::array<int, 3>& n, const Real3& lo, const Real3& hi, real jitter,
                 uint64_t seed);
 
-/// SimplexGrid<3> (grid/simplex/SimplexGrid.{hpp,cpp}) over a TetMesh, one body.
+/// The task's triangulation: boxMesh of Task::SimplexGrid, cells outside the
+/// .off domain marked EMPTY_SPACE, the others assigned to bodies by bodyAreas.
+Triangulation buildTriangulation(const Task& task);
+
+/// The cells of body `id` with their vertices renumbered in ascending global
+/// order (SimplexGrid's constructor collects vertexHandles into a std::set,
+/// SimplexGrid.cpp:18-30), neighbour grid ids and vertex states.
+TetMesh bodyMesh(const Triangulation& tr, int id);
+
+/// SimplexGrid<3> (grid/simplex/SimplexGrid.{hpp,cpp}) over the TetMesh of one body.
 class Grid {
 public:
 	explicit Grid(const TetMesh& mesh);
@@ -62,14 +100,21 @@ public:
 		int v[4] = {-1, -1, -1, -1};
 	};
 	bool isInner(int it) const { return inner[it]; }
-	/// borderNormal (SimplexGrid.hpp:151-154, normal():426-444)
+	/// SimplexGrid::normal (SimplexGrid.hpp:426-444) over the faces whose outer
+	/// grid id satisfies `use`: borderNormal (EMPTY_SPACE, :151-154),
+	/// contactNormal (one neighbour grid, :141-144), commonNormal (any, :157-160).
+	template <typename Pred> Real3 normal(int it, Pred use) const;
 	Real3 borderNormal(int it) const;
+	Real3 contactNormal(int it, int other) const;
+	Real3 commonNormal(int it) const;
 	/// findNeighborVertices (SimplexGrid.hpp:249-259): ascending local indices
 	std::vector<int> neighborVertices(int it) const;
 	/// findCellCrossedByTheRay (SimplexGrid.cpp:57-112)
 	Cell findCellCrossedByTheRay(int it, const Real3& shift) const;
 	real averageHeight = 0, minimalHeight = 0;  // collectCellHeightsStatistics (Histogram)
-	std::vector<int> innerIdx, borderIdx;       // markInnersAndBorders order
+	/// markInnersAndBorders (SimplexGrid.cpp:216-252): contact, border (with
+	/// multicontact) and inner nodes, each in ascending local order
+	std::vector<int> innerIdx, borderIdx, contactIdx;
 
 private:
 	std::vector<char> inner;

@@ -259,6 +259,16 @@ struct Task {
 		Real3 lo = {0, 0, 0}, hi = {1, 1, 1};
 		real jitter = 0;
 		uint64_t seed = 0;
+		/// Domain surface (the triangles of an .off file, Task.hpp:95 fileName):
+		/// cells whose centroid is outside it (odd crossing parity -> inside, so
+		/// inner closed surfaces such as layers_with_fracture.off's fracture are
+		/// cavities) belong to the empty space.  Empty = the whole box.
+		std::vector<Real3> offPoints;
+		std::vector<std::array<int, 3>> offFaces;
+		/// Cell -> body: the last rule whose area contains the cell centroid picks
+		/// the body id, the first body otherwise (per-cell grid ids, as the INM
+		/// mesher assigns them, InmMeshLoader.hpp:58-78).
+		std::vector<std::pair<std::shared_ptr<Area>, size_t>> bodyAreas;
 	} simplexGrid;
 
 	struct VtkSnapshotter {

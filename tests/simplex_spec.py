@@ -1,4 +1,6 @@
 """Shared simplex task builder for the CPU and GPU simplex tests."""
+import os
+
 import numpy as np
 
 from oracle import oracle as O
@@ -52,3 +54,27 @@ FREE_BORDER = [(("infinite",), "FIXED_FORCE", ZERO, True)]   # main.cpp:209-220 
 MIXED_BORDER = [(("infinite",), "FIXED_FORCE", ZERO, True),
                 (("box", (-1.0, 0.2, 0.2), (0.05, 0.8, 0.8)), "FIXED_VELOCITY",
                  (lambda t: 0.1 * t, lambda t: 0.0, lambda t: -0.05), True)]
+
+
+# BASELINE config 5: meshes/layers_with_fracture.off -- the 0.16 x 0.16 x 0.04
+# layer with a tetrahedral fracture (cavity) inside, free surface everywhere
+# (the reference's data file, copied as a fixture into tests/golden/).
+FRACTURE_OFF = os.path.join(os.path.dirname(__file__), "golden", "layers_with_fracture.off")
+
+
+def fracture_task(n=(16, 16, 8), courant=1.0, jitter=0.1, seed=7, border=None, snaps=3):
+    from gcm_amd import _gcm_host as H
+    t = H.Task()
+    t.dimensionality = 3
+    t.grid = "SIMPLEX"
+    t.courant = courant
+    t.number_of_snaps = snaps
+    t.add_body(0, [1, 1, 1], [0, 0, 0])
+    t.set_body_material(0, 4, 2, 1)
+    t.calculation_basis = [1, 0, 0, 0, 1, 0, 0, 0, 1]
+    t.set_simplex_box(list(n), [0, 0, 0], [0.16, 0.16, 0.04], jitter, seed)
+    t.set_simplex_domain_off(FRACTURE_OFF)
+    t.add_initial_quantity(("sphere", 0.03, (0.08, 0.08, 0.02)), "PRESSURE", 1.0)
+    for area, kind, values, multi in (FREE_BORDER if border is None else border):
+        t.add_simplex_border_condition(area, kind, list(values), multi)
+    return t

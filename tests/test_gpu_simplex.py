@@ -67,3 +67,23 @@ def test_simplex_border_correctors_match_oracle(H, border, n, courant, steps):
     e0 = H.SimplexEngine(host_task(n, courant, 0.1, 7))
     e0.run_steps(steps)
     assert not np.array_equal(e0.pde()[p["border"]], got[p["border"]])
+
+
+from tests.simplex_spec import fracture_task  # noqa: E402
+
+
+@pytest.mark.parametrize("courant,steps", [(1.0, 3), (1.7, 2)])
+def test_fracture_layer_matches_oracle(H, courant, steps):
+    """BASELINE config 5 (meshes/layers_with_fracture.off): the layer with the
+    fracture cavity, free surface on the box and on the fracture faces
+    (border correctors), GPU == oracle bitwise."""
+    t = fracture_task((16, 16, 8), courant)
+    p = H.simplex_plans(t)
+    e = H.SimplexEngine(t)
+    o = oracle_engine(p, courant, FREE_BORDER)
+    e.run_steps(steps)
+    for _ in range(steps):
+        o.step()
+    got, want = e.pde(), np.array(o.u)
+    assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"
+    assert np.abs(got).max() > 0

@@ -173,3 +173,89 @@ def test_border_condition_validation(H):
         H.simplex_plans(t)
     with pytest.raises(Exception, match="unknown border condition type"):
         host_task(3, border=[(("infinite",), "FIXED_STRAIN", (lambda t: 0.0,) * 3, True)])
+
+
+# ---- BASELINE config 5: the layer with a fracture (cavity) ---------------------
+
+from tests.simplex_spec import FRACTURE_OFF, FREE_BORDER, fracture_task  # noqa: E402
+
+
+def _read_off(path):
+    toks = []
+    for line in open(path):
+        toks += line.split("#")[0].split()
+    assert toks[0] == "OFF"
+    nv, nf = int(toks[1]), int(toks[2])
+    pts = np.array(toks[4:4 + 3 * nv], dtype=float).reshape(nv, 3)
+    f = np.array(toks[4 + 3 * nv:], dtype=int).reshape(nf, 4)
+    assert (f[:, 0] == 3).all()
+    return pts, f[:, 1:]
+
+
+def _inside_by_ray(pts, faces, q, d=(0.5773, 0.5781, 0.5761)):
+    """Crossing parity of a ray (Moller-Trumbore): an independent inside test."""
+    d = np.array(d)
+    n = 0
+    for a, b, c in faces:
+        A, B, C = pts[a], pts[b], pts[c]
+        e1, e2 = B - A, C - A
+        h = np.cross(d, e2)
+        det = e1 @ h
+        if abs(det) < 1e-15:
+            continue
+        s = q - A
+        u = (s @ h) / det
+        qq = np.cross(s, e1)
+        v = (d @ qq) / det
+        t = (e2 @ qq) / det
+        if u >= 0 and v >= 0 and u + v <= 1 and t > 0:
+            n += 1
+    return n % 2 == 1
+
+
+def test_fracture_off_fixture():
+    """meshes/layers_with_fracture.off: the 12 + 4 triangles of the layer box and the
+    fracture tetrahedron (12 vertices)."""
+    pts, faces = _read_off(FRACTURE_OFF)
+    assert pts.shape == (12, 3) and faces.shape == (16, 3)
+    assert pts[:8].min(0).tolist() == [0, 0, 0] and pts[:8].max(0).tolist() == [0.16, 0.16, 0.04]
+
+
+def test_fracture_mesh_is_carved(H):
+    """Cells whose centroid lies in the fracture are empty space: the kept cells'
+    centroids are inside the domain, every box cell missing from the mesh is in the
+    fracture, and the nodes around the cavity are border nodes."""
+    n = (16, 16, 8)
+    p = H.simplex_plans(fracture_task(n))
+    pts, faces = _read_off(FRACTURE_OFF)
+    P, C = p["coords"], p["cells"]
+    cen = P[C].mean(axis=1)
+    assert len(C) < 6 * n[0] * n[1] * n[2]
+    for q in cen[::97]:
+        assert _inside_by_ray(pts, faces, q)
+    # the border nodes that are not on the box surface surround the fracture
+    box = np.array([0.16, 0.16, 0.04])
+    inner_border = [i for i in p["border"] if np.all(P[i] > 0) and np.all(P[i] < box)]
+    assert len(inner_border) > 0
+    lo, hi = pts[8:].min(0) - 0.02, pts[8:].max(0) + 0.02
+    for i in inner_border:
+        assert np.all(P[i] >= lo) and np.all(P[i] <= hi)
+    # every vertex of the triangulation that survives keeps its cells
+    assert len(p["border"]) + len(p["inner"]) == len(P)
+
+
+@pytest.mark.parametrize("courant", [1.0, 1.7])
+def test_fracture_plans_match_oracle(H, courant):
+    p = H.simplex_plans(fracture_task((16, 16, 8), courant))
+    e = oracle_engine(p, courant, FREE_BORDER)
+    assert e.tau == p["tau"]
+    assert e.grid.border_idx == list(p["border"]) and e.grid.inner_idx == list(p["inner"])
+    for s in range(3):
+        st = p["stages"][s]
+        for it in range(len(p["coords"])):
+            for k in range(6):
+                f = e.feet[s][it][k]
+                assert int(st["kind"][it, k]) == KIND[f[0]], (s, it, k)
+                if f[0] == "cell":
+                    assert list(st["v"][it, k]) == list(f[1])
+    assert len(e.corrected) == len(p["border_plan"]["nodes"])
