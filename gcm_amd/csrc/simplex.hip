@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/gcmx.h"
+#include "contact.hpp"
 #include "launch.hpp"
 
 namespace {
@@ -76,6 +77,16 @@ struct gsx_ctx {
 	bool gradSet = false;
 	StageDev st[3];
 	BorderDev bd;
+};
+
+struct gsx_contact {
+	gsx_ctx *a = nullptr, *b = nullptr;
+	int n = 0;
+	int *na = nullptr, *nb = nullptr;
+	double *normal = nullptr, *S = nullptr;
+	signed char *codeA = nullptr, *codeB = nullptr;
+	double minDet[3][2] = {};
+	hipEvent_t evA = nullptr, evB = nullptr;
 };
 
 namespace {
@@ -365,6 +376,110 @@ __global__ __launch_bounds__(256) void k_sx_plain(const int* __restrict__ nodes,
 	for (int k = 0; k < kM; k++) u_[k * N + n] = u[k];
 }
 
+// ContactCorrectorInRiemannInvariants::applyInGlobalBasis (ContactCorrector.hpp:333-348):
+// matchInnersAndOuters (zeroing decided on the host), invariants -> PDE (U1),
+// ContactCorrectorInPdeVectors::applyInGlobalBasis (:150-247), PDE -> invariants (U).
+__global__ __launch_bounds__(256) void k_sx_contact(
+    const int* __restrict__ na, const int* __restrict__ nb, const double* __restrict__ normal,
+    const double* __restrict__ Sm, const signed char* __restrict__ codeA,
+    const signed char* __restrict__ codeB, const double* __restrict__ UA,
+    const double* __restrict__ U1A, const double* __restrict__ UB, const double* __restrict__ U1B,
+    double* wnA, double* wnB, int NA, int NB, int count, int stage, double min1, double min2) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= count) return;
+	const int a = na[t], b = nb[t];
+	const int ca = codeA[(size_t)stage * count + t], cb = codeB[(size_t)stage * count + t];
+	const int R[3] = {1, 3, 5}, L[3] = {0, 2, 4};  // Model.cpp:81-82
+	double wA[kM], wB[kM], uA[kM], uB[kM];
+	for (int k = 0; k < kM; k++) {
+		wA[k] = wnA[k * NA + a];
+		wB[k] = wnB[k * NB + b];
+	}
+	auto zero = [&](double (&w)[kM], int code) {
+		if (!(code & 4)) return;
+		if (code & 1) w[1] = w[3] = w[5] = 0;
+		if (code & 2) w[0] = w[2] = w[4] = 0;
+	};
+	zero(wA, ca);
+	zero(wB, cb);
+	mat_vec(U1A, wA, uA);
+	mat_vec(U1B, wB, uB);
+	const double n[3] = {normal[3 * t], normal[3 * t + 1], normal[3 * t + 2]};
+	double S[3][3];
+	for (int i = 0; i < 9; i++) S[i / 3][i % 3] = Sm[9 * (size_t)t + i];
+	double B1[3][kM], B2[3][kM];
+	gsx::fixedVelocityGlobal(B1);
+	gsx::fixedForceGlobal(n, B2);
+	const int oa = ca & 3, ob = cb & 3;
+	const int sa = oa == 0 ? 0 : oa == 3 ? 6 : 3, sb = ob == 0 ? 0 : ob == 3 ? 6 : 3;
+	if (sa == 3 && sb == 3) {
+		const auto c = gsx::contactCorrection(uA, U1A, oa == 1 ? R : L, uB, U1B, ob == 1 ? R : L, B1,
+		                                      B2, min1, min2);
+		if (c.ok) {
+			for (int k = 0; k < kM; k++) {
+				uA[k] += c.valueA[k];
+				uB[k] += c.valueB[k];
+			}
+		} else {
+			gsx::plainContactAverage(uA, uB, S);
+		}
+	} else if (sa == 6 && sb == 0) {
+		double v[kM];
+		if (gsx::doubleBorderCorrection(uA, U1A, uB, B1, B2, min1, v)) {
+			for (int k = 0; k < kM; k++) uA[k] += v[k];
+		} else {
+			gsx::plainContactOneSided(uA, uB, S);
+		}
+	} else if (sb == 6 && sa == 0) {
+		double v[kM];
+		if (gsx::doubleBorderCorrection(uB, U1B, uA, B1, B2, min1, v)) {
+			for (int k = 0; k < kM; k++) uB[k] += v[k];
+		} else {
+			gsx::plainContactOneSided(uB, uA, S);
+		}
+	} else {
+		const auto c1 = gsx::contactCorrection(uA, U1A, R, uB, U1B, L, B1, B2, min1, min2);
+		const auto c2 = gsx::contactCorrection(uA, U1A, L, uB, U1B, R, B1, B2, min1, min2);
+		if (c1.ok && c2.ok) {
+			for (int k = 0; k < kM; k++) {
+				uA[k] += (c1.valueA[k] + c2.valueA[k]) / 2;
+				uB[k] += (c1.valueB[k] + c2.valueB[k]) / 2;
+			}
+		} else {
+			gsx::plainContactAverage(uA, uB, S);
+		}
+	}
+	mat_vec(UA, uA, wA);
+	mat_vec(UB, uB, wB);
+	for (int k = 0; k < kM; k++) {
+		wnA[k * NA + a] = wA[k];
+		wnB[k * NB + b] = wB[k];
+	}
+}
+
+// ContactCorrectorInPdeVectors::applyPlainCorrection (ContactCorrector.hpp:249-262)
+// on the current layers.
+__global__ __launch_bounds__(256) void k_sx_contact_plain(const int* __restrict__ na,
+                                                          const int* __restrict__ nb,
+                                                          const double* __restrict__ Sm,
+                                                          double* uA_, double* uB_, int NA, int NB,
+                                                          int count) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= count) return;
+	const int a = na[t], b = nb[t];
+	double uA[kM], uB[kM], S[3][3];
+	for (int k = 0; k < kM; k++) {
+		uA[k] = uA_[k * NA + a];
+		uB[k] = uB_[k * NB + b];
+	}
+	for (int i = 0; i < 9; i++) S[i / 3][i % 3] = Sm[9 * (size_t)t + i];
+	gsx::plainContactAverage(uA, uB, S);
+	for (int k = 0; k < kM; k++) {
+		uA_[k * NA + a] = uA[k];
+		uB_[k * NB + b] = uB[k];
+	}
+}
+
 gcmx_status check(gsx_ctx* c) {
 	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null simplex context");
 	SX_TRY(hipSetDevice(c->device));
@@ -381,6 +496,21 @@ gcmx_status upload(T** dst, const T* src, size_t n) {
 	return GCMX_OK;
 }
 
+}  // namespace
+
+namespace {
+// Body b's stream work so far precedes the launch on a's stream, and the launch
+// precedes b's later work.
+template <class Launch>
+gcmx_status onBothStreams(gsx_contact* c, Launch launch) {
+	SX_TRY(hipEventRecord(c->evB, c->b->stream));
+	SX_TRY(hipStreamWaitEvent(c->a->stream, c->evB, 0));
+	launch();
+	SX_TRY(hipGetLastError());
+	SX_TRY(hipEventRecord(c->evA, c->a->stream));
+	SX_TRY(hipStreamWaitEvent(c->b->stream, c->evA, 0));
+	return GCMX_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -588,7 +718,7 @@ gcmx_status gsx_plain_correction(gsx_ctx* c) {
 	return GCMX_OK;
 }
 
-gcmx_status gsx_stage(gsx_ctx* c, int stage) {
+gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 	gcmx_status s = check(c);
 	if (s) return s;
 	if (stage < 0 || stage > 2) return fail(GCMX_ERR_INVALID_ARG, "stage out of range");
@@ -603,6 +733,19 @@ gcmx_status gsx_stage(gsx_ctx* c, int stage) {
 	if (st.nBorder)
 		hipLaunchKernelGGL(k_sx_nodes, dim3((st.nBorder + 255) / 256), blk, 0, c->stream, st.border,
 		                   st.nBorder, st.feet, c->coords, c->w, c->grad, c->wn, N);
+	SX_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
+gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
+	gcmx_status s = check(c);
+	if (s) return s;
+	if (stage < 0 || stage > 2) return fail(GCMX_ERR_INVALID_ARG, "stage out of range");
+	if (!c->matsSet || !c->gradSet || !c->st[stage].set)
+		return fail(GCMX_ERR_STATE, "simplex matrices / gradient plan / stage plan not set");
+	const int N = c->N;
+	const dim3 blk(256), grd((N + 255) / 256);
+	const StageDev& st = c->st[stage];
 	const BorderDev& bd = c->bd;
 	if (bd.set && bd.n) {
 		if (!bd.valuesSet) return fail(GCMX_ERR_STATE, "border values not set");
@@ -618,6 +761,93 @@ gcmx_status gsx_stage(gsx_ctx* c, int stage) {
 	SX_TRY(hipGetLastError());
 	std::swap(c->u, c->un);
 	return GCMX_OK;
+}
+
+gcmx_status gsx_stage(gsx_ctx* c, int stage) {
+	gcmx_status s = gsx_stage_nodes(c, stage);
+	if (s) return s;
+	return gsx_stage_finish(c, stage);
+}
+
+gcmx_status gsx_contact_create(gsx_ctx* a, gsx_ctx* b, int n, const int* nodes_a,
+                               const int* nodes_b, const double* normal, const double* S,
+                               const signed char* code_a, const signed char* code_b,
+                               const double* min_det, gsx_contact** out) {
+	if (!out) return fail(GCMX_ERR_INVALID_ARG, "null output");
+	*out = nullptr;
+	gcmx_status s = check(a);
+	if (s) return s;
+	if ((s = check(b))) return s;
+	if (a == b || a->device != b->device)
+		return fail(GCMX_ERR_INVALID_ARG, "a contact couples two bodies on one device");
+	if (n < 0 || !min_det || (n && (!nodes_a || !nodes_b || !normal || !S || !code_a || !code_b)))
+		return fail(GCMX_ERR_INVALID_ARG, "bad contact plan");
+	for (int i = 0; i < n; i++)
+		if (nodes_a[i] < 0 || nodes_a[i] >= a->N || nodes_b[i] < 0 || nodes_b[i] >= b->N)
+			return fail(GCMX_ERR_INVALID_ARG, "contact node out of range");
+	for (int i = 0; i < 3 * n; i++)
+		if (code_a[i] < 0 || code_a[i] > 7 || code_b[i] < 0 || code_b[i] > 7)
+			return fail(GCMX_ERR_INVALID_ARG, "bad contact wave code");
+	gsx_contact* c = new gsx_contact();
+	c->a = a;
+	c->b = b;
+	c->n = n;
+	for (int st = 0; st < 3; st++)
+		for (int k = 0; k < 2; k++) c->minDet[st][k] = min_det[st * 2 + k];
+	if ((s = upload(&c->na, nodes_a, (size_t)n)) || (s = upload(&c->nb, nodes_b, (size_t)n)) ||
+	    (s = upload(&c->normal, normal, 3 * (size_t)n)) || (s = upload(&c->S, S, 9 * (size_t)n)) ||
+	    (s = upload(&c->codeA, code_a, 3 * (size_t)n)) || (s = upload(&c->codeB, code_b, 3 * (size_t)n))) {
+		gsx_contact_destroy(c);
+		return s;
+	}
+	if (hipEventCreateWithFlags(&c->evA, hipEventDisableTiming) != hipSuccess ||
+	    hipEventCreateWithFlags(&c->evB, hipEventDisableTiming) != hipSuccess) {
+		gsx_contact_destroy(c);
+		return fail(GCMX_ERR_HIP, "hipEventCreate failed");
+	}
+	*out = c;
+	return GCMX_OK;
+}
+
+void gsx_contact_destroy(gsx_contact* c) {
+	if (!c) return;
+	(void)hipSetDevice(c->a->device);
+	void* ptrs[] = {c->na, c->nb, c->normal, c->S, c->codeA, c->codeB};
+	for (void* p : ptrs)
+		if (p) (void)hipFree(p);
+	if (c->evA) (void)hipEventDestroy(c->evA);
+	if (c->evB) (void)hipEventDestroy(c->evB);
+	delete c;
+}
+
+
+gcmx_status gsx_contact_plain(gsx_contact* c) {
+	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null contact");
+	gcmx_status s = check(c->a);
+	if (s) return s;
+	if (!c->n) return GCMX_OK;
+	return onBothStreams(c, [&] {
+		hipLaunchKernelGGL(k_sx_contact_plain, dim3((c->n + 255) / 256), dim3(256), 0, c->a->stream,
+		                   c->na, c->nb, c->S, c->a->u, c->b->u, c->a->N, c->b->N, c->n);
+	});
+}
+
+gcmx_status gsx_contact_correct(gsx_contact* c, int stage) {
+	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null contact");
+	gcmx_status s = check(c->a);
+	if (s) return s;
+	if (stage < 0 || stage > 2) return fail(GCMX_ERR_INVALID_ARG, "stage out of range");
+	if (!c->a->matsSet || !c->b->matsSet) return fail(GCMX_ERR_STATE, "simplex matrices not set");
+	if (!c->n) return GCMX_OK;
+	const double* mA = c->a->mats;
+	const double* mB = c->b->mats;
+	return onBothStreams(c, [&] {
+		hipLaunchKernelGGL(k_sx_contact, dim3((c->n + 255) / 256), dim3(256), 0, c->a->stream, c->na,
+		                   c->nb, c->normal, c->S, c->codeA, c->codeB, mA + stage * 81,
+		                   mA + 3 * 81 + stage * 81, mB + stage * 81, mB + 3 * 81 + stage * 81,
+		                   c->a->wn, c->b->wn, c->a->N, c->b->N, c->n, stage, c->minDet[stage][0],
+		                   c->minDet[stage][1]);
+	});
 }
 
 gcmx_status gsx_sync(gsx_ctx* c) {

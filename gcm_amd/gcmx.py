@@ -41,6 +41,8 @@ SYMBOLS = [
     "gsx_create", "gsx_destroy", "gsx_set_matrices", "gsx_set_gradient_plan",
     "gsx_set_stage_plan", "gsx_set_border_plan", "gsx_set_border_values",
     "gsx_plain_correction", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
+    "gsx_stage_nodes", "gsx_stage_finish", "gsx_contact_create", "gsx_contact_destroy",
+    "gsx_contact_plain", "gsx_contact_correct",
 ]
 
 

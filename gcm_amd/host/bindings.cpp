@@ -129,10 +129,9 @@ void writeVtkHost(const Task& task, size_t id, const std::string& fileName, py::
 	                           task.vtkSnapshotter.quantitiesToSnap);
 }
 
-/// GPU-free simplex set-up (simplex::buildHostPlans) as numpy arrays.
-py::dict simplexPlans(const Task& task) {
+/// One body of the GPU-free simplex set-up (simplex::buildHostPlans) as numpy arrays.
+py::dict simplexBodyDict(const simplex::BodyPlans& p, real tau) {
 	using namespace simplex;
-	const HostPlans p = buildHostPlans(task);
 	const ssize_t nv = p.mesh.nVertices(), nc = (ssize_t)p.mesh.cells.size();
 	py::array_t<double> coords({nv, (ssize_t)3});
 	for (ssize_t i = 0; i < nv; i++)
@@ -169,10 +168,12 @@ py::dict simplexPlans(const Task& task) {
 		stages.append(d);
 	}
 	py::dict d;
+	d["id"] = p.id;
 	d["coords"] = coords; d["cells"] = cells; d["U"] = U; d["U1"] = U1; d["pde"] = pde;
-	d["tau"] = p.tau; d["average_height"] = p.averageHeight;
+	d["tau"] = tau; d["average_height"] = p.averageHeight;
 	d["maximal_eigenvalue"] = p.maximalEigenvalue;
-	d["border"] = p.borderIdx; d["inner"] = p.innerIdx;
+	d["border"] = p.borderIdx; d["inner"] = p.innerIdx; d["contact"] = p.contactIdx;
+	d["global"] = p.mesh.global;
 	d["grad_offsets"] = p.gradient.offsets; d["grad_neighbors"] = p.gradient.neighbors;
 	d["grad_rows"] = p.gradient.rows; d["grad_weights"] = p.gradient.weights;
 	d["grad_M"] = p.gradient.M; d["grad_det"] = p.gradient.det;
@@ -189,10 +190,34 @@ py::dict simplexPlans(const Task& task) {
 	return d;
 }
 
+/// GPU-free simplex set-up: the first body's plans at the top level, every body in
+/// "bodies", the contacts in "contacts".
+py::dict simplexPlans(const Task& task) {
+	using namespace simplex;
+	const HostPlans hp = buildHostPlans(task);
+	py::dict d = simplexBodyDict(hp.bodies.at(0), hp.tau);
+	py::list bodies;
+	for (const auto& b : hp.bodies) bodies.append(simplexBodyDict(b, hp.tau));
+	d["bodies"] = bodies;
+	py::list contacts;
+	for (const auto& c : hp.contacts) {
+		py::dict cd;
+		cd["a"] = c.a; cd["b"] = c.b;
+		cd["nodes_a"] = c.nodesA; cd["nodes_b"] = c.nodesB;
+		cd["normal"] = c.normal; cd["S"] = c.S;
+		cd["code_a"] = std::vector<int>(c.codeA.begin(), c.codeA.end());
+		cd["code_b"] = std::vector<int>(c.codeB.begin(), c.codeB.end());
+		cd["min_det"] = std::vector<double>(&c.minDet[0][0], &c.minDet[0][0] + 6);
+		contacts.append(cd);
+	}
+	d["contacts"] = contacts;
+	return d;
+}
+
 struct PySimplexEngine {
 	std::shared_ptr<simplex::Engine> e;
-	py::array_t<double> pde() const {
-		const std::vector<double> v = e->pde();
+	py::array_t<double> pde(size_t body) const {
+		const std::vector<double> v = e->pde(body);
 		py::array_t<double> out({(ssize_t)(v.size() / 9), (ssize_t)9});
 		std::copy(v.begin(), v.end(), out.mutable_data());
 		return out;
@@ -351,7 +376,18 @@ PYBIND11_MODULE(_gcm_host, m) {
 	         [](Task& t, py::tuple area, size_t id) {
 		         t.simplexGrid.bodyAreas.push_back({makeArea(area), id});
 	         },
-	         py::arg("area"), py::arg("body"));
+	         py::arg("area"), py::arg("body"))
+	    .def("set_contact_condition",
+	         [](Task& t, const std::string& type, py::object pair) {
+		         ContactConditions::T c;
+		         if (type == "ADHESION") c = ContactConditions::T::ADHESION;
+		         else if (type == "SLIDE") c = ContactConditions::T::SLIDE;
+		         else throw Exception("unknown contact condition " + type);
+		         if (pair.is_none()) t.contactCondition.defaultCondition = c;
+		         else t.contactCondition.gridToGridConditions[pair.cast<std::pair<size_t, size_t>>()] = c;
+	         },
+	         py::arg("type"), py::arg("pair") = py::none(),
+	         "Task::contactCondition: the default, or the condition of one pair of bodies");
 
 	m.def(
 	    "host_state",
@@ -389,7 +425,9 @@ PYBIND11_MODULE(_gcm_host, m) {
 	         py::arg("task"), py::arg("device") = 0)
 	    .def("run", [](PySimplexEngine& p) { p.e->run(); })
 	    .def("run_steps", [](PySimplexEngine& p, int n) { p.e->runSteps(n); })
-	    .def("pde", &PySimplexEngine::pde, "current layer [n_vertices, 9]")
+	    .def("pde", &PySimplexEngine::pde, "current layer of a body [n_vertices, 9]",
+	         py::arg("body") = 0)
+	    .def_property_readonly("number_of_bodies", [](PySimplexEngine& p) { return p.e->numberOfBodies(); })
 	    .def_property_readonly("steps", [](PySimplexEngine& p) { return p.e->stepsDone(); })
 	    .def_property_readonly("time_step", [](PySimplexEngine& p) { return p.e->timeStepValue(); })
 	    .def_property_readonly("required_time", [](PySimplexEngine& p) { return p.e->getRequiredTime(); });

@@ -3,12 +3,15 @@
 // linal code operation by operation (paths relative to src/libgcm).
 #include "simplex.hpp"
 
+#include "../csrc/contact.hpp"
+
 #include <algorithm>
 #include <cmath>
 #include <fstream>
 #include <map>
 #include <sstream>
 #include <memory>
+#include <limits>
 #include <set>
 
 namespace gcm {
@@ -880,36 +883,29 @@ void calcBasis(const Task& task, real calc[3][3]) {
 }
 }  // namespace
 
-HostPlans buildHostPlans(const Task& task) {
-	if (task.globalSettings.dimensionality != 3) throw Exception("the simplex path is 3-D");
-	if (task.bodies.size() != 1) throw Exception("the simplex path takes one body");
-	const size_t id = task.bodies.begin()->first;
-	const auto& body = task.bodies.begin()->second;
+namespace {
+
+/// The set-up of one body (Engine::createMeshes, Engine.cpp:53-93 + the mesh's
+/// setUpPde): grid, matrices of its material, plans, initial state.
+BodyPlans buildBody(const Task& task, const Triangulation& tr, size_t id, const real calc[3][3]) {
+	const auto& body = task.bodies.at(id);
 	if (body.materialId != Materials::T::ISOTROPIC || body.modelId != Models::T::ELASTIC)
 		throw Exception("only isotropic elastic bodies are on this path");
 	if (!body.odes.empty()) throw Exception("ODEs are not on the simplex path");
-	// DefaultMesh::applyMaterialsCondition asserts BY_BODIES (engine/simplex/DefaultMesh.hpp:229-230)
-	if (task.materialConditions.type != Task::MaterialCondition::Type::BY_BODIES)
-		throw Exception("simplex materials must be given BY_BODIES");
+	if (!task.materialConditions.byBodies.bodyMaterialMap.count(id))
+		throw Exception("no material for a simplex body");
 	const auto mat = task.materialConditions.byBodies.bodyMaterialMap.at(id);
-	HostPlans p;
-	p.mesh = bodyMesh(buildTriangulation(task), (int)id);
+	BodyPlans p;
+	p.id = id;
+	p.mesh = bodyMesh(tr, (int)id);
 	Grid grid(p.mesh);
-	real calc[3][3];
-	calcBasis(task, calc);
 	ElasticModel<3>::constructGcmMatrices(p.matrices, *mat, calc);
 	p.maximalEigenvalue = p.matrices.getMaximalEigenvalue();
 	p.averageHeight = grid.averageHeight;
-	// simplex::Engine::estimateTimeStep (Engine.hpp:78-92)
-	p.tau = task.globalSettings.CourantNumber * grid.averageHeight / p.maximalEigenvalue;
 	p.gradient = buildGradientPlan(grid);
-	for (int s = 0; s < 3; s++) {
-		const Real3 dir = {calc[0][s], calc[1][s], calc[2][s]};
-		p.stages[s] = buildStagePlan(grid, dir, p.matrices.m[s].L.data(), p.tau);
-	}
-	p.border = buildBorderPlan(task, grid, p.matrices, calc, p.stages);
 	p.borderIdx = grid.borderIdx;
 	p.innerIdx = grid.innerIdx;
+	p.contactIdx = grid.contactIdx;
 	// InitialCondition::apply (util/task/InitialCondition.hpp:23-88): vectors and quantities
 	if (!task.initialCondition.waves.empty())
 		throw Exception("wave initial conditions are not on the simplex path");
@@ -936,17 +932,127 @@ HostPlans buildHostPlans(const Task& task) {
 	return p;
 }
 
-Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
-	HostPlans p = buildHostPlans(task);
-	mesh_ = std::move(p.mesh);
-	grid_ = std::make_unique<Grid>(mesh_);
-	maximalEigenvalue = p.maximalEigenvalue;
-	tau = p.tau;
-	const int nv = mesh_.nVertices();
-	std::vector<double> coords((size_t)nv * 3);
-	for (int i = 0; i < nv; i++)
-		for (int c = 0; c < 3; c++) coords[(size_t)i * 3 + c] = mesh_.v[i][c];
-	gcmxCheck(gsx_create(device, nv, coords.data(), &ctx), "gsx_create");
+int outerSize(int code) { return code == 0 ? 0 : code == 3 ? 6 : 3; }
+
+/// ContactCorrectorInRiemannInvariants::matchInnersAndOuters (ContactCorrector.hpp:365-397)
+/// on the stage's wave-index codes (0 none, 1 RIGHT, 2 LEFT, 3 both).
+void matchInnersAndOuters(int& a, int& b, bool& zeroed) {
+	const int N = (outerSize(a) + outerSize(b)) / 3;
+	zeroed = false;
+	if (N % 2 == 0) return;
+	if (N == 3) {
+		a = b = 3;
+	} else {
+		if (a == 0) a = (b == 2) ? 1 : 2;  // B LEFT -> A RIGHT, B RIGHT -> A LEFT
+		else b = (a == 2) ? 1 : 2;
+	}
+	zeroed = true;
+}
+
+/// Engine::createContacts (Engine.cpp:220-248) + addBorderOrContact / addContactNode
+/// (:252-287) for one pair of bodies, and the per-stage data of the corrector.
+ContactPlan buildContact(const Task& task, const Triangulation& tr, const std::vector<BodyPlans>& bodies,
+                         size_t ia, size_t ib, const real calc[3][3]) {
+	ContactPlan cp;
+	cp.a = ia;
+	cp.b = ib;
+	const BodyPlans& A = bodies[ia];
+	const BodyPlans& B = bodies[ib];
+	cp.condition = task.contactCondition.defaultCondition;
+	const auto key = std::make_pair(A.id, B.id);
+	if (task.contactCondition.gridToGridConditions.count(key))
+		cp.condition = task.contactCondition.gridToGridConditions.at(key);
+	// ContactCorrectorFactory (ContactCorrector.hpp:506-552): ADHESION needs elastic
+	// bodies, SLIDE acoustic ones (not on this path)
+	if (cp.condition != ContactConditions::T::ADHESION)
+		throw Exception("only ADHESION contacts between elastic bodies are supported");
+	Grid gA(A.mesh), gB(B.mesh);
+	std::vector<int> localA((size_t)tr.all.nVertices(), -1), localB((size_t)tr.all.nVertices(), -1);
+	for (int i = 0; i < A.mesh.nVertices(); i++) localA[(size_t)A.mesh.global[(size_t)i]] = i;
+	for (int i = 0; i < B.mesh.nVertices(); i++) localB[(size_t)B.mesh.global[(size_t)i]] = i;
+	for (int g = 0; g < tr.all.nVertices(); g++) {  // triangulation vertex order
+		const int la = localA[(size_t)g], lb = localB[(size_t)g];
+		if (la < 0 || lb < 0) continue;
+		const auto& o = A.mesh.otherGrids[(size_t)la];
+		if (o.size() != 1 || o[0] != (int)B.id) continue;  // incidentGrids == {A, B}
+		const Real3 n = gA.contactNormal(la, (int)B.id);
+		if (n[0] == 0 && n[1] == 0 && n[2] == 0) continue;
+		cp.nodesA.push_back(la);
+		cp.nodesB.push_back(lb);
+		for (int r = 0; r < 3; r++) cp.normal.push_back(n[r]);
+		real S[3][3];
+		detail::localBasisOf<3>(n.data(), S);
+		for (int r = 0; r < 3; r++)
+			for (int c = 0; c < 3; c++) cp.S.push_back(S[r][c]);
+	}
+	const size_t nn = cp.nodesA.size();
+	cp.codeA.assign(3 * nn, 0);
+	cp.codeB.assign(3 * nn, 0);
+	for (int s = 0; s < 3; s++)
+		for (size_t i = 0; i < nn; i++) {
+			int a = A.stages[s].outerCode[(size_t)cp.nodesA[i]];
+			int b = B.stages[s].outerCode[(size_t)cp.nodesB[i]];
+			bool zeroed;
+			matchInnersAndOuters(a, b, zeroed);
+			cp.codeA[s * nn + i] = (signed char)(a | (zeroed ? 4 : 0));
+			cp.codeB[s * nn + i] = (signed char)(b | (zeroed ? 4 : 0));
+		}
+	// getMaximalPossibleDeterminants (ContactCorrector.hpp:250-276): B along the
+	// stage direction, A's LEFT and B's RIGHT outer columns
+	if (nn) {
+		static const int LEFT[3] = {0, 2, 4}, RIGHT[3] = {1, 3, 5};
+		for (int s = 0; s < 3; s++) {
+			const double dir[3] = {calc[0][s], calc[1][s], calc[2][s]};
+			double B1[3][9], B2[3][9];
+			gsx::fixedVelocityGlobal(B1);
+			gsx::fixedForceGlobal(dir, B2);
+			const double zero[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+			const auto c = gsx::contactCorrection(zero, A.matrices.m[s].U1.data(), LEFT, zero,
+			                                      B.matrices.m[s].U1.data(), RIGHT, B1, B2, 0, 0);
+			if (!c.ok || !(c.det1 > 0) || !(c.det2 > 0))
+				throw Exception("degenerate contact system along the stage direction");
+			cp.minDet[s][0] = 1e-3 * c.det1;
+			cp.minDet[s][1] = 1e-3 * c.det2;
+		}
+	}
+	return cp;
+}
+
+}  // namespace
+
+HostPlans buildHostPlans(const Task& task) {
+	if (task.globalSettings.dimensionality != 3) throw Exception("the simplex path is 3-D");
+	if (task.bodies.empty()) throw Exception("the simplex task has no bodies");
+	// DefaultMesh::applyMaterialsCondition asserts BY_BODIES (engine/simplex/DefaultMesh.hpp:229-230)
+	if (task.materialConditions.type != Task::MaterialCondition::Type::BY_BODIES)
+		throw Exception("simplex materials must be given BY_BODIES");
+	real calc[3][3];
+	calcBasis(task, calc);
+	const Triangulation tr = buildTriangulation(task);
+	HostPlans hp;
+	for (const auto& b : task.bodies) hp.bodies.push_back(buildBody(task, tr, b.first, calc));
+	// simplex::Engine::estimateTimeStep (Engine.hpp:78-92): minimal over bodies
+	hp.tau = std::numeric_limits<real>::max();
+	for (const auto& b : hp.bodies) {
+		const real t = task.globalSettings.CourantNumber * b.averageHeight / b.maximalEigenvalue;
+		if (t < hp.tau) hp.tau = t;
+	}
+	for (auto& b : hp.bodies) {
+		Grid grid(b.mesh);
+		for (int s = 0; s < 3; s++) {
+			const Real3 dir = {calc[0][s], calc[1][s], calc[2][s]};
+			b.stages[s] = buildStagePlan(grid, dir, b.matrices.m[s].L.data(), hp.tau);
+		}
+		b.border = buildBorderPlan(task, grid, b.matrices, calc, b.stages);
+	}
+	for (size_t i = 0; i < hp.bodies.size(); i++)  // Utils::makePairs order
+		for (size_t j = i + 1; j < hp.bodies.size(); j++)
+			hp.contacts.push_back(buildContact(task, tr, hp.bodies, i, j, calc));
+	return hp;
+}
+
+namespace {
+void uploadBody(gsx_ctx* ctx, const BodyPlans& p) {
 	std::vector<double> U(3 * 81), U1(3 * 81);
 	for (int s = 0; s < 3; s++) {
 		std::copy(p.matrices.m[s].U.begin(), p.matrices.m[s].U.end(), U.begin() + s * 81);
@@ -965,18 +1071,44 @@ Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
 		          "gsx_set_stage_plan");
 	}
 	gcmxCheck(gsx_upload(ctx, p.pde.data()), "gsx_upload");
+}
+}  // namespace
+
+Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
+	HostPlans p = buildHostPlans(task);
+	tau = p.tau;
 	conditions = task.borderConditions;
-	const auto& b = p.border;
-	if (!conditions.empty()) {
-		gcmxCheck(gsx_set_border_plan(ctx, (int)b.type.size(), b.type.data(), b.minDet.data(),
-		                              (int)b.nodes.size(), b.nodes.data(), b.cond.data(), b.B.data(),
-		                              b.S.data(), b.outer.data()),
-		          "gsx_set_border_plan");
-		hasBorderPlan = true;
-		// applyPlainBorderContactCorrection(Clock::Time()) (Engine.cpp:44)
-		setBorderValues(Clock::Time());
-		gcmxCheck(gsx_plain_correction(ctx), "gsx_plain_correction");
+	for (auto& bp : p.bodies) {
+		Body b;
+		const int nv = bp.mesh.nVertices();
+		std::vector<double> coords((size_t)nv * 3);
+		for (int i = 0; i < nv; i++)
+			for (int c = 0; c < 3; c++) coords[(size_t)i * 3 + c] = bp.mesh.v[(size_t)i][c];
+		gcmxCheck(gsx_create(device, nv, coords.data(), &b.ctx), "gsx_create");
+		bodies.push_back(std::move(b));
+		Body& body = bodies.back();
+		body.mesh = std::move(bp.mesh);
+		uploadBody(body.ctx, bp);
+		const auto& bd = bp.border;
+		if (!conditions.empty()) {
+			gcmxCheck(gsx_set_border_plan(body.ctx, (int)bd.type.size(), bd.type.data(),
+			                              bd.minDet.data(), (int)bd.nodes.size(), bd.nodes.data(),
+			                              bd.cond.data(), bd.B.data(), bd.S.data(), bd.outer.data()),
+			          "gsx_set_border_plan");
+			body.hasBorderPlan = true;
+		}
 	}
+	for (const auto& cp : p.contacts) {
+		gsx_contact* c = nullptr;
+		gcmxCheck(gsx_contact_create(bodies[cp.a].ctx, bodies[cp.b].ctx, (int)cp.nodesA.size(),
+		                             cp.nodesA.data(), cp.nodesB.data(), cp.normal.data(), cp.S.data(),
+		                             cp.codeA.data(), cp.codeB.data(), &cp.minDet[0][0], &c),
+		          "gsx_contact_create");
+		contacts.push_back(c);
+	}
+	// applyPlainBorderContactCorrection(Clock::Time()) (Engine.cpp:44)
+	setBorderValues(Clock::Time());
+	plainCorrections();
 	afterConstruction(task);
 }
 
@@ -984,27 +1116,42 @@ void Engine::setBorderValues(real time) {
 	std::vector<double> v;
 	for (const auto& c : conditions)
 		for (const auto& f : c.values) v.push_back(f(time));  // BorderCondition::b (:33-40)
-	gcmxCheck(gsx_set_border_values(ctx, v.data()), "gsx_set_border_values");
+	for (auto& b : bodies)
+		if (b.hasBorderPlan) gcmxCheck(gsx_set_border_values(b.ctx, v.data()), "gsx_set_border_values");
 }
 
-Engine::~Engine() { gsx_destroy(ctx); }
+/// applyPlainBorderContactCorrection (Engine.cpp:193-211): contacts, then borders.
+void Engine::plainCorrections() {
+	for (auto* c : contacts) gcmxCheck(gsx_contact_plain(c), "gsx_contact_plain");
+	for (auto& b : bodies)
+		if (b.hasBorderPlan) gcmxCheck(gsx_plain_correction(b.ctx), "gsx_plain_correction");
+}
+
+Engine::~Engine() {
+	for (auto* c : contacts) gsx_contact_destroy(c);
+	for (auto& b : bodies) gsx_destroy(b.ctx);
+}
 
 real Engine::estimateTimeStep() { return tau; }
 
-// simplex::Engine::nextTimeStep (engine/simplex/Engine.cpp:95-116) with a
-// constant basis: plain border correction at the next time layer, then the three
-// gcmStage calls (the border correctors run inside gsx_stage with b(t + tau)).
+// simplex::Engine::nextTimeStep (engine/simplex/Engine.cpp:95-116) with a constant
+// basis: plain corrections at the next time layer, then gcmStage (:119-143) for
+// every stage: beforeStage + contactAndBorderStage of every body, the contact
+// correctors, then (per body) its border correctors, innerStage, afterStage, swap.
 void Engine::nextTimeStep() {
-	if (hasBorderPlan) {
-		setBorderValues(Clock::Time() + Clock::TimeStep());
-		gcmxCheck(gsx_plain_correction(ctx), "gsx_plain_correction");
+	setBorderValues(Clock::Time() + Clock::TimeStep());
+	plainCorrections();
+	for (int stage = 0; stage < 3; stage++) {
+		for (auto& b : bodies) gcmxCheck(gsx_stage_nodes(b.ctx, stage), "gsx_stage_nodes");
+		for (auto* c : contacts) gcmxCheck(gsx_contact_correct(c, stage), "gsx_contact_correct");
+		for (auto& b : bodies) gcmxCheck(gsx_stage_finish(b.ctx, stage), "gsx_stage_finish");
 	}
-	for (int stage = 0; stage < 3; stage++) gcmxCheck(gsx_stage(ctx, stage), "gsx_stage");
 }
 
-std::vector<real> Engine::pde() const {
-	std::vector<real> out((size_t)mesh_.nVertices() * 9);
-	gcmxCheck(gsx_download(ctx, out.data()), "gsx_download");
+std::vector<real> Engine::pde(size_t body) const {
+	const Body& b = bodies.at(body);
+	std::vector<real> out((size_t)b.mesh.nVertices() * 9);
+	gcmxCheck(gsx_download(b.ctx, out.data()), "gsx_download");
 	return out;
 }
 

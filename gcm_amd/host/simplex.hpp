@@ -185,19 +185,58 @@ BorderPlan buildBorderPlan(const Task& task, const Grid& grid, const GcmMatrices
 namespace gcm {
 namespace simplex {
 
-/// simplex::Engine<3, CgalTriangulation> (engine/simplex/Engine.{hpp,cpp}) for one
-/// isotropic-elastic body: GcmType ADVECT_RIEMANN_INVARIANTS, SplittingType
+/// One contact of Engine::contacts (engine/simplex/Engine.hpp:36-47): the node
+/// pairs addContactNode collected (Engine.cpp:273-287) in triangulation order,
+/// with the static data ContactCorrectorInRiemannInvariants needs per stage.
+struct ContactPlan {
+	size_t a = 0, b = 0;               // indices into HostPlans::bodies (ids a < b)
+	ContactConditions::T condition = ContactConditions::T::ADHESION;
+	std::vector<int> nodesA, nodesB;   // local vertex indices
+	std::vector<double> normal;        // [n][3] contactNormal of A towards B
+	std::vector<double> S;             // [n][9] createLocalBasis(normal), row-major
+	/// [3][n] per side: wave indices after matchInnersAndOuters
+	/// (ContactCorrector.hpp:365-397): bits 0-1 = 0 none, 1 RIGHT, 2 LEFT, 3 both;
+	/// bit 2 = the matching zeroed those invariants (odd N)
+	std::vector<signed char> codeA, codeB;
+	double minDet[3][2] = {};          // 1e-3 * getMaximalPossibleDeterminants (:250-276)
+};
+
+/// Everything simplex::Engine's constructor builds for one body.
+struct BodyPlans {
+	size_t id = 0;
+	TetMesh mesh;
+	real averageHeight = 0, maximalEigenvalue = 0;
+	GcmMatrices<3> matrices;
+	GradientPlan gradient;
+	StagePlan stages[3];
+	BorderPlan border;
+	std::vector<real> pde;  // initial layer, 9 per vertex
+	std::vector<int> borderIdx, innerIdx, contactIdx;
+};
+
+/// GPU-free set-up of the simplex path: the task's bodies (ascending ids), their
+/// contacts (Utils::makePairs order) and the time step.
+struct HostPlans {
+	real tau = 0;
+	std::vector<BodyPlans> bodies;
+	std::vector<ContactPlan> contacts;
+};
+HostPlans buildHostPlans(const Task& task);
+
+/// simplex::Engine<3, CgalTriangulation> (engine/simplex/Engine.{hpp,cpp}) for
+/// isotropic-elastic bodies: GcmType ADVECT_RIEMANN_INVARIANTS, SplittingType
 /// PRODUCT, BorderCalcMode GLOBAL_BASIS, constant Task::calculationBasis,
 /// Task::borderConditions through the border correctors (FIXED_FORCE,
-/// FIXED_VELOCITY); border nodes no condition covers keep zero outer invariants.
+/// FIXED_VELOCITY) and ADHESION contacts through the contact correctors; border
+/// nodes no condition covers keep zero outer invariants.
 class Engine : public AbstractEngine {
 public:
 	explicit Engine(const Task& task, int device = 0);
 	~Engine() override;
-	const Grid& grid() const { return *grid_; }
-	const TetMesh& mesh() const { return mesh_; }
-	/// current layer, 9 doubles per vertex (downloads)
-	std::vector<real> pde() const;
+	size_t numberOfBodies() const { return bodies.size(); }
+	const TetMesh& mesh(size_t body = 0) const { return bodies.at(body).mesh; }
+	/// current layer of a body, 9 doubles per vertex (downloads)
+	std::vector<real> pde(size_t body = 0) const;
 	real timeStepValue() const { return tau; }
 
 protected:
@@ -206,28 +245,18 @@ protected:
 	void writeSnapshots(const int) override {}
 
 private:
-	TetMesh mesh_;
-	std::unique_ptr<Grid> grid_;
-	gsx_ctx* ctx = nullptr;
-	real maximalEigenvalue = 0, tau = 0;
+	struct Body {
+		TetMesh mesh;
+		gsx_ctx* ctx = nullptr;
+		bool hasBorderPlan = false;
+	};
+	std::vector<Body> bodies;
+	std::vector<gsx_contact*> contacts;
+	real tau = 0;
 	std::vector<Task::BorderCondition> conditions;
-	bool hasBorderPlan = false;
 	void setBorderValues(real time);
+	void plainCorrections();
 };
-
-/// GPU-free set-up of the simplex path: mesh, the time step and the static plans
-/// the Engine uploads (for tests and tools).
-struct HostPlans {
-	TetMesh mesh;
-	real averageHeight = 0, maximalEigenvalue = 0, tau = 0;
-	GcmMatrices<3> matrices;
-	GradientPlan gradient;
-	StagePlan stages[3];
-	BorderPlan border;
-	std::vector<real> pde;  // initial layer, 9 per vertex
-	std::vector<int> borderIdx, innerIdx;
-};
-HostPlans buildHostPlans(const Task& task);
 
 }  // namespace simplex
 }  // namespace gcm

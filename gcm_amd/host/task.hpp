@@ -56,6 +56,10 @@ struct BorderConditions {
 struct Grids {
 	enum class T { CUBIC, SIMPLEX };
 };
+/// util/Enum.hpp:70-76
+struct ContactConditions {
+	enum class T { ADHESION, SLIDE };
+};
 
 // ------------------------------------------------------------------ areas --
 /// util/math/Area.hpp:8-120.  contains() is strict (points on the border are outside).
@@ -247,6 +251,13 @@ struct Task {
 		std::vector<TimeDependency> values;
 	};
 	std::vector<BorderCondition> borderConditions;
+
+	/// Task::ContactCondition (Task.hpp:216-220): simplex contact correctors between
+	/// bodies (pair key = (smaller id, larger id)).
+	struct ContactCondition {
+		ContactConditions::T defaultCondition = ContactConditions::T::ADHESION;
+		std::map<std::pair<size_t, size_t>, ContactConditions::T> gridToGridConditions;
+	} contactCondition;
 
 	/// The reference's Task::calculationBasis (Task.hpp:129): 9 numbers, column i =
 	/// direction of stage i.  Required (constant) on the simplex path here.

@@ -236,8 +236,38 @@ gcmx_status gsx_set_border_values(gsx_ctx* ctx, const double* b);
 gcmx_status gsx_plain_correction(gsx_ctx* ctx);
 /* One stage: beforeStage (invariants + gradients), contactAndBorderStage,
  * the border correctors (applyInGlobalBasis, when a border plan is set),
- * innerStage, afterStage (U1) and the PRODUCT swap (engine/simplex/Engine.cpp:117-148). */
+ * innerStage, afterStage (U1) and the PRODUCT swap (engine/simplex/Engine.cpp:117-148).
+ * gsx_stage = gsx_stage_nodes + gsx_stage_finish; a multi-body engine runs the
+ * contact correctors (gsx_contact_correct) of every contact between the two halves
+ * of every body, as Engine::gcmStage orders them (Engine.cpp:119-143). */
 gcmx_status gsx_stage(gsx_ctx* ctx, int stage);
+/* beforeStage + contactAndBorderStage (contact and border nodes' new invariants). */
+gcmx_status gsx_stage_nodes(gsx_ctx* ctx, int stage);
+/* border correctors + innerStage + afterStage + swap. */
+gcmx_status gsx_stage_finish(gsx_ctx* ctx, int stage);
+
+/* ---- simplex contact correctors ----------------------------------------------
+ * ContactCorrectorInRiemannInvariants<Elastic, Elastic, AdhesionContactMatrixCreator>
+ * (engine/simplex/ContactCorrector.hpp:303-419, 466-483) between two bodies on the
+ * same device: one entry of Engine::contacts (Engine.hpp:36-47, Engine.cpp:220-287).
+ * Pair i couples node nodes_a[i] of body a with nodes_b[i] of body b; normal[i]
+ * is contactNormal of a towards b [n][3], S[i] = createLocalBasis(normal[i])
+ * [n][9] row-major.  code_a / code_b [3][n]: per stage the node's wave indices
+ * after matchInnersAndOuters (bits 0-1: 0 none, 1 RIGHT {1,3,5}, 2 LEFT {0,2,4},
+ * 3 both; bit 2: the matching zeroed them).  min_det [3][2] = 1e-3 *
+ * getMaximalPossibleDeterminants of each stage (ContactCorrector.hpp:250-276). */
+typedef struct gsx_contact gsx_contact;
+gcmx_status gsx_contact_create(gsx_ctx* a, gsx_ctx* b, int n, const int* nodes_a,
+                               const int* nodes_b, const double* normal, const double* S,
+                               const signed char* code_a, const signed char* code_b,
+                               const double* min_det, gsx_contact** out);
+void        gsx_contact_destroy(gsx_contact* c);
+/* applyPlainCorrection (ContactCorrector.hpp:420-430 -> ElasticModel::
+ * applyPlainContactCorrectionAsAverage, ElasticModel.hpp:239-272) on the current layers. */
+gcmx_status gsx_contact_plain(gsx_contact* c);
+/* applyInGlobalBasis at stage `stage` (ContactCorrector.hpp:333-348, 150-247) on the
+ * new-layer invariants; call between gsx_stage_nodes and gsx_stage_finish of both bodies. */
+gcmx_status gsx_contact_correct(gsx_contact* c, int stage);
 gcmx_status gsx_sync(gsx_ctx* ctx);
 
 /* ---- synchronisation and timing ------------------------------------------- */

@@ -316,10 +316,17 @@ def plain_border_correction(u, kind, normal, value):  # ElasticModel.hpp:202-228
 
 # --------------------------------------------------------------- grid --
 
-class Grid:
-    """SimplexGrid<3> over a given mesh (coords [n][3], cells [m][4])."""
+EMPTY = -1                  # Grid::EmptySpaceFlag
 
-    def __init__(self, coords: Sequence[Sequence[float]], cells: Sequence[Sequence[int]]):
+
+class Grid:
+    """SimplexGrid<3> over a given mesh (coords [n][3], cells [m][4]).  For a body of
+    a multi-body task, ``face_grid(cell, i)`` names the grid across a face with no
+    neighbour in the body (EMPTY or another body id) and ``other_grids[it]`` the
+    other grid ids around a vertex (SimplexGrid::gridsAroundVertex minus its own)."""
+
+    def __init__(self, coords: Sequence[Sequence[float]], cells: Sequence[Sequence[int]],
+                 face_grid=None, other_grids=None):
         self.P = [tuple(float(x) for x in c) for c in coords]
         self.cells = [tuple(int(x) for x in c) for c in cells]
         nv = len(self.P)
@@ -344,16 +351,35 @@ class Grid:
                 if self.nb[ci][i] < 0:
                     for k in range(1, 4):
                         self.inner[c[(i + k) % 4]] = False
+        self.face_grid = face_grid or (lambda ci, i: EMPTY)
+        if other_grids is None:
+            other_grids = [[] if self.inner[i] else [EMPTY] for i in range(nv)]
+        self.other_grids = other_grids
+        for i in range(nv):
+            assert (not other_grids[i]) == self.inner[i]
+        # markInnersAndBorders (SimplexGrid.cpp:216-252)
         self.inner_idx = [i for i in range(nv) if self.inner[i]]
-        self.border_idx = [i for i in range(nv) if not self.inner[i]]
+        self.contact_idx = [i for i in range(nv) if len(other_grids[i]) == 1
+                            and other_grids[i][0] != EMPTY]
+        cs = set(self.contact_idx)
+        self.border_idx = [i for i in range(nv) if not self.inner[i] and i not in cs]
         self.average_height = self._average_height()
 
     def border_normal(self, it):  # SimplexGrid.hpp:151-154, 426-444; Cgal3DTriangulation.hpp:109-118
+        return self.normal(it, lambda g: g == EMPTY)
+
+    def contact_normal(self, it, other):  # SimplexGrid.hpp:141-144
+        return self.normal(it, lambda g: g == other)
+
+    def common_normal(self, it):  # SimplexGrid.hpp:157-160
+        return self.normal(it, lambda g: True)
+
+    def normal(self, it, use):
         normals = []
         for ci in self.inc[it]:
             c = self.cells[ci]
             for i in range(4):
-                if self.nb[ci][i] < 0 and c[i] != it:
+                if self.nb[ci][i] < 0 and c[i] != it and use(self.face_grid(ci, i)):
                     normals.append(_opposite_face_normal(
                         self.P[c[i]], self.P[c[(i + 1) % 4]], self.P[c[(i + 2) % 4]],
                         self.P[c[(i + 3) % 4]]))
@@ -575,12 +601,13 @@ class Engine:
              (0, 2, 3, 4), (0, 2, 3, 5), (0, 2, 4, 5), (0, 3, 4, 5), (1, 2, 3, 4), (1, 2, 3, 5),
              (1, 2, 4, 5), (1, 3, 4, 5), (2, 3, 4, 5)]
 
-    def __init__(self, coords, cells, U, U1, L, basis, courant, pde0, border_conditions=()):
+    def __init__(self, coords, cells, U, U1, L, basis, courant, pde0, border_conditions=(),
+                 grid=None, tau=None):
         """U, U1: [3][9][9]; L: [3][9]; basis: 3x3 (column s = stage s); pde0 [n][9];
         border_conditions: Task::borderConditions as dicts {"contains": point -> bool,
         "type": "FIXED_FORCE" | "FIXED_VELOCITY", "values": [3 functions of t],
         "multi": useForMulticontactNodes}."""
-        self.grid = Grid(coords, cells)
+        self.grid = grid if grid is not None else Grid(coords, cells)
         self.U = [[[float(x) for x in row] for row in U[s]] for s in range(3)]
         self.U1 = [[[float(x) for x in row] for row in U1[s]] for s in range(3)]
         self.L = [[float(x) for x in L[s]] for s in range(3)]
@@ -590,6 +617,8 @@ class Engine:
             for k in range(9):
                 mx = max(mx, abs(self.L[s][k]))
         self.tau = courant * self.grid.average_height / mx  # Engine.hpp:78-92
+        if tau is not None:
+            self.tau = tau                    # minimal over the bodies
         self.u = [[float(x) for x in row] for row in pde0]
         self.outers = [{} for _ in range(3)]
         self.feet = [self._plan(s) for s in range(3)]
@@ -603,15 +632,15 @@ class Engine:
         g = self.grid
         self.corrected = []                   # (node, condition, normal)
         for it in g.border_idx:
-            n = g.border_normal(it)
-            multi = n == (0.0, 0.0, 0.0)
+            multi = g.border_normal(it) == (0.0, 0.0, 0.0)
             chosen = None
             for ci, c in enumerate(self.conditions):
                 if c["contains"](g.P[it]) and (not multi or c.get("multi", True)):
                     chosen = ci
             if chosen is None:
                 continue
-            if multi:
+            n = g.common_normal(it)
+            if n == (0.0, 0.0, 0.0):
                 raise ValueError("zero common normal at a border node")
             self.corrected.append((it, chosen, n))
         self.min_det = {}
@@ -748,23 +777,37 @@ class Engine:
             out.append(s)
         return out
 
-    def stage(self, s, t_next=None):
-        """gcmStage with PRODUCT splitting (engine/simplex/Engine.cpp:119-135)."""
+    def stage_nodes(self, s):
+        """beforeStage + contactAndBorderStage (engine/simplex/Engine.cpp:119-127)."""
         g = self.grid
         n = len(g.P)
-        w = [self._mat_vec(self.U[s], self.u[i]) for i in range(n)]     # beforeStage
-        grads = g.gradients(w)
-        wn = [[0.0] * 9 for _ in range(n)]
-        for order in (g.border_idx, g.inner_idx):  # contactAndBorderStage, innerStage
-            if order is g.inner_idx and self.corrected:   # correctContactsAndBorders
-                self._correct(s, wn, self.time + self.tau if t_next is None else t_next)
-            for it in order:
-                for k in range(9):
-                    if k >= 6:
-                        wn[it][k] = w[it][k]
-                    else:
-                        wn[it][k] = self._interp(it, k, self.feet[s][it][k], w, wn, grads)
-        self.u = [self._mat_vec(self.U1[s], wn[i]) for i in range(n)]   # afterStage + swap
+        self._w = w = [self._mat_vec(self.U[s], self.u[i]) for i in range(n)]
+        self._grads = g.gradients(w)
+        self.wn = [[0.0] * 9 for _ in range(n)]
+        for it in g.contact_idx + g.border_idx:
+            self._node(s, it)
+
+    def stage_finish(self, s, t_next=None):
+        """border correctors, innerStage, afterStage + swap (Engine.cpp:128-143)."""
+        g = self.grid
+        if self.corrected:
+            self._correct(s, self.wn, self.time + self.tau if t_next is None else t_next)
+        for it in g.inner_idx:
+            self._node(s, it)
+        self.u = [self._mat_vec(self.U1[s], self.wn[i]) for i in range(len(g.P))]
+
+    def _node(self, s, it):
+        for k in range(9):
+            if k >= 6:
+                self.wn[it][k] = self._w[it][k]
+            else:
+                self.wn[it][k] = self._interp(it, k, self.feet[s][it][k], self._w, self.wn,
+                                              self._grads)
+
+    def stage(self, s, t_next=None):
+        """gcmStage with PRODUCT splitting (engine/simplex/Engine.cpp:119-135)."""
+        self.stage_nodes(s)
+        self.stage_finish(s, t_next)
 
     def step(self):
         """simplex::Engine::nextTimeStep (Engine.cpp:95-116) + the Clock tick."""
@@ -773,3 +816,344 @@ class Engine:
         for s in range(3):
             self.stage(s, t_next)
         self.time = self.time + self.tau
+
+
+# ------------------------------------------------------- contact correctors --
+# engine/simplex/ContactCorrector.hpp (ContactCorrectorInRiemannInvariants over
+# ContactCorrectorInPdeVectors, AdhesionContactMatrixCreator), the two-body
+# calculateOuterWaveCorrection (common.hpp:220-260), ElasticModel's global-basis
+# border matrices and plain contact corrections (ElasticModel.hpp:157-300), and
+# the 6 x 6 determinant / solve of util/math/GslUtils.hpp through GSL's LU
+# (gsl_linalg_LU_decomp / _det / _solve; GSL is absent and not vendored: the
+# classic Doolittle algorithm with partial pivoting is restated -- unpinned).
+
+def _b1_global():  # borderMatrixFixedVelocityGlobalBasis (ElasticModel.hpp:183-194)
+    return [[1.0 if k == i else 0.0 for k in range(9)] for i in range(3)]
+
+
+def _b2_global(n):  # borderMatrixFixedForceGlobalBasis (ElasticModel.hpp:162-176)
+    B = []
+    for i in range(3):
+        row = [0.0] * 9
+        for j in range(3):
+            row[_sym(i, j)] = n[j]
+        B.append(row)
+    return B
+
+
+def _col(v):
+    return [[x] for x in v]
+
+
+def _flat(m):
+    return [r[0] for r in m]
+
+
+def _invert33(m):  # linal/functions.hpp:128-134
+    c = [m[1][1] * m[2][2] - m[1][2] * m[2][1], m[0][2] * m[2][1] - m[0][1] * m[2][2],
+         m[0][1] * m[1][2] - m[1][1] * m[0][2], m[1][2] * m[2][0] - m[1][0] * m[2][2],
+         m[0][0] * m[2][2] - m[0][2] * m[2][0], m[0][2] * m[1][0] - m[0][0] * m[1][2],
+         m[1][0] * m[2][1] - m[1][1] * m[2][0], m[0][1] * m[2][0] - m[0][0] * m[2][1],
+         m[0][0] * m[1][1] - m[0][1] * m[1][0]]
+    det = _det33(m)
+    return [[c[3 * i + j] / det for j in range(3)] for i in range(3)]
+
+
+def contact_wave_correction(uA, OmegaA, B1A, B2A, uB, OmegaB, B1B, B2B, min1, min2):
+    """(det1, det2, successful, valueA, valueB) -- common.hpp:220-260."""
+    zero = [0.0] * 9
+    R1 = _mat_mul(B1A, OmegaA)
+    det1 = abs(_det33(R1))
+    if not det1 > min1:
+        return det1, 0.0, False, zero, zero
+    R = _invert33(R1)
+    b1B, b1A = _flat(_mat_mul(B1B, _col(uB))), _flat(_mat_mul(B1A, _col(uA)))
+    p = _flat(_mat_mul(R, _col([b1B[i] - b1A[i] for i in range(3)])))
+    Q = _mat_mul(R, _mat_mul(B1B, OmegaB))
+    B2OB, B2OA = _mat_mul(B2B, OmegaB), _mat_mul(B2A, OmegaA)
+    B2OAQ = _mat_mul(B2OA, Q)
+    A = [[B2OB[i][j] - B2OAQ[i][j] for j in range(3)] for i in range(3)]
+    t = _flat(_mat_mul(B2OA, _col(p)))
+    b2A, b2B = _flat(_mat_mul(B2A, _col(uA))), _flat(_mat_mul(B2B, _col(uB)))
+    f = [(t[i] + b2A[i]) - b2B[i] for i in range(3)]
+    det2 = abs(_det33(A))
+    if not det2 > min2:
+        return det1, det2, False, zero, zero
+    alphaB = list(_solve3(A, f))
+    Qa = _flat(_mat_mul(Q, _col(alphaB)))
+    alphaA = [p[i] + Qa[i] for i in range(3)]
+    return (det1, det2, True, _flat(_mat_mul(OmegaA, _col(alphaA))),
+            _flat(_mat_mul(OmegaB, _col(alphaB))))
+
+
+def _gsl_lu_decomp(A):
+    """gsl_linalg_LU_decomp: returns (LU, permutation, signum)."""
+    N = len(A)
+    A = [list(r) for r in A]
+    perm = list(range(N))
+    signum = 1
+    for j in range(N - 1):
+        mx, piv = abs(A[j][j]), j
+        for i in range(j + 1, N):
+            if abs(A[i][j]) > mx:
+                mx, piv = abs(A[i][j]), i
+        if piv != j:
+            A[j], A[piv] = A[piv], A[j]
+            perm[j], perm[piv] = perm[piv], perm[j]
+            signum = -signum
+        ajj = A[j][j]
+        if ajj != 0.0:
+            for i in range(j + 1, N):
+                aij = A[i][j] / ajj
+                A[i][j] = aij
+                for k in range(j + 1, N):
+                    A[i][k] = A[i][k] - aij * A[j][k]
+    return A, perm, signum
+
+
+def _gsl_lu_det(LU, signum):
+    det = float(signum)
+    for i in range(len(LU)):
+        det *= LU[i][i]
+    return det
+
+
+def _gsl_lu_solve(LU, perm, b):
+    N = len(LU)
+    x = [b[perm[i]] for i in range(N)]          # gsl_permute_vector
+    for i in range(1, N):                       # dtrsv lower, unit
+        t = x[i]
+        for j in range(i):
+            t -= LU[i][j] * x[j]
+        x[i] = t
+    x[N - 1] = x[N - 1] / LU[N - 1][N - 1]      # dtrsv upper, non-unit
+    for i in range(N - 2, -1, -1):
+        t = x[i]
+        for j in range(i + 1, N):
+            t -= LU[i][j] * x[j]
+        x[i] = t / LU[i][i]
+    return x
+
+
+def outer_wave_correction_gsl(u, Omega, B, b, min_valid):
+    """The one-body calculateOuterWaveCorrection (common.hpp:179-197) for N > 3."""
+    M = _mat_mul(B, Omega)
+    LU, perm, sg = _gsl_lu_decomp(M)
+    det = abs(_gsl_lu_det(LU, sg))
+    if not det > min_valid:
+        return det, False, [0.0] * 9
+    Bu = _flat(_mat_mul(B, _col(u)))
+    alpha = _gsl_lu_solve(LU, perm, [b[i] - Bu[i] for i in range(len(b))])
+    return det, True, _flat(_mat_mul(Omega, _col(alpha)))
+
+
+def _sigma_local(u, S):
+    sg = [[u[_sym(i, j)] for j in range(3)] for i in range(3)]
+    ST = [[S[j][i] for j in range(3)] for i in range(3)]
+    return _mat_mul(_mat_mul(ST, sg), S)
+
+
+def _sigma_global(u, S, sl):
+    ST = [[S[j][i] for j in range(3)] for i in range(3)]
+    sg = _mat_mul(_mat_mul(S, sl), ST)
+    for i in range(3):
+        for j in range(3):
+            u[_sym(i, j)] = sg[i][j]
+
+
+def plain_contact_average(uA, uB, normal):  # ElasticModel.hpp:239-272
+    uA, uB = list(uA), list(uB)
+    v = [(uA[i] + uB[i]) / 2 for i in range(3)]
+    uA[:3], uB[:3] = v, list(v)
+    S = local_basis(normal)
+    lA, lB = _sigma_local(uA, S), _sigma_local(uB, S)
+    sn = [(lA[i][2] + lB[i][2]) / 2 for i in range(3)]
+    for l in (lA, lB):
+        for i in range(3):
+            l[i][2] = sn[i]
+        for j in range(3):
+            l[2][j] = sn[j]
+    _sigma_global(uA, S, lA)
+    _sigma_global(uB, S, lB)
+    return uA, uB
+
+
+def plain_contact_one_sided(uA, uB, normal):  # ElasticModel.hpp:279-300
+    uA = list(uA)
+    uA[:3] = uB[:3]
+    S = local_basis(normal)
+    lA, lB = _sigma_local(uA, S), _sigma_local(uB, S)
+    sn = [lB[i][2] for i in range(3)]
+    for i in range(3):
+        lA[i][2] = sn[i]
+    for j in range(3):
+        lA[2][j] = sn[j]
+    _sigma_global(uA, S, lA)
+    return uA
+
+
+class MultiEngine:
+    """simplex::Engine<3> with several bodies of one triangulation and ADHESION
+    contacts between them (engine/simplex/Engine.cpp:14-48, 95-287).
+
+    bodies: list (ascending ids) of dicts {"id", "coords", "cells", "global" (local ->
+    triangulation vertex), "U", "U1", "L", "pde"} -- the mesh is input data."""
+
+    def __init__(self, bodies, basis, courant, border_conditions=()):
+        faces = {}
+        for b in bodies:
+            for c in b["cells"]:
+                for i in range(4):
+                    f = tuple(sorted(int(b["global"][c[(i + k) % 4]]) for k in (1, 2, 3)))
+                    faces.setdefault(f, []).append(int(b["id"]))
+        empty_vertices = set()
+        face_grids = []
+        for b in bodies:
+            glob = [int(x) for x in b["global"]]
+            g0 = Grid(b["coords"], b["cells"])  # topology only
+            fg = {}
+            for ci, c in enumerate(g0.cells):
+                for i in range(4):
+                    if g0.nb[ci][i] < 0:
+                        f = tuple(sorted(glob[c[(i + k) % 4]] for k in (1, 2, 3)))
+                        others = [x for x in faces[f] if x != int(b["id"])]
+                        fg[(ci, i)] = others[0] if others else EMPTY
+                        if not others:
+                            empty_vertices.update(f)
+            face_grids.append(fg)
+        owners = {}
+        for b in bodies:
+            for g in b["global"]:
+                owners.setdefault(int(g), set()).add(int(b["id"]))
+        self.bodies = []
+        grids = []
+        for b, fg in zip(bodies, face_grids):
+            glob = [int(x) for x in b["global"]]
+            other = []
+            for g in glob:
+                o = sorted(owners[g] - {int(b["id"])})
+                if g in empty_vertices:
+                    o = [EMPTY] + o
+                other.append(o)
+            grids.append(Grid(b["coords"], b["cells"], lambda ci, i, fg=fg: fg[(ci, i)], other))
+        tau = None
+        for b, g in zip(bodies, grids):   # Engine::estimateTimeStep: minimal over bodies
+            mx = max(abs(float(x)) for s in range(3) for x in b["L"][s])
+            t = courant * g.average_height / mx
+            tau = t if tau is None or t < tau else tau
+        self.tau = tau
+        for b, g in zip(bodies, grids):
+            self.bodies.append(Engine(b["coords"], b["cells"], b["U"], b["U1"], b["L"], basis,
+                                      courant, b["pde"], border_conditions, grid=g, tau=tau))
+        self.ids = [int(b["id"]) for b in bodies]
+        self.globals = [[int(x) for x in b["global"]] for b in bodies]
+        self.basis = [[float(basis[r][c]) for c in range(3)] for r in range(3)]
+        self.contacts = []
+        for ia in range(len(bodies)):       # Utils::makePairs + addContactNode
+            for ib in range(ia + 1, len(bodies)):
+                self.contacts.append(self._contact(ia, ib))
+        self.time = 0.0
+        for c in self.contacts:             # applyPlainBorderContactCorrection(0)
+            self._plain(c)
+        # (each body's Engine already applied its border plain correction at t = 0)
+
+    def _contact(self, ia, ib):
+        A, B = self.bodies[ia], self.bodies[ib]
+        la = {g: i for i, g in enumerate(self.globals[ia])}
+        lb = {g: i for i, g in enumerate(self.globals[ib])}
+        pairs = []
+        for g in sorted(set(la) & set(lb)):
+            a, b = la[g], lb[g]
+            if A.grid.other_grids[a] != [self.ids[ib]]:
+                continue
+            n = A.grid.contact_normal(a, self.ids[ib])
+            if n != (0.0, 0.0, 0.0):
+                pairs.append((a, b, n))
+        min_det = {}
+        if pairs:                            # getMaximalPossibleDeterminants (hpp:250-276)
+            for s in range(3):
+                d = (self.basis[0][s], self.basis[1][s], self.basis[2][s])
+                B1, B2 = _b1_global(), _b2_global(d)
+                d1, d2, ok, _, _ = contact_wave_correction(
+                    [0.0] * 9, A._omega(s, LEFT), B1, B2, [0.0] * 9, B._omega(s, RIGHT), B1, B2, 0, 0)
+                if not (ok and d1 > 0 and d2 > 0):
+                    raise ValueError("degenerate contact system")
+                min_det[s] = (1e-3 * d1, 1e-3 * d2)
+        return {"a": ia, "b": ib, "pairs": pairs, "min_det": min_det}
+
+    def _plain(self, c):
+        A, B = self.bodies[c["a"]], self.bodies[c["b"]]
+        for a, b, n in c["pairs"]:
+            A.u[a], B.u[b] = plain_contact_average(A.u[a], B.u[b], n)
+
+    def _correct(self, c, s):
+        """ContactCorrectorInRiemannInvariants::applyInGlobalBasis (hpp:333-348)."""
+        A, B = self.bodies[c["a"]], self.bodies[c["b"]]
+        min1, min2 = c["min_det"].get(s, (0.0, 0.0))
+        both = sorted(LEFT + RIGHT)
+        for a, b, n in c["pairs"]:
+            oa, ob = list(A.outers[s].get(a, [])), list(B.outers[s].get(b, []))
+            N = (len(oa) + len(ob)) // 3    # matchInnersAndOuters (hpp:365-397)
+            if N % 2 == 1:
+                if N == 3:
+                    oa, ob = list(both), list(both)
+                elif not oa:
+                    oa = RIGHT if ob == LEFT else LEFT
+                else:
+                    ob = RIGHT if oa == LEFT else LEFT
+                for i in oa:
+                    A.wn[a][i] = 0
+                for i in ob:
+                    B.wn[b][i] = 0
+            uA = A._mat_vec(A.U1[s], A.wn[a])
+            uB = B._mat_vec(B.U1[s], B.wn[b])
+            B1, B2 = _b1_global(), _b2_global(n)
+            if len(oa) == 3 and len(ob) == 3:
+                _, _, ok, vA, vB = contact_wave_correction(uA, A._omega(s, oa), B1, B2,
+                                                           uB, B._omega(s, ob), B1, B2, min1, min2)
+                if ok:
+                    uA = [uA[i] + vA[i] for i in range(9)]
+                    uB = [uB[i] + vB[i] for i in range(9)]
+                else:
+                    uA, uB = plain_contact_average(uA, uB, n)
+            elif (len(oa) == 6 and not ob) or (len(ob) == 6 and not oa):
+                X, uX, uY = (A, uA, uB) if oa else (B, uB, uA)
+                Bm = B1 + B2
+                b12 = _flat(_mat_mul(B1, _col(uY))) + _flat(_mat_mul(B2, _col(uY)))
+                Om = [X._omega(s, RIGHT)[i] + X._omega(s, LEFT)[i] for i in range(9)]
+                _, ok, v = outer_wave_correction_gsl(uX, Om, Bm, b12, min1)
+                uX = [uX[i] + v[i] for i in range(9)] if ok else plain_contact_one_sided(uX, uY, n)
+                if oa:
+                    uA = uX
+                else:
+                    uB = uX
+            else:
+                r1 = contact_wave_correction(uA, A._omega(s, RIGHT), B1, B2,
+                                             uB, B._omega(s, LEFT), B1, B2, min1, min2)
+                r2 = contact_wave_correction(uA, A._omega(s, LEFT), B1, B2,
+                                             uB, B._omega(s, RIGHT), B1, B2, min1, min2)
+                if r1[2] and r2[2]:
+                    uA = [uA[i] + (r1[3][i] + r2[3][i]) / 2 for i in range(9)]
+                    uB = [uB[i] + (r1[4][i] + r2[4][i]) / 2 for i in range(9)]
+                else:
+                    uA, uB = plain_contact_average(uA, uB, n)
+            A.wn[a] = A._mat_vec(A.U[s], uA)
+            B.wn[b] = B._mat_vec(B.U[s], uB)
+
+    def step(self):
+        """simplex::Engine::nextTimeStep (Engine.cpp:95-116)."""
+        t_next = self.time + self.tau
+        for c in self.contacts:
+            self._plain(c)
+        for e in self.bodies:
+            e._plain_correction(t_next)
+        for s in range(3):
+            for e in self.bodies:
+                e.stage_nodes(s)
+            for c in self.contacts:
+                self._correct(c, s)
+            for e in self.bodies:
+                e.stage_finish(s, t_next)
+        self.time = self.time + self.tau
+        for e in self.bodies:
+            e.time = self.time

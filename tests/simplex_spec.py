@@ -78,3 +78,41 @@ def fracture_task(n=(16, 16, 8), courant=1.0, jitter=0.1, seed=7, border=None, s
     for area, kind, values, multi in (FREE_BORDER if border is None else border):
         t.add_simplex_border_condition(area, kind, list(values), multi)
     return t
+
+
+# Two layers of different isotropic-elastic materials glued by an ADHESION
+# contact (ContactCorrectorInRiemannInvariants), free surface outside: per-cell
+# body ids by cell centroid (z > 0.5 -> body 1), as the INM mesher assigns them.
+LAYER_MATERIALS = {0: (4.0, 2.0, 1.0), 1: (2.0, 1.0, 0.5)}
+
+
+def layered_task(n=6, courant=1.0, jitter=0.1, seed=7, border=None, snaps=3,
+                 materials=LAYER_MATERIALS, cavity=False):
+    from gcm_amd import _gcm_host as H
+    t = H.Task()
+    t.dimensionality = 3
+    t.grid = "SIMPLEX"
+    t.courant = courant
+    t.number_of_snaps = snaps
+    for i, (rho, lam, mu) in sorted(materials.items()):
+        t.add_body(i, [1, 1, 1], [0, 0, 0])
+        t.set_body_material(i, rho, lam, mu)
+    t.calculation_basis = [1, 0, 0, 0, 1, 0, 0, 0, 1]
+    t.set_simplex_box([n, n, n], [0, 0, 0], [1, 1, 1], jitter, seed)
+    t.add_simplex_body_area(("box", (-1, -1, 0.5), (2, 2, 2)), 1)
+    t.set_contact_condition("ADHESION")
+    t.add_initial_quantity(("sphere", 0.3, (0.5, 0.5, 0.3)), "PRESSURE", 1.0)
+    t.add_initial_vector(("box", (0.2, 0.2, 0.55), (0.8, 0.8, 0.9)),
+                         [0.1, -0.2, 0.3, 0.0, 0.05, 0.0, 0.0, 0.0, 0.0])
+    for area, kind, values, multi in (FREE_BORDER if border is None else border):
+        t.add_simplex_border_condition(area, kind, list(values), multi)
+    return t
+
+
+def oracle_multi(plans, courant, border=FREE_BORDER, materials=LAYER_MATERIALS):
+    bodies = []
+    for b in plans["bodies"]:
+        U, U1, L = O.isotropic_elastic_matrices(3, *materials[int(b["id"])])
+        bodies.append({"id": b["id"], "coords": b["coords"], "cells": b["cells"],
+                       "global": b["global"], "U": U, "U1": U1, "L": L, "pde": b["pde"]})
+    return S.MultiEngine(bodies, np.eye(3), courant, oracle_conditions(border))

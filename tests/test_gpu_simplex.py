@@ -87,3 +87,32 @@ def test_fracture_layer_matches_oracle(H, courant, steps):
     got, want = e.pde(), np.array(o.u)
     assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"
     assert np.abs(got).max() > 0
+
+
+from tests.simplex_spec import layered_task, oracle_multi  # noqa: E402
+
+
+@pytest.mark.parametrize("n,courant,steps,border", [(6, 1.0, 3, None), (6, 1.7, 2, None),
+                                                    (5, 1.3, 2, MIXED_BORDER)],
+                         ids=["c1", "c1.7", "mixed-c1.3"])
+def test_layered_adhesion_contact_matches_oracle(H, n, courant, steps, border):
+    """Two bodies of different materials glued by ADHESION: the contact correctors
+    (the 3 + 3 system, the 6 x 6 GSL system of a one-sided node and the averaged
+    pair) between the bodies' node and inner phases, the plain contact correction
+    at every step, border correctors on the outer surface: GPU == oracle bitwise."""
+    t = layered_task(n, courant, border=border)
+    p = H.simplex_plans(t)
+    e = H.SimplexEngine(t)
+    assert e.number_of_bodies == 2 and e.time_step == p["tau"]
+    o = oracle_multi(p, courant, border=border if border is not None else FREE_BORDER)
+    e.run_steps(steps)
+    for _ in range(steps):
+        o.step()
+    for i in range(2):
+        got, want = e.pde(i), np.array(o.bodies[i].u)
+        assert np.array_equal(got, want), f"body {i}: {int((got != want).sum())} values differ"
+    # adhesion holds at the contact nodes: equal velocities across the contact
+    c = p["contacts"][0]
+    va, vb = e.pde(0)[c["nodes_a"], :3], e.pde(1)[c["nodes_b"], :3]
+    assert np.abs(va).max() > 0
+    assert np.abs(va - vb).max() <= 1e-12 * max(1.0, np.abs(va).max())

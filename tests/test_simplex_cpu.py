@@ -259,3 +259,80 @@ def test_fracture_plans_match_oracle(H, courant):
                 if f[0] == "cell":
                     assert list(st["v"][it, k]) == list(f[1])
     assert len(e.corrected) == len(p["border_plan"]["nodes"])
+
+
+# ---- two bodies, ADHESION contact correctors ---------------------------------
+
+from tests.simplex_spec import LAYER_MATERIALS, layered_task, oracle_multi  # noqa: E402
+
+
+@pytest.mark.parametrize("n,courant", [(5, 1.0), (6, 1.7)])
+def test_layered_contact_plans_match_oracle(H, n, courant):
+    """Body meshes, node states, time step, contact node pairs and normals, and the
+    per-stage wave codes after matchInnersAndOuters: product == oracle."""
+    p = H.simplex_plans(layered_task(n, courant))
+    o = oracle_multi(p, courant)
+    assert o.tau == p["tau"]
+    assert len(p["bodies"]) == 2 and len(p["contacts"]) == 1
+    for b, e in zip(p["bodies"], o.bodies):
+        g = e.grid
+        assert g.inner_idx == list(b["inner"]) and g.border_idx == list(b["border"])
+        assert g.contact_idx == list(b["contact"]) and len(b["contact"]) > 0
+        assert [x[0] for x in e.corrected] == list(b["border_plan"]["nodes"])
+        assert np.array_equal(np.array([x[2] for x in e.corrected]).ravel(),
+                              np.array(b["border_plan"]["normal"]))
+        U, U1, _ = O.isotropic_elastic_matrices(3, *LAYER_MATERIALS[int(b["id"])])
+        assert np.array_equal(U1, b["U1"])
+    c, oc = p["contacts"][0], o.contacts[0]
+    assert list(c["nodes_a"]) == [x[0] for x in oc["pairs"]]
+    assert list(c["nodes_b"]) == [x[1] for x in oc["pairs"]]
+    assert np.array_equal(np.array(c["normal"]), np.array([x[2] for x in oc["pairs"]]).ravel())
+    assert c["min_det"] == [oc["min_det"][s][k] for s in range(3) for k in range(2)]
+    nn = len(c["nodes_a"])
+    code = {(): 0, (1, 3, 5): 1, (0, 2, 4): 2, (0, 1, 2, 3, 4, 5): 3}
+    size = {0: 0, 1: 3, 2: 3, 3: 6}
+
+    def match(ca, cb):  # matchInnersAndOuters (ContactCorrector.hpp:365-397)
+        N = (size[ca] + size[cb]) // 3
+        if N % 2 == 0:
+            return ca, cb
+        if N == 3:
+            return 3 | 4, 3 | 4
+        if ca == 0:
+            return (1 if cb == 2 else 2) | 4, cb | 4
+        return ca | 4, (1 if ca == 2 else 2) | 4
+
+    A, B = o.bodies
+    for s in range(3):
+        for i, (a, b, _) in enumerate(oc["pairs"]):
+            want = match(code[tuple(A.outers[s].get(a, []))], code[tuple(B.outers[s].get(b, []))])
+            assert (c["code_a"][s * nn + i], c["code_b"][s * nn + i]) == want
+    # branch coverage of the configuration: the 3+3 system and the 6 x 6 (GSL) one
+    codes = {(c["code_a"][k] & 3, c["code_b"][k] & 3) for k in range(3 * nn)}
+    assert any(x in codes for x in [(1, 2), (2, 1)])
+    assert any(x in codes for x in [(3, 0), (0, 3)])
+
+
+def test_gsl_lu_restatement():
+    """The oracle's GSL LU (determinant, solve) against numpy on random 6 x 6 systems."""
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        A = rng.standard_normal((6, 6))
+        b = rng.standard_normal(6)
+        LU, perm, sg = S._gsl_lu_decomp(A.tolist())
+        assert abs(S._gsl_lu_det(LU, sg) - np.linalg.det(A)) < 1e-9 * abs(np.linalg.det(A)) + 1e-12
+        x = S._gsl_lu_solve(LU, perm, b.tolist())
+        assert np.allclose(A @ np.array(x), b, atol=1e-9)
+
+
+def test_plain_contact_average_satisfies_adhesion():
+    """applyPlainContactCorrectionAsAverage: equal velocities and equal normal
+    tractions afterwards."""
+    rng = np.random.default_rng(5)
+    n = np.array([0.3, -0.4, 0.866])
+    n = n / np.linalg.norm(n)
+    uA, uB = S.plain_contact_average(rng.standard_normal(9).tolist(), rng.standard_normal(9).tolist(),
+                                     tuple(n))
+    sig = lambda u: np.array([[u[3], u[4], u[5]], [u[4], u[6], u[7]], [u[5], u[7], u[8]]])
+    assert np.allclose(uA[:3], uB[:3])
+    assert np.allclose(sig(uA) @ n, sig(uB) @ n)
