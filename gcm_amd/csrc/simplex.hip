@@ -11,7 +11,10 @@
 //   k_sx_nodes(inner)     innerStage (hpp:98-112) -- space-time feet read the border
 //                         nodes' new invariants written by the previous launch
 //   k_sx_transform(U1_s)  afterStage: u_new = U1_s w_new (hpp:115-126), then swap.
-// Storage is SoA: component c of node n at [c * N + n]; gradients [r][c][n].
+// Layers u, un and the new invariants wn are SoA (component c of node n at
+// [c * N + n]); the invariants w of beforeStage, their gradients and the
+// coordinates are node-major (w[n][9], grad[n][3][6], coords[n][3]) because the
+// gradient and node kernels gather them per neighbour / per cell vertex.
 // Arithmetic follows the reference expression by expression (-ffp-contract=off).
 #include <hip/hip_runtime.h>
 
@@ -55,8 +58,19 @@ struct BorderDev {
 	bool set = false, valuesSet = false;
 };
 
+struct StageShift {  // crossingPoints' shift of every invariant: direction * (-tau L(k))
+	double d[6][3];
+};
+
+// Feet in a compact, coalesced layout ([k][n]): fv = the cell's (or face's)
+// vertices, flam = barycentric weights, fmeta = kind | slot(i) << (4 + 4 i).  The
+// foot point of a CELL foot is recomputed as coords[n] + shift[k], the same IEEE
+// sum the host's plan made (gsx_set_stage_plan checks it).
 struct StageDev {
-	gsx_foot* feet = nullptr;
+	int4* fv = nullptr;
+	double4* flam = nullptr;
+	int* fmeta = nullptr;
+	StageShift shift{};
 	int* border = nullptr;
 	int* inner = nullptr;
 	int nBorder = 0, nInner = 0;
@@ -68,6 +82,7 @@ struct StageDev {
 struct gsx_ctx {
 	int device = 0, N = 0;
 	hipStream_t stream = nullptr;
+	std::vector<double> hostCoords;  // [n][3]
 	double *coords = nullptr, *u = nullptr, *un = nullptr, *w = nullptr, *wn = nullptr,
 	       *grad = nullptr;
 	double* mats = nullptr;  // [2][3][81]: U then U1
@@ -91,7 +106,10 @@ struct gsx_contact {
 
 namespace {
 
-// out[c] = M(c,0) in[0] + sum_{j>=1} M(c,j) in[j]  (linal/operators.hpp:109-123)
+// out[c] = M(c,0) in[0] + sum_{j>=1} M(c,j) in[j]  (linal/operators.hpp:109-123).
+// AOS_OUT: the invariants of beforeStage are written node-major ([n][9]) because
+// the gradient and node kernels gather them per neighbour / per cell vertex.
+template <bool AOS_OUT>
 __global__ __launch_bounds__(256) void k_sx_transform(const double* __restrict__ in,
                                                       double* __restrict__ out,
                                                       const double* __restrict__ Mx, int N) {
@@ -105,7 +123,8 @@ __global__ __launch_bounds__(256) void k_sx_transform(const double* __restrict__
 		double s = Mx[c * kM + 0] * v[0];
 #pragma unroll
 		for (int j = 1; j < kM; j++) s += Mx[c * kM + j] * v[j];
-		out[c * N + n] = s;
+		if (AOS_OUT) out[(size_t)n * kM + c] = s;
+		else out[c * N + n] = s;
 	}
 }
 
@@ -117,44 +136,66 @@ __device__ __forceinline__ double det3(double m11, double m12, double m13, doubl
 
 // linearLeastSquares(A, b, W) = solve(A^T W A, A^T (W b)) per component, with
 // transposeMultiply's order (first term, then +=) over all kMaxNb rows: the
-// unused rows are zero rows and add +0.
+// unused rows are zero rows and add +0.  Neighbour-outer loop: each neighbour's
+// weight and its invariants (one node-major record) are read once; every
+// component still sums its terms in neighbour order.  The LSQ row is the same
+// IEEE difference coords[neighbour] - coords[node] the host plan made
+// (gsx_set_gradient_plan checks it).  Only invariants 0..5 get gradients: the
+// zero-eigenvalue invariants 6..8 are exact hits and never interpolated
+// (hpp:166-170).  w is node-major [n][9], grad [n][3][6].
+constexpr int kG = 6;
 __global__ __launch_bounds__(256) void k_sx_gradient(const double* __restrict__ w,
                                                      double* __restrict__ grad,
                                                      const int* __restrict__ off,
                                                      const int* __restrict__ nbs,
-                                                     const double* __restrict__ rows,
+                                                     const double* __restrict__ coords,
                                                      const double* __restrict__ wts,
                                                      const double* __restrict__ Mm,
                                                      const double* __restrict__ dets, int N) {
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
 	if (n >= N) return;
 	const int b0 = off[n], K = off[n + 1] - b0;
-	const double* M = Mm + 9 * n;
-	const double det = dets[n];
-	for (int c = 0; c < kM; c++) {
-		const double wc = w[c * N + n];
-		double r0 = 0, r1 = 0, r2 = 0;
-		for (int i = 0; i < K; i++) {
-			const int e = b0 + i;
-			const double bi = w[c * N + nbs[e]] - wc;  // b(i) = pde(neighbor) - pde(it)
-			const double wb = wts[e] * bi;             // (W * b)(i)
-			const double t0 = rows[3 * e + 0] * wb, t1 = rows[3 * e + 1] * wb,
-			             t2 = rows[3 * e + 2] * wb;
+	double wc[kG], r0[kG], r1[kG], r2[kG];
+#pragma unroll
+	for (int c = 0; c < kG; c++) wc[c] = w[(size_t)n * kM + c];
+	const double x0 = coords[3 * (size_t)n], x1 = coords[3 * (size_t)n + 1],
+	             x2 = coords[3 * (size_t)n + 2];
+	for (int i = 0; i < K; i++) {
+		const int e = b0 + i;
+		const int nb = nbs[e];
+		const double* wn = w + (size_t)nb * kM;
+		const double a0 = coords[3 * (size_t)nb] - x0, a1 = coords[3 * (size_t)nb + 1] - x1,
+		             a2 = coords[3 * (size_t)nb + 2] - x2;
+		const double we = wts[e];
+#pragma unroll
+		for (int c = 0; c < kG; c++) {
+			const double bi = wn[c] - wc[c];  // b(i) = pde(neighbor) - pde(it)
+			const double wb = we * bi;        // (W * b)(i)
+			const double t0 = a0 * wb, t1 = a1 * wb, t2 = a2 * wb;
 			if (i == 0) {
-				r0 = t0; r1 = t1; r2 = t2;
+				r0[c] = t0; r1[c] = t1; r2[c] = t2;
 			} else {
-				r0 += t0; r1 += t1; r2 += t2;
+				r0[c] += t0; r1[c] += t1; r2[c] += t2;
 			}
 		}
+	}
+	const double* M = Mm + 9 * (size_t)n;
+	const double det = dets[n];
+	const double m0 = M[0], m1 = M[1], m2 = M[2], m3 = M[3], m4 = M[4], m5 = M[5], m6 = M[6],
+	             m7 = M[7], m8 = M[8];
+	double* g = grad + (size_t)n * 3 * kG;
+#pragma unroll
+	for (int c = 0; c < kG; c++) {
+		double y0 = r0[c], y1 = r1[c], y2 = r2[c];
 		if (K < kMaxNb) {  // the zero rows: 0 * (0 * 0) = +0
-			r0 += 0.0; r1 += 0.0; r2 += 0.0;
+			y0 += 0.0; y1 += 0.0; y2 += 0.0;
 		}
-		const double d1 = det3(r0, M[1], M[2], r1, M[4], M[5], r2, M[7], M[8]);
-		const double d2 = det3(M[0], r0, M[2], M[3], r1, M[5], M[6], r2, M[8]);
-		const double d3 = det3(M[0], M[1], r0, M[3], M[4], r1, M[6], M[7], r2);
-		grad[(0 * kM + c) * N + n] = d1 / det;
-		grad[(1 * kM + c) * N + n] = d2 / det;
-		grad[(2 * kM + c) * N + n] = d3 / det;
+		const double d1 = det3(y0, m1, m2, y1, m4, m5, y2, m7, m8);
+		const double d2 = det3(m0, y0, m2, m3, y1, m5, m6, y2, m8);
+		const double d3 = det3(m0, m1, y0, m3, m4, y1, m6, m7, y2);
+		g[0 * kG + c] = d1 / det;
+		g[1 * kG + c] = d2 / det;
+		g[2 * kG + c] = d3 / det;
 	}
 }
 
@@ -163,7 +204,9 @@ __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ?
 
 // interpolateValuesAround (hpp:156-198) for the listed nodes, feet resolved on the host.
 __global__ __launch_bounds__(256) void k_sx_nodes(const int* __restrict__ nodes, int count,
-                                                  const gsx_foot* __restrict__ feet,
+                                                  const int4* __restrict__ fv,
+                                                  const double4* __restrict__ flam,
+                                                  const int* __restrict__ fmeta, StageShift sh,
                                                   const double* __restrict__ coords,
                                                   const double* __restrict__ w,
                                                   const double* __restrict__ grad,
@@ -171,43 +214,57 @@ __global__ __launch_bounds__(256) void k_sx_nodes(const int* __restrict__ nodes,
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int n = nodes[t];
+	const double x0 = coords[3 * (size_t)n + 0], x1 = coords[3 * (size_t)n + 1],
+	             x2 = coords[3 * (size_t)n + 2];
 	for (int k = 0; k < kM; k++) {
 		double ans;
 		if (k >= 6) {
-			ans = w[k * N + n];  // dx(k) == 0: exact hit (hpp:166-170)
+			ans = w[(size_t)n * kM + k];  // dx(k) == 0: exact hit (hpp:166-170)
 		} else {
-			const gsx_foot& f = feet[(size_t)n * 6 + k];
-			if (f.kind == GSX_FOOT_CELL) {
+			const size_t e = (size_t)k * N + n;
+			const int meta = fmeta[e];
+			const int kind = meta & 15;
+			if (kind == GSX_FOOT_CELL) {
 				// TetrahedronInterpolator::hybridInterpolate (hpp:93-104)
+				const int4 fvv = fv[e];
+				const double4 l = flam[e];
+				const int vs[4] = {fvv.x, fvv.y, fvv.z, fvv.w};
+				const double lam[4] = {l.x, l.y, l.z, l.w};
+				const double q0 = x0 + sh.d[k][0], q1 = x1 + sh.d[k][1], q2 = x2 + sh.d[k][2];
 				double v[4], term[4];
 #pragma unroll
 				for (int i = 0; i < 4; i++) {
-					const int p = f.v[i];
-					v[i] = w[k * N + p];
-					const double d0 = f.q[0] - coords[0 * N + p];
-					const double d1 = f.q[1] - coords[1 * N + p];
-					const double d2 = f.q[2] - coords[2 * N + p];
-					double dot = grad[(0 * kM + k) * N + p] * d0;
-					dot += grad[(1 * kM + k) * N + p] * d1;
-					dot += grad[(2 * kM + k) * N + p] * d2;
+					const int p = vs[i];
+					v[i] = w[(size_t)p * kM + k];
+					const double d0 = q0 - coords[3 * (size_t)p + 0];
+					const double d1 = q1 - coords[3 * (size_t)p + 1];
+					const double d2 = q2 - coords[3 * (size_t)p + 2];
+					const double* gp = grad + (size_t)p * 3 * kG;
+					double dot = gp[0 * kG + k] * d0;
+					dot += gp[1 * kG + k] * d1;
+					dot += gp[2 * kG + k] * d2;
 					term[i] = v[i] + dot / 2.0;
 				}
 				const double quadratic =
-				    f.lam[0] * term[0] + f.lam[1] * term[1] + f.lam[2] * term[2] + f.lam[3] * term[3];
+				    lam[0] * term[0] + lam[1] * term[1] + lam[2] * term[2] + lam[3] * term[3];
 				const double mn = std_min(std_min(std_min(v[0], v[1]), v[2]), v[3]);
 				const double mx = std_max(std_max(std_max(v[0], v[1]), v[2]), v[3]);
 				const double limited = std_min(std_max(quadratic, mn), mx);
 				ans = (quadratic == limited)
 				          ? quadratic
-				          : f.lam[0] * v[0] + f.lam[1] * v[1] + f.lam[2] * v[2] + f.lam[3] * v[3];
-			} else if (f.kind == GSX_FOOT_SPACETIME) {
+				          : lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
+			} else if (kind == GSX_FOOT_SPACETIME) {
+				const int4 fvv = fv[e];
+				const double4 l = flam[e];
+				const int vs[3] = {fvv.x, fvv.y, fvv.z};
+				const double lam[4] = {l.x, l.y, l.z, l.w};
 				double val[4];
 #pragma unroll
 				for (int i = 0; i < 4; i++) {
-					const int s = f.slot[i];
-					val[i] = (s < 3) ? w[k * N + f.v[s]] : wn[k * N + f.v[s - 3]];
+					const int s = (meta >> (4 + 4 * i)) & 15;
+					val[i] = (s < 3) ? w[(size_t)vs[s] * kM + k] : wn[k * N + vs[s - 3]];
 				}
-				ans = f.lam[0] * val[0] + f.lam[1] * val[1] + f.lam[2] * val[2] + f.lam[3] * val[3];
+				ans = lam[0] * val[0] + lam[1] * val[1] + lam[2] * val[2] + lam[3] * val[3];
 			} else {
 				ans = 0.0;  // outer invariant / walk ended on a vertex
 			}
@@ -527,13 +584,11 @@ gcmx_status gsx_create(int device, int n_nodes, const double* coords, gsx_ctx** 
 	SX_TRY(hipSetDevice(device));
 	SX_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
 	const size_t N = (size_t)n_nodes;
-	std::vector<double> soa(3 * N);
-	for (size_t n = 0; n < N; n++)
-		for (int r = 0; r < 3; r++) soa[r * N + n] = coords[3 * n + r];
-	gcmx_status s = upload(&c->coords, soa.data(), 3 * N);
+	c->hostCoords.assign(coords, coords + 3 * N);
+	gcmx_status s = upload(&c->coords, coords, 3 * N);  // node-major [n][3]
 	if (s) { gsx_destroy(c); return s; }
 	double** bufs[5] = {&c->u, &c->un, &c->w, &c->wn, &c->grad};
-	const size_t sizes[5] = {kM * N, kM * N, kM * N, kM * N, 3 * kM * N};
+	const size_t sizes[5] = {kM * N, kM * N, kM * N, kM * N, 3 * 6 * N};
 	for (int i = 0; i < 5; i++) {
 		if (hipMalloc(bufs[i], sizes[i] * sizeof(double)) != hipSuccess ||
 		    hipMemset(*bufs[i], 0, sizes[i] * sizeof(double)) != hipSuccess) {
@@ -557,7 +612,9 @@ void gsx_destroy(gsx_ctx* c) {
 	for (void* p : bptrs)
 		if (p) (void)hipFree(p);
 	for (auto& st : c->st) {
-		if (st.feet) (void)hipFree(st.feet);
+		if (st.fv) (void)hipFree(st.fv);
+		if (st.flam) (void)hipFree(st.flam);
+		if (st.fmeta) (void)hipFree(st.fmeta);
 		if (st.border) (void)hipFree(st.border);
 		if (st.inner) (void)hipFree(st.inner);
 	}
@@ -583,51 +640,78 @@ gcmx_status gsx_set_gradient_plan(gsx_ctx* c, const int* off, const int* nbs, co
                                   const double* wts, const double* M, const double* det) {
 	gcmx_status s = check(c);
 	if (s) return s;
-	if (!off || !M || !det) return fail(GCMX_ERR_INVALID_ARG, "null gradient plan");
+	if (!off || !nbs || !rows || !wts || !M || !det)
+		return fail(GCMX_ERR_INVALID_ARG, "null gradient plan");
 	const int N = c->N, E = off[N];
 	if (off[0] != 0 || E < 0) return fail(GCMX_ERR_INVALID_ARG, "bad gradient offsets");
 	for (int n = 0; n < N; n++) {
 		const int K = off[n + 1] - off[n];
 		if (K < 1 || K > kMaxNb) return fail(GCMX_ERR_INVALID_ARG, "1..20 neighbours per node expected");
 		if (!(det[n] != 0)) return fail(GCMX_ERR_INVALID_ARG, "singular gradient system");
+		for (int e = off[n]; e < off[n + 1]; e++) {
+			if (nbs[e] < 0 || nbs[e] >= N) return fail(GCMX_ERR_INVALID_ARG, "neighbour out of range");
+			// the device recomputes the LSQ row from the coordinates
+			for (int r = 0; r < 3; r++)
+				if (!(c->hostCoords[3 * (size_t)nbs[e] + r] - c->hostCoords[3 * (size_t)n + r] ==
+				      rows[3 * (size_t)e + r]))
+					return fail(GCMX_ERR_INVALID_ARG, "gradient row is not coords[nb] - coords[n]");
+		}
 	}
-	for (int e = 0; e < E; e++)
-		if (nbs[e] < 0 || nbs[e] >= N) return fail(GCMX_ERR_INVALID_ARG, "neighbour out of range");
 	SX_TRY(hipStreamSynchronize(c->stream));
 	if ((s = upload(&c->gOff, off, (size_t)N + 1)) || (s = upload(&c->gNb, nbs, (size_t)E)) ||
-	    (s = upload(&c->gRows, rows, 3 * (size_t)E)) || (s = upload(&c->gW, wts, (size_t)E)) ||
-	    (s = upload(&c->gM, M, 9 * (size_t)N)) || (s = upload(&c->gDet, det, (size_t)N)))
+	    (s = upload(&c->gW, wts, (size_t)E)) || (s = upload(&c->gM, M, 9 * (size_t)N)) ||
+	    (s = upload(&c->gDet, det, (size_t)N)))
 		return s;
 	c->gradSet = true;
 	return GCMX_OK;
 }
 
-gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, int nb,
-                               const int* border, int ni, const int* inner) {
+gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, const double* shift,
+                               int nb, const int* border, int ni, const int* inner) {
 	gcmx_status s = check(c);
 	if (s) return s;
-	if (stage < 0 || stage > 2 || !feet || nb < 0 || ni < 0 || (nb && !border) || (ni && !inner))
+	if (stage < 0 || stage > 2 || !feet || !shift || nb < 0 || ni < 0 || (nb && !border) ||
+	    (ni && !inner))
 		return fail(GCMX_ERR_INVALID_ARG, "bad stage plan");
 	const int N = c->N;
 	for (int i = 0; i < nb; i++)
 		if (border[i] < 0 || border[i] >= N) return fail(GCMX_ERR_INVALID_ARG, "node out of range");
 	for (int i = 0; i < ni; i++)
 		if (inner[i] < 0 || inner[i] >= N) return fail(GCMX_ERR_INVALID_ARG, "node out of range");
-	for (size_t e = 0; e < (size_t)N * 6; e++) {
-		const gsx_foot& f = feet[e];
-		const int nv = f.kind == GSX_FOOT_CELL ? 4 : f.kind == GSX_FOOT_SPACETIME ? 3 : 0;
-		if (f.kind < 0 || f.kind > 3) return fail(GCMX_ERR_INVALID_ARG, "bad foot kind");
-		for (int i = 0; i < nv; i++)
-			if (f.v[i] < 0 || f.v[i] >= N) return fail(GCMX_ERR_INVALID_ARG, "foot vertex out of range");
-		if (f.kind == GSX_FOOT_SPACETIME)
-			for (int i = 0; i < 4; i++)
-				if (f.slot[i] < 0 || f.slot[i] > 5) return fail(GCMX_ERR_INVALID_ARG, "bad slot");
-	}
+	std::vector<int4> fv((size_t)N * 6);
+	std::vector<double4> flam((size_t)N * 6);
+	std::vector<int> fmeta((size_t)N * 6);
+	for (int n = 0; n < N; n++)
+		for (int k = 0; k < 6; k++) {
+			const gsx_foot& f = feet[(size_t)n * 6 + k];
+			const int nv = f.kind == GSX_FOOT_CELL ? 4 : f.kind == GSX_FOOT_SPACETIME ? 3 : 0;
+			if (f.kind < 0 || f.kind > 3) return fail(GCMX_ERR_INVALID_ARG, "bad foot kind");
+			for (int i = 0; i < nv; i++)
+				if (f.v[i] < 0 || f.v[i] >= N) return fail(GCMX_ERR_INVALID_ARG, "foot vertex out of range");
+			int meta = f.kind;
+			if (f.kind == GSX_FOOT_SPACETIME)
+				for (int i = 0; i < 4; i++) {
+					if (f.slot[i] < 0 || f.slot[i] > 5) return fail(GCMX_ERR_INVALID_ARG, "bad slot");
+					meta |= f.slot[i] << (4 + 4 * i);
+				}
+			if (f.kind == GSX_FOOT_CELL)
+				for (int r = 0; r < 3; r++)
+					if (!(c->hostCoords[3 * (size_t)n + r] + shift[k * 3 + r] == f.q[r]))
+						return fail(GCMX_ERR_INVALID_ARG, "foot point is not node + shift");
+			const size_t e = (size_t)k * N + n;
+			fv[e] = make_int4(nv > 0 ? f.v[0] : 0, nv > 1 ? f.v[1] : 0, nv > 2 ? f.v[2] : 0,
+			                  nv > 3 ? f.v[3] : 0);
+			flam[e] = make_double4(f.lam[0], f.lam[1], f.lam[2], f.lam[3]);
+			fmeta[e] = meta;
+		}
 	SX_TRY(hipStreamSynchronize(c->stream));
 	StageDev& st = c->st[stage];
-	if ((s = upload(&st.feet, feet, (size_t)N * 6)) || (s = upload(&st.border, border, (size_t)nb)) ||
-	    (s = upload(&st.inner, inner, (size_t)ni)))
+	if ((s = upload(&st.fv, fv.data(), fv.size())) || (s = upload(&st.flam, flam.data(), flam.size())) ||
+	    (s = upload(&st.fmeta, fmeta.data(), fmeta.size())) ||
+	    (s = upload(&st.border, border, (size_t)nb)) || (s = upload(&st.inner, inner, (size_t)ni)))
 		return s;
+	for (int k = 0; k < 6; k++)
+		for (int r = 0; r < 3; r++) st.shift.d[k][r] = shift[k * 3 + r];
 	st.nBorder = nb;
 	st.nInner = ni;
 	st.set = true;
@@ -727,12 +811,13 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 	const int N = c->N;
 	const dim3 blk(256), grd((N + 255) / 256);
 	const StageDev& st = c->st[stage];
-	hipLaunchKernelGGL(k_sx_transform, grd, blk, 0, c->stream, c->u, c->w, c->mats + stage * 81, N);
+	hipLaunchKernelGGL(k_sx_transform<true>, grd, blk, 0, c->stream, c->u, c->w, c->mats + stage * 81, N);
 	hipLaunchKernelGGL(k_sx_gradient, grd, blk, 0, c->stream, c->w, c->grad, c->gOff, c->gNb,
-	                   c->gRows, c->gW, c->gM, c->gDet, N);
+	                   c->coords, c->gW, c->gM, c->gDet, N);
 	if (st.nBorder)
 		hipLaunchKernelGGL(k_sx_nodes, dim3((st.nBorder + 255) / 256), blk, 0, c->stream, st.border,
-		                   st.nBorder, st.feet, c->coords, c->w, c->grad, c->wn, N);
+		                   st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
+		                   c->wn, N);
 	SX_TRY(hipGetLastError());
 	return GCMX_OK;
 }
@@ -755,8 +840,9 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 	}
 	if (st.nInner)
 		hipLaunchKernelGGL(k_sx_nodes, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
-		                   st.nInner, st.feet, c->coords, c->w, c->grad, c->wn, N);
-	hipLaunchKernelGGL(k_sx_transform, grd, blk, 0, c->stream, c->wn, c->un,
+		                   st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
+		                   c->wn, N);
+	hipLaunchKernelGGL(k_sx_transform<false>, grd, blk, 0, c->stream, c->wn, c->un,
 	                   c->mats + 3 * 81 + stage * 81, N);
 	SX_TRY(hipGetLastError());
 	std::swap(c->u, c->un);

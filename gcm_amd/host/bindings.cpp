@@ -428,6 +428,11 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    .def("pde", &PySimplexEngine::pde, "current layer of a body [n_vertices, 9]",
 	         py::arg("body") = 0)
 	    .def_property_readonly("number_of_bodies", [](PySimplexEngine& p) { return p.e->numberOfBodies(); })
+	    .def_property_readonly("number_of_contact_pairs",
+	                           [](PySimplexEngine& p) { return p.e->numberOfContactPairs(); })
+	    .def("number_of_vertices", [](PySimplexEngine& p, size_t body) { return p.e->mesh(body).nVertices(); },
+	         py::arg("body") = 0)
+	    .def("sync", [](PySimplexEngine& p) { p.e->sync(); }, "wait for the bodies' streams")
 	    .def_property_readonly("steps", [](PySimplexEngine& p) { return p.e->stepsDone(); })
 	    .def_property_readonly("time_step", [](PySimplexEngine& p) { return p.e->timeStepValue(); })
 	    .def_property_readonly("required_time", [](PySimplexEngine& p) { return p.e->getRequiredTime(); });

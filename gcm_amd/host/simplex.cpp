@@ -696,6 +696,7 @@ StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[
 			const real dx = -tau * L[k];  // crossingPoints (common.hpp:46-52)
 			if (dx == 0) throw Exception("zero crossing point for a wave invariant");
 			const Real3 shift = mul(direction, dx);
+			for (int r = 0; r < 3; r++) plan.shift[k][r] = shift[r];
 			const Grid::Cell t = grid.findCellCrossedByTheRay(it, shift);
 			const Real3 q = add(m.v[it], shift);
 			if (t.n == 4) {
@@ -1065,7 +1066,7 @@ void uploadBody(gsx_ctx* ctx, const BodyPlans& p) {
 	          "gsx_set_gradient_plan");
 	for (int s = 0; s < 3; s++) {
 		const auto& st = p.stages[s];
-		gcmxCheck(gsx_set_stage_plan(ctx, s, st.feet.data(), (int)st.borderNodes.size(),
+		gcmxCheck(gsx_set_stage_plan(ctx, s, st.feet.data(), &st.shift[0][0], (int)st.borderNodes.size(),
 		                             st.borderNodes.data(), (int)st.innerNodes.size(),
 		                             st.innerNodes.data()),
 		          "gsx_set_stage_plan");
@@ -1105,6 +1106,7 @@ Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
 		                             cp.codeA.data(), cp.codeB.data(), &cp.minDet[0][0], &c),
 		          "gsx_contact_create");
 		contacts.push_back(c);
+		contactPairs += cp.nodesA.size();
 	}
 	// applyPlainBorderContactCorrection(Clock::Time()) (Engine.cpp:44)
 	setBorderValues(Clock::Time());
@@ -1147,6 +1149,12 @@ void Engine::nextTimeStep() {
 		for (auto& b : bodies) gcmxCheck(gsx_stage_finish(b.ctx, stage), "gsx_stage_finish");
 	}
 }
+
+void Engine::sync() const {
+	for (const auto& b : bodies) gcmxCheck(gsx_sync(b.ctx), "gsx_sync");
+}
+
+size_t Engine::numberOfContactPairs() const { return contactPairs; }
 
 std::vector<real> Engine::pde(size_t body) const {
 	const Body& b = bodies.at(body);

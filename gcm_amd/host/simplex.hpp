@@ -137,6 +137,7 @@ private:
 /// Static data of one stage for the device (gsx_set_stage_plan).
 struct StagePlan {
 	std::vector<gsx_foot> feet;  // [node][6] invariants 0..5 (6..8 have dx == 0)
+	double shift[6][3] = {};     // direction * dx(k) (crossingPoints, common.hpp:46-52)
 	std::vector<int> borderNodes, innerNodes;
 	/// waveIndices of every node after contactAndBorderStage: 0 none, 1 RIGHT,
 	/// 2 LEFT, 3 both (gsx_set_border_plan's outer codes)
@@ -238,6 +239,9 @@ public:
 	/// current layer of a body, 9 doubles per vertex (downloads)
 	std::vector<real> pde(size_t body = 0) const;
 	real timeStepValue() const { return tau; }
+	/// wait for every body's stream (timing)
+	void sync() const;
+	size_t numberOfContactPairs() const;
 
 protected:
 	void nextTimeStep() override;
@@ -252,6 +256,7 @@ private:
 	};
 	std::vector<Body> bodies;
 	std::vector<gsx_contact*> contacts;
+	size_t contactPairs = 0;
 	real tau = 0;
 	std::vector<Task::BorderCondition> conditions;
 	void setBorderValues(real time);

@@ -203,10 +203,13 @@ gcmx_status gsx_set_matrices(gsx_ctx* ctx, const double* U, const double* U1);
 gcmx_status gsx_set_gradient_plan(gsx_ctx* ctx, const int* offsets, const int* neighbors,
                                   const double* rows, const double* weights, const double* M,
                                   const double* det);
-/* Feet of stage `stage`: feet[n_nodes][6] (invariants 0..5), the border nodes
- * (contactAndBorderStage) and the inner nodes (innerStage), in calculation order. */
-gcmx_status gsx_set_stage_plan(gsx_ctx* ctx, int stage, const gsx_foot* feet, int n_border,
-                               const int* border_nodes, int n_inner, const int* inner_nodes);
+/* Feet of stage `stage`: feet[n_nodes][6] (invariants 0..5), the shift of each
+ * invariant's characteristic (crossingPoints: direction * (-tau L(k)), [6][3]; a
+ * CELL foot's q must equal coords + shift, the device recomputes it), the border
+ * nodes (contactAndBorderStage) and the inner nodes (innerStage), in calculation order. */
+gcmx_status gsx_set_stage_plan(gsx_ctx* ctx, int stage, const gsx_foot* feet, const double* shift,
+                               int n_border, const int* border_nodes, int n_inner,
+                               const int* inner_nodes);
 gcmx_status gsx_upload(gsx_ctx* ctx, const double* aos /* [n][9] */);
 gcmx_status gsx_download(gsx_ctx* ctx, double* aos);
 /* Border correctors (engine/simplex/BorderCorrector.hpp:82-276, BorderCalcMode

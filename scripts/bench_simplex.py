@@ -1,0 +1,74 @@
+"""Throughput of the simplex (tetrahedral) path on one GPU -- BASELINE configs 4-5.
+
+The reference's simplex configs run on CGAL meshes of cube.off (config 4) and
+layers_with_fracture.off (config 5); CGAL is absent, so the meshes are jittered
+Kuhn tetrahedralisations:
+
+* cube:     the unit cube, n^3 cubes, free surface on every face (the reference's
+            parseTaskCgal3d: FIXED_FORCE 0 from an InfiniteArea), pressure sphere;
+* fracture: the 0.16 x 0.16 x 0.04 layer of layers_with_fracture.off with its
+            tetrahedral fracture carved out, free surface on the box and the fracture;
+* layered:  the unit cube split at z = 0.5 into two bodies of different materials
+            glued by an ADHESION contact, free surface outside.
+
+A node-step is one mesh vertex advanced one full time step (3 stages, border and
+contact correctors included).  Timed: K steps of SimplexEngine.run_steps between
+two stream synchronisations, inputs resident on the device.  Prints one JSON line
+per workload.
+
+    python scripts/bench_simplex.py [--workloads cube,fracture,layered] [--n 64]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def build(name, n):
+    from tests.simplex_spec import FREE_BORDER, fracture_task, host_task, layered_task
+    if name == "cube":
+        return host_task(n, 1.0, 0.1, 7, border=FREE_BORDER), f"unit cube, {n}^3 Kuhn cubes"
+    if name == "fracture":
+        cells = (n, n, max(4, n // 4))
+        return fracture_task(cells, 1.0), f"layers_with_fracture.off, {cells} Kuhn cubes"
+    if name == "layered":
+        return layered_task(n, 1.0), f"two layers + ADHESION contact, {n}^3 Kuhn cubes"
+    raise ValueError(name)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workloads", default="cube,fracture,layered")
+    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    from gcm_amd import _gcm_host as H
+    for name in a.workloads.split(","):
+        t0 = time.perf_counter()
+        task, desc = build(name, a.n)
+        task.number_of_snaps = 10 ** 6
+        e = H.SimplexEngine(task)
+        setup = time.perf_counter() - t0
+        nv = sum(e.number_of_vertices(b) for b in range(e.number_of_bodies))
+        e.run_steps(a.warmup)
+        e.sync()
+        t1 = time.perf_counter()
+        e.run_steps(a.steps)
+        e.sync()
+        dt = time.perf_counter() - t1
+        print(json.dumps({
+            "metric": "simplex Mnode-steps/s", "workload": name, "mesh": desc,
+            "value": round(nv * a.steps / dt / 1e6, 2), "unit": "Mnode-steps/s",
+            "ms_per_step": round(dt / a.steps * 1e3, 4), "vertices": nv,
+            "bodies": e.number_of_bodies, "contact_pairs": e.number_of_contact_pairs,
+            "steps": a.steps, "warmup": a.warmup, "setup_s": round(setup, 1), "dtype": "f64",
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
