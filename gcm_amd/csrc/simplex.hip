@@ -3,19 +3,18 @@
 //
 // One stage s (engine/simplex/Engine.cpp:117-148, GLOBAL_BASIS + PRODUCT):
 //   k_sx_transform(U_s)   beforeStage: w = U_s u for every node
-//                         (GridCharacteristicMethodInRiemannInvariants.hpp:44-56)
+//                         (GridCharacteristicMethodInRiemannInvariants.hpp:44-56);
+//                         only at the first stage of a step -- later stages get w
+//                         from the previous stage's final writers
 //   k_sx_gradient         Differentiation::estimateGradient of w (Differentiation.hpp:33-63)
-//   k_sx_nodes(border)    contactAndBorderStage (hpp:57-95)
-//   k_sx_correct          border correctors, applyInGlobalBasis (BorderCorrector.hpp:118-165,
-//                         256-265), on the border nodes' new invariants
-//   k_sx_nodes(inner)     innerStage (hpp:98-112) -- space-time feet read the border
-//                         nodes' new invariants written by the previous launch
-//   k_sx_transform(U1_s)  afterStage: u_new = U1_s w_new (hpp:115-126), then swap.
-// Layers u, un and the new invariants wn are SoA (component c of node n at
-// [c * N + n]); the invariants w of beforeStage, their gradients and the
-// coordinates are node-major (w[n][9], grad[n][3][6], coords[n][3]) because the
-// gradient and node kernels gather them per neighbour / per cell vertex.
-// Arithmetic follows the reference expression by expression (-ffp-contract=off).
+//   k_sx_border           contactAndBorderStage (hpp:57-95) + the border correctors
+//                         (applyInGlobalBasis, BorderCorrector.hpp:118-165, 256-265)
+//                         + afterStage and the next beforeStage of these nodes
+//   k_sx_contact          (multi-body) the contact correctors (ContactCorrector.hpp)
+//                         + afterStage / next beforeStage of the contact nodes
+//   k_sx_inner            innerStage (hpp:98-112) -- space-time feet read the border
+//                         nodes' corrected new invariants -- + afterStage
+//                         (u_new = U1_s w_new, hpp:115-126) + next beforeStage; swap.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -92,6 +91,11 @@ struct gsx_ctx {
 	bool gradSet = false;
 	StageDev st[3];
 	BorderDev bd;
+	double* wnext = nullptr;             // next stage's invariants, node-major [n][9]
+	bool chained = false;                // w already holds this stage's invariants
+	int* corrOf = nullptr;               // node -> border-plan entry or -1
+	char* deferred = nullptr;            // node in a contact: the contact kernel finalizes it
+	std::vector<char> hostDeferred;
 };
 
 struct gsx_contact {
@@ -203,19 +207,17 @@ __device__ __forceinline__ double std_min(double a, double b) { return (b < a) ?
 __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
 
 // interpolateValuesAround (hpp:156-198) for the listed nodes, feet resolved on the host.
-__global__ __launch_bounds__(256) void k_sx_nodes(const int* __restrict__ nodes, int count,
-                                                  const int4* __restrict__ fv,
-                                                  const double4* __restrict__ flam,
-                                                  const int* __restrict__ fmeta, StageShift sh,
-                                                  const double* __restrict__ coords,
-                                                  const double* __restrict__ w,
-                                                  const double* __restrict__ grad,
-                                                  double* __restrict__ wn, int N) {
-	const int t = blockIdx.x * blockDim.x + threadIdx.x;
-	if (t >= count) return;
-	const int n = nodes[t];
+__device__ __forceinline__ void node_invariants(int n, const int4* __restrict__ fv,
+                                                const double4* __restrict__ flam,
+                                                const int* __restrict__ fmeta, const StageShift& sh,
+                                                const double* __restrict__ coords,
+                                                const double* __restrict__ w,
+                                                const double* __restrict__ grad,
+                                                const double* __restrict__ wn, int N,
+                                                double (&out)[kM]) {
 	const double x0 = coords[3 * (size_t)n + 0], x1 = coords[3 * (size_t)n + 1],
 	             x2 = coords[3 * (size_t)n + 2];
+#pragma unroll
 	for (int k = 0; k < kM; k++) {
 		double ans;
 		if (k >= 6) {
@@ -254,6 +256,7 @@ __global__ __launch_bounds__(256) void k_sx_nodes(const int* __restrict__ nodes,
 				          ? quadratic
 				          : lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
 			} else if (kind == GSX_FOOT_SPACETIME) {
+				// the face's border nodes: current invariants w, new invariants wn
 				const int4 fvv = fv[e];
 				const double4 l = flam[e];
 				const int vs[3] = {fvv.x, fvv.y, fvv.z};
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(256) void k_sx_nodes(const int* __restrict__ nodes,
 				ans = 0.0;  // outer invariant / walk ended on a vertex
 			}
 		}
-		wn[k * N + n] = ans;
+		out[k] = ans;
 	}
 }
 
@@ -373,26 +376,20 @@ __device__ __forceinline__ void mat_vec(const double* __restrict__ Mx, const dou
 	}
 }
 
-// BorderCorrectorInRiemannInvariants::applyInGlobalBasis (BorderCorrector.hpp:256-265):
-// invariants -> PDE (U1), BorderCorrectorInPdeVectors::applyInGlobalBasis (:118-165),
-// PDE -> invariants (U).
-__global__ __launch_bounds__(256) void k_sx_correct(const int* __restrict__ nodes,
-                                                    const int* __restrict__ cond,
-                                                    const double* __restrict__ Bm,
-                                                    const double* __restrict__ Sm,
-                                                    const signed char* __restrict__ outer,
-                                                    const double* __restrict__ U,
-                                                    const double* __restrict__ U1, double* wn,
-                                                    int count, int stage, int N, BorderArgs args) {
-	const int t = blockIdx.x * blockDim.x + threadIdx.x;
-	if (t >= count) return;
-	const int n = nodes[t], c = cond[t];
+// BorderCorrectorInRiemannInvariants::applyInGlobalBasis (BorderCorrector.hpp:256-265)
+// on one node's new invariants w: -> PDE (U1), BorderCorrectorInPdeVectors::
+// applyInGlobalBasis (:118-165), -> invariants (U).  t = the node's border-plan entry.
+__device__ void border_correct(double (&w)[kM], int t, const int* __restrict__ cond,
+                               const double* __restrict__ Bm, const double* __restrict__ Sm,
+                               const signed char* __restrict__ outer, int count,
+                               const double* __restrict__ U, const double* __restrict__ U1,
+                               int stage, const BorderArgs& args) {
+	const int c = cond[t];
 	const int code = outer[(size_t)stage * count + t];
 	const double* B = Bm + 27 * (size_t)t;
 	const double b[3] = {args.b[c][0], args.b[c][1], args.b[c][2]};
 	const double minValid = args.minDet[c][stage];
-	double w[kM], u[kM];
-	for (int k = 0; k < kM; k++) w[k] = wn[k * N + n];
+	double u[kM];
 	mat_vec(U1, w, u);
 	const int R[3] = {1, 3, 5}, L[3] = {0, 2, 4};  // Model.cpp:81-82
 	if (code == 1 || code == 2) {
@@ -414,12 +411,78 @@ __global__ __launch_bounds__(256) void k_sx_correct(const int* __restrict__ node
 		}
 	}
 	mat_vec(U, u, w);
-	for (int k = 0; k < kM; k++) wn[k * N + n] = w[k];
+}
+
+// afterStage for one node (u_new = U1_s w_new, hpp:115-126) and, when the next
+// stage of the step follows, its beforeStage (w' = U_{s+1} u_new, node-major):
+// the node's final writer does both, so no separate transform pass is needed.
+__device__ __forceinline__ void finalize(int n, const double (&wv)[kM], const double* __restrict__ U1,
+                                         const double* __restrict__ Unext, double* __restrict__ un,
+                                         double* __restrict__ wnext, int N) {
+	double u[kM];
+	mat_vec(U1, wv, u);
+#pragma unroll
+	for (int k = 0; k < kM; k++) un[k * N + n] = u[k];
+	if (Unext) {
+		double w2[kM];
+		mat_vec(Unext, u, w2);
+#pragma unroll
+		for (int k = 0; k < kM; k++) wnext[(size_t)n * kM + k] = w2[k];
+	}
+}
+
+struct BorderDevArgs {  // the border plan's device arrays (null cond = no plan)
+	const int *corrOf, *cond;
+	const double *B, *S;
+	const signed char* outer;
+	int count;
+};
+
+// contactAndBorderStage (hpp:57-95) for the contact and border nodes, the border
+// correctors of the border-plan nodes inline (BorderCorrector.hpp:118-165: they
+// only read the node's own new invariants) and, for every node that is not in a
+// contact, afterStage + the next beforeStage.  wn keeps the corrected invariants
+// of these nodes: inner space-time feet and the contact correctors read them.
+__global__ __launch_bounds__(64) void k_sx_border(
+    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
+    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
+    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, BorderArgs args,
+    const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
+    double* __restrict__ un, double* __restrict__ wnext, int stage, int N) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= count) return;
+	const int n = nodes[t];
+	double out[kM];
+	node_invariants(n, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
+	if (bp.cond) {
+		const int ci = bp.corrOf[n];
+		if (ci >= 0) border_correct(out, ci, bp.cond, bp.B, bp.S, bp.outer, bp.count, U, U1, stage, args);
+	}
+#pragma unroll
+	for (int k = 0; k < kM; k++) wn[k * N + n] = out[k];
+	if (!deferred[n]) finalize(n, out, U1, Unext, un, wnext, N);
+}
+
+// innerStage (hpp:98-112) + afterStage + the next beforeStage for the inner nodes;
+// space-time feet read the border nodes' corrected new invariants (wn).
+__global__ __launch_bounds__(256) void k_sx_inner(
+    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
+    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
+    const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
+    double* __restrict__ un, double* __restrict__ wnext, int N) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= count) return;
+	const int n = nodes[t];
+	double out[kM];
+	node_invariants(n, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
+	finalize(n, out, U1, Unext, un, wnext, N);
 }
 
 // BorderCorrectorInPdeVectors::applyPlainCorrection (BorderCorrector.hpp:167-178) on
 // the current layer.
-__global__ __launch_bounds__(256) void k_sx_plain(const int* __restrict__ nodes,
+__global__ __launch_bounds__(64) void k_sx_plain(const int* __restrict__ nodes,
                                                   const int* __restrict__ cond,
                                                   const double* __restrict__ Sm, double* u_,
                                                   int count, int N, BorderArgs args) {
@@ -436,12 +499,14 @@ __global__ __launch_bounds__(256) void k_sx_plain(const int* __restrict__ nodes,
 // ContactCorrectorInRiemannInvariants::applyInGlobalBasis (ContactCorrector.hpp:333-348):
 // matchInnersAndOuters (zeroing decided on the host), invariants -> PDE (U1),
 // ContactCorrectorInPdeVectors::applyInGlobalBasis (:150-247), PDE -> invariants (U).
-__global__ __launch_bounds__(256) void k_sx_contact(
+__global__ __launch_bounds__(64) void k_sx_contact(
     const int* __restrict__ na, const int* __restrict__ nb, const double* __restrict__ normal,
     const double* __restrict__ Sm, const signed char* __restrict__ codeA,
     const signed char* __restrict__ codeB, const double* __restrict__ UA,
     const double* __restrict__ U1A, const double* __restrict__ UB, const double* __restrict__ U1B,
-    double* wnA, double* wnB, int NA, int NB, int count, int stage, double min1, double min2) {
+    double* wnA, double* wnB, int NA, int NB, int count, int stage, double min1, double min2,
+    const double* __restrict__ UnextA, const double* __restrict__ UnextB, double* unA, double* unB,
+    double* wnextA, double* wnextB) {
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int a = na[t], b = nb[t];
@@ -512,6 +577,8 @@ __global__ __launch_bounds__(256) void k_sx_contact(
 		wnA[k * NA + a] = wA[k];
 		wnB[k * NB + b] = wB[k];
 	}
+	finalize(a, wA, U1A, UnextA, unA, wnextA, NA);
+	finalize(b, wB, U1B, UnextB, unB, wnextB, NB);
 }
 
 // ContactCorrectorInPdeVectors::applyPlainCorrection (ContactCorrector.hpp:249-262)
@@ -587,14 +654,19 @@ gcmx_status gsx_create(int device, int n_nodes, const double* coords, gsx_ctx** 
 	c->hostCoords.assign(coords, coords + 3 * N);
 	gcmx_status s = upload(&c->coords, coords, 3 * N);  // node-major [n][3]
 	if (s) { gsx_destroy(c); return s; }
-	double** bufs[5] = {&c->u, &c->un, &c->w, &c->wn, &c->grad};
-	const size_t sizes[5] = {kM * N, kM * N, kM * N, kM * N, 3 * 6 * N};
-	for (int i = 0; i < 5; i++) {
+	double** bufs[6] = {&c->u, &c->un, &c->w, &c->wn, &c->grad, &c->wnext};
+	const size_t sizes[6] = {kM * N, kM * N, kM * N, kM * N, 3 * 6 * N, kM * N};
+	for (int i = 0; i < 6; i++) {
 		if (hipMalloc(bufs[i], sizes[i] * sizeof(double)) != hipSuccess ||
 		    hipMemset(*bufs[i], 0, sizes[i] * sizeof(double)) != hipSuccess) {
 			gsx_destroy(c);
 			return fail(GCMX_ERR_OOM, "simplex layer allocation failed");
 		}
+	}
+	c->hostDeferred.assign(N, 0);
+	if ((s = upload(&c->deferred, c->hostDeferred.data(), N))) {
+		gsx_destroy(c);
+		return s;
 	}
 	*out = c;
 	return GCMX_OK;
@@ -604,7 +676,8 @@ void gsx_destroy(gsx_ctx* c) {
 	if (!c) return;
 	(void)hipSetDevice(c->device);
 	if (c->stream) (void)hipStreamSynchronize(c->stream);
-	void* ptrs[] = {c->coords, c->u, c->un, c->w, c->wn, c->grad, c->mats, c->gOff, c->gNb,
+	void* ptrs[] = {c->coords, c->u, c->un, c->w, c->wn, c->grad, c->wnext, c->corrOf, c->deferred,
+	                c->mats, c->gOff, c->gNb,
 	                c->gRows, c->gW, c->gM, c->gDet};
 	for (void* p : ptrs)
 		if (p) (void)hipFree(p);
@@ -728,6 +801,7 @@ gcmx_status gsx_upload(gsx_ctx* c, const double* aos) {
 		for (int k = 0; k < kM; k++) soa[k * N + n] = aos[kM * n + k];
 	SX_TRY(hipStreamSynchronize(c->stream));
 	SX_TRY(hipMemcpy(c->u, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice));
+	c->chained = false;
 	return GCMX_OK;
 }
 
@@ -767,6 +841,12 @@ gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const d
 	    (s = upload(&bd.B, B, 27 * (size_t)n)) || (s = upload(&bd.S, S, 9 * (size_t)n)) ||
 	    (s = upload(&bd.outer, outer, 3 * (size_t)n)))
 		return s;
+	std::vector<int> corrOf((size_t)c->N, -1);
+	for (int i = 0; i < n; i++) {
+		if (corrOf[(size_t)nodes[i]] >= 0) return fail(GCMX_ERR_INVALID_ARG, "node corrected twice");
+		corrOf[(size_t)nodes[i]] = i;
+	}
+	if ((s = upload(&c->corrOf, corrOf.data(), corrOf.size()))) return s;
 	bd.n = n;
 	bd.nCond = n_cond;
 	bd.args = BorderArgs{};
@@ -796,11 +876,19 @@ gcmx_status gsx_plain_correction(gsx_ctx* c) {
 	const BorderDev& bd = c->bd;
 	if (!bd.set || !bd.valuesSet) return fail(GCMX_ERR_STATE, "border plan / values not set");
 	if (bd.n)
-		hipLaunchKernelGGL(k_sx_plain, dim3((bd.n + 255) / 256), dim3(256), 0, c->stream, bd.nodes,
+		hipLaunchKernelGGL(k_sx_plain, dim3((bd.n + 63) / 64), dim3(64), 0, c->stream, bd.nodes,
 		                   bd.cond, bd.S, c->u, bd.n, c->N, bd.args);
 	SX_TRY(hipGetLastError());
 	return GCMX_OK;
 }
+
+namespace {
+// The next stage's U for the fused beforeStage, or null after the last stage of
+// the step (the next step starts with the plain corrections, which change u).
+const double* nextU(const gsx_ctx* c, int stage) {
+	return stage < 2 ? c->mats + (stage + 1) * 81 : nullptr;
+}
+}  // namespace
 
 gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 	gcmx_status s = check(c);
@@ -808,16 +896,28 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 	if (stage < 0 || stage > 2) return fail(GCMX_ERR_INVALID_ARG, "stage out of range");
 	if (!c->matsSet || !c->gradSet || !c->st[stage].set)
 		return fail(GCMX_ERR_STATE, "simplex matrices / gradient plan / stage plan not set");
+	const BorderDev& bd = c->bd;
+	if (bd.set && bd.n && !bd.valuesSet) return fail(GCMX_ERR_STATE, "border values not set");
 	const int N = c->N;
 	const dim3 blk(256), grd((N + 255) / 256);
 	const StageDev& st = c->st[stage];
-	hipLaunchKernelGGL(k_sx_transform<true>, grd, blk, 0, c->stream, c->u, c->w, c->mats + stage * 81, N);
+	// beforeStage: the invariants come from the previous stage's final writers when
+	// chained, otherwise from a transform pass
+	if (!(c->chained && stage > 0))
+		hipLaunchKernelGGL(k_sx_transform<true>, grd, blk, 0, c->stream, c->u, c->w,
+		                   c->mats + stage * 81, N);
+	c->chained = false;
 	hipLaunchKernelGGL(k_sx_gradient, grd, blk, 0, c->stream, c->w, c->grad, c->gOff, c->gNb,
 	                   c->coords, c->gW, c->gM, c->gDet, N);
-	if (st.nBorder)
-		hipLaunchKernelGGL(k_sx_nodes, dim3((st.nBorder + 255) / 256), blk, 0, c->stream, st.border,
+	if (st.nBorder) {
+		const BorderDevArgs bp = {c->corrOf, (bd.set && bd.n) ? bd.cond : nullptr, bd.B, bd.S,
+		                          bd.outer, bd.n};
+		// border lists are short (a surface): 64-thread blocks spread them over the CUs
+		hipLaunchKernelGGL(k_sx_border, dim3((st.nBorder + 63) / 64), dim3(64), 0, c->stream, st.border,
 		                   st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
-		                   c->wn, N);
+		                   c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
+		                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N);
+	}
 	SX_TRY(hipGetLastError());
 	return GCMX_OK;
 }
@@ -829,23 +929,18 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 	if (!c->matsSet || !c->gradSet || !c->st[stage].set)
 		return fail(GCMX_ERR_STATE, "simplex matrices / gradient plan / stage plan not set");
 	const int N = c->N;
-	const dim3 blk(256), grd((N + 255) / 256);
+	const dim3 blk(256);
 	const StageDev& st = c->st[stage];
-	const BorderDev& bd = c->bd;
-	if (bd.set && bd.n) {
-		if (!bd.valuesSet) return fail(GCMX_ERR_STATE, "border values not set");
-		hipLaunchKernelGGL(k_sx_correct, dim3((bd.n + 255) / 256), blk, 0, c->stream, bd.nodes,
-		                   bd.cond, bd.B, bd.S, bd.outer, c->mats + stage * 81,
-		                   c->mats + 3 * 81 + stage * 81, c->wn, bd.n, stage, N, bd.args);
-	}
 	if (st.nInner)
-		hipLaunchKernelGGL(k_sx_nodes, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
+		hipLaunchKernelGGL(k_sx_inner, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
 		                   st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
-		                   c->wn, N);
-	hipLaunchKernelGGL(k_sx_transform<false>, grd, blk, 0, c->stream, c->wn, c->un,
-	                   c->mats + 3 * 81 + stage * 81, N);
+		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N);
 	SX_TRY(hipGetLastError());
 	std::swap(c->u, c->un);
+	if (stage < 2) {
+		std::swap(c->w, c->wnext);
+		c->chained = true;
+	}
 	return GCMX_OK;
 }
 
@@ -883,6 +978,19 @@ gcmx_status gsx_contact_create(gsx_ctx* a, gsx_ctx* b, int n, const int* nodes_a
 	if ((s = upload(&c->na, nodes_a, (size_t)n)) || (s = upload(&c->nb, nodes_b, (size_t)n)) ||
 	    (s = upload(&c->normal, normal, 3 * (size_t)n)) || (s = upload(&c->S, S, 9 * (size_t)n)) ||
 	    (s = upload(&c->codeA, code_a, 3 * (size_t)n)) || (s = upload(&c->codeB, code_b, 3 * (size_t)n))) {
+		gsx_contact_destroy(c);
+		return s;
+	}
+	if (hipStreamSynchronize(a->stream) != hipSuccess || hipStreamSynchronize(b->stream) != hipSuccess) {
+		gsx_contact_destroy(c);
+		return fail(GCMX_ERR_HIP, "hipStreamSynchronize failed");
+	}
+	for (int i = 0; i < n; i++) {
+		a->hostDeferred[(size_t)nodes_a[i]] = 1;
+		b->hostDeferred[(size_t)nodes_b[i]] = 1;
+	}
+	if ((s = upload(&a->deferred, a->hostDeferred.data(), a->hostDeferred.size())) ||
+	    (s = upload(&b->deferred, b->hostDeferred.data(), b->hostDeferred.size()))) {
 		gsx_contact_destroy(c);
 		return s;
 	}
@@ -928,11 +1036,12 @@ gcmx_status gsx_contact_correct(gsx_contact* c, int stage) {
 	const double* mA = c->a->mats;
 	const double* mB = c->b->mats;
 	return onBothStreams(c, [&] {
-		hipLaunchKernelGGL(k_sx_contact, dim3((c->n + 255) / 256), dim3(256), 0, c->a->stream, c->na,
+		hipLaunchKernelGGL(k_sx_contact, dim3((c->n + 63) / 64), dim3(64), 0, c->a->stream, c->na,
 		                   c->nb, c->normal, c->S, c->codeA, c->codeB, mA + stage * 81,
 		                   mA + 3 * 81 + stage * 81, mB + stage * 81, mB + 3 * 81 + stage * 81,
 		                   c->a->wn, c->b->wn, c->a->N, c->b->N, c->n, stage, c->minDet[stage][0],
-		                   c->minDet[stage][1]);
+		                   c->minDet[stage][1], nextU(c->a, stage), nextU(c->b, stage), c->a->un,
+		                   c->b->un, c->a->wnext, c->b->wnext);
 	});
 }
 
