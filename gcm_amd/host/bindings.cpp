@@ -360,6 +360,12 @@ PYBIND11_MODULE(_gcm_host, m) {
 	         },
 	         py::arg("area"), py::arg("type"), py::arg("values"),
 	         py::arg("use_for_multicontact_nodes") = true)
+	    .def("set_simplex_inm_mesh",
+	         [](Task& t, const std::string& fileName) {
+		         t.simplexGrid.mesher = Task::SimplexGrid::Mesher::INM_MESHER;
+		         t.simplexGrid.fileName = fileName;
+	         },
+	         py::arg("file_name"), "INM_MESHER: points, cells and per-cell body ids from a file")
 	    .def("set_simplex_domain",
 	         [](Task& t, std::vector<std::array<real, 3>> points, std::vector<std::array<int, 3>> faces) {
 		         t.simplexGrid.offPoints.assign(points.begin(), points.end());
@@ -412,6 +418,50 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    },
 	    "GPU-free VtkSnapshotter file of one body (set-up layer, or `pde`)", py::arg("task"),
 	    py::arg("body_id"), py::arg("file_name"), py::arg("pde") = py::none());
+
+	m.def(
+	    "write_simplex_vtk",
+	    [](const Task& t, const std::string& fileName, py::object pde, size_t body) {
+		    // GPU-free simplex VtkSnapshotter file of one body: the set-up layer or `pde`
+		    const simplex::HostPlans hp = simplex::buildHostPlans(t);
+		    const simplex::BodyPlans& b = hp.bodies.at(body);
+		    std::vector<real> u = b.pde;
+		    if (!pde.is_none()) {
+			    auto a = pde.cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
+			    if ((size_t)a.size() != u.size()) throw Exception("pde has the wrong size");
+			    std::copy(a.data(), a.data() + a.size(), u.begin());
+		    }
+		    simplex::writeVtkSnapshot(fileName, b.mesh.v, b.mesh.cells, u.data(),
+		                              t.materialConditions.byBodies.bodyMaterialMap.at(b.id)->materialNumber,
+		                              t.vtkSnapshotter.quantitiesToSnap);
+	    },
+	    py::arg("task"), py::arg("file_name"), py::arg("pde") = py::none(), py::arg("body") = 0);
+
+	m.def(
+	    "read_inm",
+	    [](const std::string& fileName) {
+		    std::vector<Real3> pts;
+		    std::vector<std::array<int, 4>> cells;
+		    std::vector<int> mats;
+		    simplex::readInm(fileName, pts, cells, mats);
+		    py::array_t<double> P({(ssize_t)pts.size(), (ssize_t)3});
+		    for (size_t i = 0; i < pts.size(); i++)
+			    for (int c = 0; c < 3; c++) P.mutable_at((ssize_t)i, c) = pts[i][c];
+		    return py::make_tuple(P, cells, mats);
+	    },
+	    "InmMeshLoader::readFromFile: (points, cells (1-based), materials)", py::arg("file_name"));
+
+	m.def(
+	    "simplex_triangulation",
+	    [](const Task& t) {
+		    const simplex::Triangulation tr = simplex::buildTriangulation(t);
+		    py::array_t<double> P({(ssize_t)tr.all.v.size(), (ssize_t)3});
+		    for (size_t i = 0; i < tr.all.v.size(); i++)
+			    for (int c = 0; c < 3; c++) P.mutable_at((ssize_t)i, c) = tr.all.v[i][c];
+		    return py::make_tuple(P, tr.all.cells, tr.gridId);
+	    },
+	    "The task's whole triangulation: (points, cells (0-based), grid id per cell, -1 = empty)",
+	    py::arg("task"));
 
 	m.def("simplex_plans", &simplexPlans,
 	      "GPU-free simplex set-up: mesh, time step, gradient and stage plans", py::arg("task"));

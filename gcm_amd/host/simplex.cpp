@@ -314,9 +314,90 @@ void readOff(const std::string& fileName, std::vector<Real3>& points,
 	}
 }
 
+void readInm(const std::string& fileName, std::vector<Real3>& points,
+             std::vector<std::array<int, 4>>& cells, std::vector<int>& materials) {
+	std::ifstream in(fileName);
+	if (!in) throw Exception("cannot open " + fileName);
+	auto fields = [](const std::string& line) {
+		std::istringstream ls(line);
+		std::vector<std::string> out;
+		std::string t;
+		while (ls >> t) out.push_back(t);
+		return out;
+	};
+	std::string line;
+	auto next = [&]() {
+		if (!std::getline(in, line)) throw Exception("truncated INM mesh file " + fileName);
+		return fields(line);
+	};
+	auto f = next();  // readPoints (:121-141)
+	if (f.size() != 1) throw Exception("INM: number of points expected");
+	const long np = std::stol(f[0]);
+	if (np < 4) throw Exception("INM: fewer points than a cell has");
+	points.assign((size_t)np, Real3{});
+	for (long i = 0; i < np; i++) {
+		f = next();
+		if (f.size() != 3) throw Exception("INM: a point needs 3 coordinates");
+		for (int c = 0; c < 3; c++) points[(size_t)i][c] = std::stod(f[(size_t)c]);
+	}
+	f = next();  // readCells (:144-164)
+	if (f.size() != 1) throw Exception("INM: number of cells expected");
+	const long nc = std::stol(f[0]);
+	if (nc < 1) throw Exception("INM: no cells");
+	cells.clear();
+	materials.clear();
+	for (long i = 0; i < nc; i++) {
+		f = next();
+		if (f.size() != 5) throw Exception("INM: a cell needs 4 vertices and a material");
+		std::array<int, 4> c;
+		for (int k = 0; k < 4; k++) {
+			c[k] = std::stoi(f[(size_t)k]);
+			if (c[k] < 1 || c[k] > np) throw Exception("INM: cell vertex out of range");
+		}
+		cells.push_back(c);
+		materials.push_back(std::stoi(f[4]));
+	}
+	f = next();  // checkEndOfFile (:167-172)
+	if (f.size() != 1 || std::stoi(f[0]) != 0) throw Exception("INM: the file must end with 0");
+}
+
+namespace {
+/// The INM mesher: the file's cells are the triangulation (the reference inserts
+/// the points into a CGAL Delaunay triangulation and gives each of its cells the
+/// material of the same INM cell, InmMeshLoader.hpp:47-93; CGAL is absent, so the
+/// file must hold the whole tetrahedralisation), grid id = material.
+Triangulation inmTriangulation(const Task& task) {
+	std::vector<Real3> pts;
+	std::vector<std::array<int, 4>> cells;
+	std::vector<int> mats;
+	readInm(task.simplexGrid.fileName, pts, cells, mats);
+	Triangulation tr;
+	tr.all.v = pts;
+	for (auto c : cells) {
+		for (int& x : c) x -= 1;  // INM numbers vertices from 1
+		const real vol = orientedVolume(pts[(size_t)c[0]], pts[(size_t)c[1]], pts[(size_t)c[2]],
+		                                pts[(size_t)c[3]]);
+		if (!(vol != 0)) throw Exception("INM: degenerate cell");
+		if (vol < 0) std::swap(c[2], c[3]);
+		tr.all.cells.push_back(c);
+	}
+	tr.all.buildTopology();
+	for (int m : mats) {
+		if (!task.bodies.count((size_t)m)) throw Exception("INM: a cell's material names no body");
+		tr.gridId.push_back(m);
+	}
+	return tr;
+}
+}  // namespace
+
 Triangulation buildTriangulation(const Task& task) {
 	const auto& sg = task.simplexGrid;
 	if (task.bodies.empty()) throw Exception("the simplex task has no bodies");
+	if (sg.mesher == Task::SimplexGrid::Mesher::INM_MESHER) {
+		if (!sg.offFaces.empty() || !sg.bodyAreas.empty())
+			throw Exception("INM meshes carry their own cells and grid ids");
+		return inmTriangulation(task);
+	}
 	Triangulation tr;
 	tr.all = boxMesh(sg.cells, sg.lo, sg.hi, sg.jitter, sg.seed);
 	const int firstBody = (int)task.bodies.begin()->first;
@@ -1081,6 +1162,8 @@ Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
 	conditions = task.borderConditions;
 	for (auto& bp : p.bodies) {
 		Body b;
+		b.id = bp.id;
+		b.materialNumber = task.materialConditions.byBodies.bodyMaterialMap.at(bp.id)->materialNumber;
 		const int nv = bp.mesh.nVertices();
 		std::vector<double> coords((size_t)nv * 3);
 		for (int i = 0; i < nv; i++)
@@ -1111,7 +1194,23 @@ Engine::Engine(const Task& task, int device) : AbstractEngine(task) {
 	// applyPlainBorderContactCorrection(Clock::Time()) (Engine.cpp:44)
 	setBorderValues(Clock::Time());
 	plainCorrections();
+	stepsPerSnap = std::max(1, task.globalSettings.stepsPerSnap);
+	for (const Snapshotters::T t : task.globalSettings.snapshottersId) {
+		if (t == Snapshotters::T::VTK) vtk = std::make_unique<VtkSnapshotter>(task);
+		else throw Exception("only the VTK snapshotter is on the simplex path");
+	}
 	afterConstruction(task);
+}
+
+/// Engine::writeSnapshots (Engine.cpp:313-320) with the VTK snapshotter of every
+/// body (VtkSnapshotter.hpp:20-61): the layer is downloaded only when due.
+void Engine::writeSnapshots(const int step) {
+	if (!vtk || step % stepsPerSnap != 0) return;
+	for (size_t i = 0; i < bodies.size(); i++) {
+		const std::vector<real> u = pde(i);
+		writeVtkSnapshot(vtk->fileName(bodies[i].id, step), bodies[i].mesh.v, bodies[i].mesh.cells,
+		                 u.data(), bodies[i].materialNumber, vtk->quantities);
+	}
 }
 
 void Engine::setBorderValues(real time) {

@@ -69,6 +69,11 @@ struct Triangulation {
 bool offContains(const std::vector<Real3>& points, const std::vector<std::array<int, 3>>& faces,
                  const Real3& p);
 
+/// InmMeshLoader::readFromFile (grid/simplex/mesh_loaders/InmMeshLoader.hpp:96-170):
+/// points, cells (1-based INM vertex numbers) and the material of every cell.
+void readInm(const std::string& fileName, std::vector<Real3>& points,
+             std::vector<std::array<int, 4>>& cells, std::vector<int>& materials);
+
 /// Read the vertices and triangles of an .off file (the reference meshes/*.off).
 void readOff(const std::string& fileName, std::vector<Real3>& points,
              std::vector<std::array<int, 3>>& faces);
@@ -182,6 +187,7 @@ BorderPlan buildBorderPlan(const Task& task, const Grid& grid, const GcmMatrices
 }  // namespace gcm
 
 #include "engine.hpp"
+#include "snapshot.hpp"
 
 namespace gcm {
 namespace simplex {
@@ -246,10 +252,12 @@ public:
 protected:
 	void nextTimeStep() override;
 	real estimateTimeStep() override;
-	void writeSnapshots(const int) override {}
+	void writeSnapshots(const int step) override;
 
 private:
 	struct Body {
+		size_t id = 0;
+		int materialNumber = 0;
 		TetMesh mesh;
 		gsx_ctx* ctx = nullptr;
 		bool hasBorderPlan = false;
@@ -259,6 +267,8 @@ private:
 	size_t contactPairs = 0;
 	real tau = 0;
 	std::vector<Task::BorderCondition> conditions;
+	std::unique_ptr<VtkSnapshotter> vtk;
+	int stepsPerSnap = 1;
 	void setBorderValues(real time);
 	void plainCorrections();
 };

@@ -52,6 +52,96 @@ std::string Snapshotter::makeFileNameForSnapshot(const std::string& meshId, cons
 }
 
 namespace cubic {
+const char* quantityName(PhysicalQuantities::T q);
+}
+
+namespace simplex {
+
+void writeVtu(const std::string& fileName, const std::vector<float>& points,
+              const std::vector<std::array<int, 4>>& cells, const std::vector<VtkPointArray>& arrays) {
+	const uint64_t n = points.size() / 3, nc = cells.size();
+	if (points.size() != 3 * n) throw Exception("writeVtu: points size");
+	for (const auto& a : arrays)
+		if (a.values.size() != n * (uint64_t)a.components) throw Exception("writeVtu: array size");
+	std::vector<int64_t> conn, offs;
+	std::vector<uint8_t> types(nc, 10);  // VTK_TETRA
+	for (const auto& c : cells) {
+		for (int x : c) {
+			if (x < 0 || (uint64_t)x >= n) throw Exception("writeVtu: cell vertex out of range");
+			conn.push_back(x);
+		}
+		offs.push_back((int64_t)conn.size());
+	}
+	std::ofstream f(fileName, std::ios::binary);
+	if (!f.is_open()) throw Exception("cannot open " + fileName);
+	f << "<?xml version=\"1.0\"?>\n"
+	  << "<VTKFile type=\"UnstructuredGrid\" version=\"1.0\" byte_order=\"LittleEndian\" "
+	     "header_type=\"UInt64\">\n"
+	  << "  <UnstructuredGrid>\n"
+	  << "    <Piece NumberOfPoints=\"" << n << "\" NumberOfCells=\"" << nc << "\">\n"
+	  << "      <PointData>\n";
+	uint64_t offset = 0;
+	for (const auto& a : arrays) {
+		f << "        <DataArray type=\"Float32\" Name=\"" << a.name << "\" NumberOfComponents=\""
+		  << a.components << "\" format=\"appended\" offset=\"" << offset << "\"/>\n";
+		offset += 8 + 4 * (uint64_t)a.values.size();
+	}
+	f << "      </PointData>\n      <CellData>\n      </CellData>\n      <Points>\n"
+	  << "        <DataArray type=\"Float32\" Name=\"Points\" NumberOfComponents=\"3\" "
+	     "format=\"appended\" offset=\"" << offset << "\"/>\n      </Points>\n      <Cells>\n";
+	offset += 8 + 4 * (uint64_t)points.size();
+	f << "        <DataArray type=\"Int64\" Name=\"connectivity\" format=\"appended\" offset=\""
+	  << offset << "\"/>\n";
+	offset += 8 + 8 * (uint64_t)conn.size();
+	f << "        <DataArray type=\"Int64\" Name=\"offsets\" format=\"appended\" offset=\"" << offset
+	  << "\"/>\n";
+	offset += 8 + 8 * (uint64_t)offs.size();
+	f << "        <DataArray type=\"UInt8\" Name=\"types\" format=\"appended\" offset=\"" << offset
+	  << "\"/>\n      </Cells>\n    </Piece>\n  </UnstructuredGrid>\n"
+	  << "  <AppendedData encoding=\"raw\">\n   _";
+	auto block = [&f](const void* data, uint64_t bytes) {
+		f.write(reinterpret_cast<const char*>(&bytes), 8);
+		f.write(reinterpret_cast<const char*>(data), (std::streamsize)bytes);
+	};
+	for (const auto& a : arrays) block(a.values.data(), 4 * (uint64_t)a.values.size());
+	block(points.data(), 4 * (uint64_t)points.size());
+	block(conn.data(), 8 * (uint64_t)conn.size());
+	block(offs.data(), 8 * (uint64_t)offs.size());
+	block(types.data(), (uint64_t)types.size());
+	f << "\n  </AppendedData>\n</VTKFile>\n";
+	if (!f.good()) throw Exception("write failed: " + fileName);
+}
+
+void writeVtkSnapshot(const std::string& fileName, const std::vector<Real3>& coords,
+                      const std::vector<std::array<int, 4>>& cells, const real* pde,
+                      int materialNumber, const std::vector<PhysicalQuantities::T>& quantities) {
+	const size_t n = coords.size();
+	std::vector<float> points(3 * n);
+	VtkPointArray vel{"Velocity", 3, std::vector<float>(3 * n)};
+	std::vector<VtkPointArray> qs;
+	for (auto q : quantities) {
+		if (!hasQuantity(3, q)) throw Exception("quantity to snap is not in this PDE vector");
+		qs.push_back(VtkPointArray{cubic::quantityName(q), 1, std::vector<float>(n)});
+	}
+	VtkPointArray mat{"material_index", 1, std::vector<float>(n, (float)materialNumber)};
+	for (size_t p = 0; p < n; p++) {  // VtkIterator: vertices in local order
+		const real* v = pde + 9 * p;
+		for (int i = 0; i < 3; i++) {
+			points[3 * p + i] = (float)coords[p][i];
+			vel.values[3 * p + i] = (float)v[i];
+		}
+		for (size_t k = 0; k < qs.size(); k++) qs[k].values[p] = (float)getQuantity(3, quantities[k], v);
+	}
+	std::vector<VtkPointArray> arrays;
+	arrays.push_back(std::move(vel));
+	for (auto& a : qs) arrays.push_back(std::move(a));
+	arrays.push_back(std::move(mat));
+	writeVtu(fileName, points, cells, arrays);
+}
+
+}  // namespace simplex
+
+namespace cubic {
 
 const char* quantityName(PhysicalQuantities::T q) {  // util/Enum.cpp:5-21
 	typedef PhysicalQuantities::T Q;

@@ -53,6 +53,48 @@ std::string zeroPadded(int number, int length);
 /// mkdir -p of the directory part of `fileName`
 void makeParentDirectories(const std::string& fileName);
 
+/// VtkSnapshotter's arrays of one vertex list (VtkSnapshotter.hpp:28-70):
+/// "Velocity", the quantities by name, "material_index" -- name, components, values.
+struct VtkPointArray {
+	std::string name;
+	int components = 1;
+	std::vector<float> values;
+};
+
+namespace simplex {
+
+/// Write a VTK XML UnstructuredGrid (.vtu) file of tetrahedra (what
+/// vtkXMLUnstructuredGridWriter makes of VtkUtils' SimplexGrid output,
+/// VtkUtils.hpp:54-66, 140-160): points (3 floats per vertex), cells (4 vertex
+/// indices each, VTK_TETRA), the point arrays in order.  Appended raw binary.
+void writeVtu(const std::string& fileName, const std::vector<float>& points,
+              const std::vector<std::array<int, 4>>& cells, const std::vector<VtkPointArray>& arrays);
+
+/// VtkSnapshotter::snapshotImpl (VtkSnapshotter.hpp:20-61) for a simplex body:
+/// the vertex coordinates, pde [n][9], one material number for the body.  GPU-free.
+void writeVtkSnapshot(const std::string& fileName, const std::vector<Real3>& coords,
+                      const std::vector<std::array<int, 4>>& cells, const real* pde,
+                      int materialNumber, const std::vector<PhysicalQuantities::T>& quantities);
+
+/// The simplex VtkSnapshotter: file naming of Snapshotter (snapshots/vtk/mesh<id>
+/// core00snap<step>.vtu) on top of writeVtkSnapshot.
+class VtkSnapshotter : public Snapshotter {
+public:
+	explicit VtkSnapshotter(const Task& task)
+	    : Snapshotter(task), quantities(task.vtkSnapshotter.quantitiesToSnap) {}
+	std::string fileName(size_t meshId, int step) const {
+		return makeFileNameForSnapshot(std::to_string(meshId), step, "vtu", "vtk");
+	}
+	const std::vector<PhysicalQuantities::T> quantities;
+
+protected:
+	void snapshotImpl(const AbstractGrid*, const int) override {
+		throw Exception("simplex::VtkSnapshotter writes through simplex::Engine::writeSnapshots");
+	}
+};
+
+}  // namespace simplex
+
 namespace cubic {
 
 /// One named Float32 point array of a .vts file (components 1 or 3).

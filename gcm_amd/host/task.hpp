@@ -266,6 +266,11 @@ struct Task {
 	/// Task::SimplexGrid (Task.hpp:84-127) -- CGAL is absent, so the mesh is the
 	/// jittered Kuhn tetrahedralisation of a box (simplex::boxMesh).
 	struct SimplexGrid {
+		/// Task::SimplexGrid::Mesher (Task.hpp:86-90): BOX_MESHER (this build's
+		/// stand-in for CGAL_MESHER, absent) or INM_MESHER (fileName: points,
+		/// cells and per-cell grid ids, InmMeshLoader.hpp)
+		enum class Mesher { BOX_MESHER, INM_MESHER } mesher = Mesher::BOX_MESHER;
+		std::string fileName;
 		std::array<int, 3> cells = {0, 0, 0};  // cubes per axis
 		Real3 lo = {0, 0, 0}, hi = {1, 1, 1};
 		real jitter = 0;

@@ -91,3 +91,25 @@ def read_vts(path):
         arrays[name] = np.frombuffer(data[off + 8:off + 8 + nbytes], dtype="<f4").reshape(-1, int(comps))
     points = arrays.pop("Points")
     return dims, arrays, points
+
+
+def read_vtu(path):
+    """Parse a VTK XML UnstructuredGrid file with appended raw data (UInt64 headers)
+    as gcm_amd's simplex VtkSnapshotter writes it.  Returns ({name: array [n, c]},
+    points [n, 3], connectivity [m, 4], offsets [m], types [m])."""
+    import re
+    raw = open(path, "rb").read()
+    head, _, rest = raw.partition(b"<AppendedData encoding=\"raw\">")
+    text = head.decode()
+    data = rest[rest.index(b"_") + 1:]
+    dt = {"Float32": "<f4", "Int64": "<i8", "UInt8": "u1"}
+    arrays = {}
+    for typ, name, tail in re.findall(r'<DataArray type="(\w+)" Name="([^"]+)"([^/]*)/>', text):
+        off = int(re.search(r'offset="(\d+)"', tail).group(1))
+        comps = re.search(r'NumberOfComponents="(\d+)"', tail)
+        nbytes = int(np.frombuffer(data[off:off + 8], dtype="<u8")[0])
+        a = np.frombuffer(data[off + 8:off + 8 + nbytes], dtype=dt[typ])
+        arrays[name] = a.reshape(-1, int(comps.group(1))) if comps else a
+    points = arrays.pop("Points")
+    conn = arrays.pop("connectivity").reshape(-1, 4)
+    return arrays, points, conn, arrays.pop("offsets"), arrays.pop("types")

@@ -87,7 +87,8 @@ LAYER_MATERIALS = {0: (4.0, 2.0, 1.0), 1: (2.0, 1.0, 0.5)}
 
 
 def layered_task(n=6, courant=1.0, jitter=0.1, seed=7, border=None, snaps=3,
-                 materials=LAYER_MATERIALS, cavity=False):
+                 materials=LAYER_MATERIALS, inm=None):
+    """inm: load the mesh from this INM file (INM_MESHER) instead of the box mesher."""
     from gcm_amd import _gcm_host as H
     t = H.Task()
     t.dimensionality = 3
@@ -98,8 +99,11 @@ def layered_task(n=6, courant=1.0, jitter=0.1, seed=7, border=None, snaps=3,
         t.add_body(i, [1, 1, 1], [0, 0, 0])
         t.set_body_material(i, rho, lam, mu)
     t.calculation_basis = [1, 0, 0, 0, 1, 0, 0, 0, 1]
-    t.set_simplex_box([n, n, n], [0, 0, 0], [1, 1, 1], jitter, seed)
-    t.add_simplex_body_area(("box", (-1, -1, 0.5), (2, 2, 2)), 1)
+    if inm is None:
+        t.set_simplex_box([n, n, n], [0, 0, 0], [1, 1, 1], jitter, seed)
+        t.add_simplex_body_area(("box", (-1, -1, 0.5), (2, 2, 2)), 1)
+    else:
+        t.set_simplex_inm_mesh(str(inm))
     t.set_contact_condition("ADHESION")
     t.add_initial_quantity(("sphere", 0.3, (0.5, 0.5, 0.3)), "PRESSURE", 1.0)
     t.add_initial_vector(("box", (0.2, 0.2, 0.55), (0.8, 0.8, 0.9)),
@@ -116,3 +120,17 @@ def oracle_multi(plans, courant, border=FREE_BORDER, materials=LAYER_MATERIALS):
         bodies.append({"id": b["id"], "coords": b["coords"], "cells": b["cells"],
                        "global": b["global"], "U": U, "U1": U1, "L": L, "pde": b["pde"]})
     return S.MultiEngine(bodies, np.eye(3), courant, oracle_conditions(border))
+
+
+def write_inm(path, points, cells, materials):
+    """INM mesh text (InmMeshLoader.hpp:96-172): points, cells with 1-based vertices
+    and a material, terminating 0."""
+    with open(path, "w") as f:
+        f.write(f"{len(points)}\n")
+        for p in points:
+            f.write(" ".join(repr(float(x)) for x in p) + "\n")
+        f.write(f"{len(cells)}\n")
+        for c, m in zip(cells, materials):
+            f.write(" ".join(str(int(x) + 1) for x in c) + f" {int(m)}\n")
+        f.write("0\n")
+

@@ -6,6 +6,7 @@ mesh invariants the reference's own grid test checks (TestSimplexGrid.cpp:51-91:
 inner nodes have a zero border normal, border normals of a cube point along the
 face normals within 0.3).  Reference numerics parity is unpinned (CGAL absent)."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -336,3 +337,76 @@ def test_plain_contact_average_satisfies_adhesion():
     sig = lambda u: np.array([[u[3], u[4], u[5]], [u[4], u[6], u[7]], [u[5], u[7], u[8]]])
     assert np.allclose(uA[:3], uB[:3])
     assert np.allclose(sig(uA) @ n, sig(uB) @ n)
+
+
+def test_simplex_vtu_snapshot(H, tmp_path):
+    """VtkSnapshotter of a simplex body (VtkSnapshotter.hpp:20-61, VtkUtils.hpp:54-66,
+    140-160): an UnstructuredGrid of VTK_TETRA cells over the mesh vertices with
+    "Velocity", the quantities to snap and "material_index" (Float32)."""
+    from tests.helpers import read_vtu
+    t = layered_task(4, 1.0)
+    t.set_vtk_quantities(["PRESSURE", "Sxy"])
+    p = H.simplex_plans(t)
+    for body in (0, 1):
+        b = p["bodies"][body]
+        path = str(tmp_path / f"s{body}.vtu")
+        rng = np.random.default_rng(body)
+        layer = rng.standard_normal((len(b["coords"]), 9))
+        H.write_simplex_vtk(t, path, layer, body)
+        arrays, pts, conn, offs, types = read_vtu(path)
+        assert np.array_equal(pts, b["coords"].astype(np.float32))
+        assert np.array_equal(conn, b["cells"]) and (types == 10).all()
+        assert np.array_equal(offs, 4 * np.arange(1, len(conn) + 1))
+        assert list(arrays) == ["Velocity", "pressure", "Sxy", "material_index"]
+        assert np.array_equal(arrays["Velocity"], layer[:, :3].astype(np.float32))
+        pres = -(layer[:, 3] + layer[:, 6] + layer[:, 8]) / 3
+        assert np.array_equal(arrays["pressure"][:, 0], pres.astype(np.float32))
+        assert np.array_equal(arrays["Sxy"][:, 0], layer[:, 4].astype(np.float32))
+
+
+# ---- INM_MESHER ----------------------------------------------------------------
+
+INM_FIXTURE = os.path.join(os.path.dirname(__file__), "golden", "testInmLoader.out")
+
+
+def test_inm_reader_known_answers(H):
+    """TestInmMeshLoader.readFromFile (TestInmMeshLoader.cpp:19-68) on the reference's
+    meshes/testInmLoader.out (copied as a fixture)."""
+    P, C, M = H.read_inm(INM_FIXTURE)
+    assert P.shape == (12, 3) and len(C) == 3
+    assert abs(P[3][0] - -2.583210754394531250e+01) < 1e-9
+    assert abs(P[4][0] - 2.400143432617187500e+01) < 1e-9
+    assert abs(P[11][0] - -6.843022155761718750e+01) < 1e-9
+    assert abs(P[0][1] - 4.283624267578125000e+01) < 1e-9
+    assert abs(P[11][1] - 3.788503265380859375e+01) < 1e-9
+    assert abs(P[0][2] - 1.406894775390625000e+03) < 1e-9
+    mats = {tuple(sorted(c)): m for c, m in zip(C, M)}
+    assert mats == {(1, 2, 3, 4): 4, (5, 6, 7, 8): 5, (9, 10, 11, 12): 1}
+
+
+def test_inm_mesher_reproduces_the_triangulation(H, tmp_path):
+    """A triangulation written as an INM file and loaded through INM_MESHER gives the
+    same bodies, plans and contacts as the mesher that made it."""
+    from tests.simplex_spec import write_inm
+    t = layered_task(5, 1.3)
+    P, C, G = H.simplex_triangulation(t)
+    path = tmp_path / "layers.out"
+    write_inm(path, P, C, G)
+    a, b = H.simplex_plans(t), H.simplex_plans(layered_task(5, 1.3, inm=path))
+    assert a["tau"] == b["tau"]
+    for x, y in zip(a["bodies"], b["bodies"]):
+        for k in ("coords", "cells", "pde", "inner", "border", "contact", "global"):
+            assert np.array_equal(np.array(x[k]), np.array(y[k])), k
+        for s in range(3):
+            assert np.array_equal(x["stages"][s]["kind"], y["stages"][s]["kind"])
+            assert np.array_equal(x["stages"][s]["lam"], y["stages"][s]["lam"])
+    assert a["contacts"][0]["code_a"] == b["contacts"][0]["code_a"]
+
+
+def test_inm_mesher_rejects_unknown_materials(H, tmp_path):
+    from tests.simplex_spec import write_inm
+    P, C, G = H.simplex_triangulation(layered_task(3))
+    path = tmp_path / "bad.out"
+    write_inm(path, P, C, [7] * len(C))
+    with pytest.raises(Exception):
+        H.simplex_plans(layered_task(3, inm=path))
