@@ -76,6 +76,14 @@ struct PyEngine {
 		return out;
 	}
 	void runSteps(int n) { e->runSteps(n); }
+	/// wait for a body's device work (timing)
+	void sync(size_t id) {
+		gcmx_ctx* c = nullptr;
+		if (D == 1) c = as<1>().getMesh(id)->ctx();
+		else if (D == 2) c = as<2>().getMesh(id)->ctx();
+		else c = as<3>().getMesh(id)->ctx();
+		gcmxCheck(gcmx_sync(c), "gcmx_sync");
+	}
 	std::string path(size_t id) {
 		gcmx_ctx* c = nullptr;
 		if (D == 1) c = as<1>().getMesh(id)->ctx();
@@ -499,6 +507,7 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    .def("run_steps", &PyEngine::runSteps)
 	    .def("pde", &PyEngine::pde, "current layer of a body, all nodes incl. ghosts [..., M]")
 	    .def("path", &PyEngine::path)
+	    .def("sync", &PyEngine::sync, py::arg("body") = 0)
 	    .def("maximal_eigenvalue", &PyEngine::maximalEigenvalue)
 	    .def_property_readonly("steps", [](PyEngine& p) { return p.e->stepsDone(); })
 	    .def_property_readonly("required_time", [](PyEngine& p) { return p.e->getRequiredTime(); })

@@ -1,0 +1,63 @@
+"""Throughput of a physical cubic run: free surfaces on all six faces (cubic
+BorderConditions, engine/cubic/BorderConditions.hpp:81-114), optionally the
+Maxwell viscosity ODE (rheology/ode/MaxwellViscosityOde.hpp), through the C++
+engine (cubic::Engine<3>::nextTimeStep: border fill -> stage -> swap per axis,
+then the ODEs).  Border conditions change the ghosts every stage, so the engine
+runs the per-stage kernels (split path) instead of the one-pass fused step.
+
+    python scripts/bench_physics.py [--n 256] [--steps 10] [--maxwell]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+FACE_FORCE = {0: ["Sxx", "Sxy", "Sxz"], 1: ["Sxy", "Syy", "Syz"], 2: ["Sxz", "Syz", "Szz"]}
+
+
+def task(n, maxwell):
+    from gcm_amd import _gcm_host as H
+    t = H.Task()
+    t.dimensionality = 3
+    t.border_size = 2
+    t.h = [1.0, 1.0, 1.0]
+    t.courant = 0.9
+    t.number_of_snaps = 10 ** 6
+    t.add_body(0, [n, n, n], [0, 0, 0])
+    t.set_default_material(4.0, 2.0, 1.0, tau0=50.0 if maxwell else 0.0)
+    t.add_initial_quantity(("sphere", n / 4, (n / 2, n / 2, n / 2)), "PRESSURE", 10.0)
+    for d, qs in FACE_FORCE.items():  # free surface: zero traction on both faces of axis d
+        t.add_border_condition(0, d, ("infinite",), {q: (lambda time: 0.0) for q in qs})
+    if maxwell:
+        t.add_ode(0, "MAXWELL_VISCOSITY")
+    return t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--maxwell", action="store_true")
+    a = ap.parse_args()
+    from gcm_amd import _gcm_host as H
+    e = H.Engine(task(a.n, a.maxwell))
+    e.run_steps(a.warmup)
+    e.sync()
+    t0 = time.perf_counter()
+    e.run_steps(a.steps)
+    e.sync()
+    dt = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "Mnode-steps/s, cubic engine with free surfaces" + (" + Maxwell ODE" if a.maxwell else ""),
+        "value": round(a.n ** 3 * a.steps / dt / 1e6, 1), "unit": "Mnode-steps/s",
+        "ms_per_step": round(dt / a.steps * 1e3, 4), "n": a.n, "steps": a.steps,
+        "path": e.path(0), "dtype": "f64"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
