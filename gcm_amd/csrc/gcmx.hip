@@ -60,7 +60,10 @@ struct gcmx_ctx {
 	int device = 0;
 	hipStream_t stream = nullptr;
 	hipStream_t comm_stream = nullptr;
+	hipStream_t inner_stream = nullptr;  // interior planes of the X-slab schedule (low priority)
+	hipStream_t bnd_stream = nullptr;    // right boundary planes of the X-slab schedule
 	hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_bnd = nullptr;
 	gcmx_grid_desc desc{};
 	Geo geo{};
 	int D = 0, M = 0, bs = 0;
@@ -423,10 +426,20 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 		gcmx_destroy(c);
 		return fail(GCMX_ERR_OOM, "device allocation failed");
 	}
-	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-	    hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking) != hipSuccess ||
+	// Main stream at the highest priority, the interior-plane stream at the
+	// lowest: the boundary planes of a slab step (and the halo they feed) are
+	// dispatched ahead of the interior blocks that run beside them.
+	int prio_lo = 0, prio_hi = 0;
+	if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+	if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+	    hipStreamCreateWithPriority(&c->inner_stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+	    hipStreamCreateWithPriority(&c->bnd_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+	    hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
 	    hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
-	    hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming) != hipSuccess) {
+	    hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming) != hipSuccess ||
+	    hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+	    hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+	    hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming) != hipSuccess) {
 		gcmx_destroy(c);
 		return fail(GCMX_ERR_HIP, "stream/event creation failed");
 	}
@@ -445,6 +458,8 @@ void gcmx_destroy(gcmx_ctx* c) {
 	hipSetDevice(c->device);
 	if (c->stream) hipStreamSynchronize(c->stream);
 	if (c->comm_stream) hipStreamSynchronize(c->comm_stream);
+	if (c->inner_stream) hipStreamSynchronize(c->inner_stream);
+	if (c->bnd_stream) hipStreamSynchronize(c->bnd_stream);
 	drain_timings(c);
 	if (c->comm) ncclCommDestroy(c->comm);
 	hipFree(c->cur);
@@ -457,8 +472,13 @@ void gcmx_destroy(gcmx_ctx* c) {
 	hipFree(c->ode_d);
 	if (c->ev_ready) hipEventDestroy(c->ev_ready);
 	if (c->ev_halo) hipEventDestroy(c->ev_halo);
+	if (c->ev_fork) hipEventDestroy(c->ev_fork);
+	if (c->ev_join) hipEventDestroy(c->ev_join);
+	if (c->ev_bnd) hipEventDestroy(c->ev_bnd);
 	if (c->stream) hipStreamDestroy(c->stream);
 	if (c->comm_stream) hipStreamDestroy(c->comm_stream);
+	if (c->inner_stream) hipStreamDestroy(c->inner_stream);
+	if (c->bnd_stream) hipStreamDestroy(c->bnd_stream);
 	delete c;
 }
 
@@ -643,6 +663,25 @@ static bool use_xyz() {
 	return on;
 }
 
+// GCMX_SLAB_SCHEDULE=1: run the X-slab step schedule (interior / boundary
+// planes on two streams) without a communicator, to time it on one GPU.
+static int slab_schedule_mode() {
+	static const int m = [] {
+		const char* e = std::getenv("GCMX_SLAB_SCHEDULE");
+		return e ? std::atoi(e) : 0;
+	}();
+	return m;
+}
+
+// GCMX_XYZ_ROWS=<n>: force the fused kernel's rows per block (tuning only).
+static int xyz_rows_forced() {
+	static const int v = [] {
+		const char* e = std::getenv("GCMX_XYZ_ROWS");
+		return e ? std::atoi(e) : 0;
+	}();
+	return v;
+}
+
 gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
@@ -673,31 +712,55 @@ gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 		// One pass per step (cur -> nxt, then swap).  Ghost planes of `cur` must
 		// hold E_n; the exchange of the NEW boundary planes (E_{n+1}, into the
 		// ghost planes of `nxt`) runs while the interior planes are computed.
-		auto xyz = [&](int x0, int x1) {
-			Timed t(c, "fused_xyz", plane_bytes * (x1 - x0), c->stream);
-			return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, c->stream);
+		auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int chunk) {
+			Timed t(c, name, plane_bytes * (x1 - x0), st);
+			return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, chunk);
 		};
-		if (halo && X >= 4 * bs) {
-			if (!c->halo_pending) {
+		if (slab_schedule_mode() == 2 && !halo && X >= 4 * bs) {
+			// A/B reference only (GCMX_SLAB_SCHEDULE=2, no communicator): the
+			// earlier one-stream schedule, boundary planes then interior.
+			ok = xyz("fused_xyz_boundary", 0, bs, c->stream, 0) &&
+			     xyz("fused_xyz_boundary", X - bs, X, c->stream, 0) &&
+			     xyz("fused_xyz", bs, X - bs, c->stream, 0);
+		} else if ((halo || slab_schedule_mode() == 1) && X >= 4 * bs) {
+			// X-slab schedule.  The interior planes [bs, X-bs) read no ghost plane:
+			// they start at once on the low-priority inner stream, ordered only
+			// after the previous step (ev_fork), not after the halo.  The boundary
+			// planes wait for the halo, run on the high-priority main stream in
+			// thin 16-row blocks (they finish early, so the exchange of the NEW
+			// boundary planes overlaps the interior), then the main stream joins
+			// the interior.  Buffers: the interior writes nxt's inner planes only,
+			// the halo writes nxt's ghost planes (no overlap); both read cur.
+			HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+			HIP_TRY(hipStreamWaitEvent(c->inner_stream, c->ev_fork, 0));
+			ok = xyz("fused_xyz", bs, X - bs, c->inner_stream, xyz_rows_forced());
+			HIP_TRY(hipEventRecord(c->ev_join, c->inner_stream));
+			if (ok && halo && !c->halo_pending) {
 				s = halo_post(c);
 				if (s) return s;
 			}
 			s = halo_wait(c);
 			if (s) return s;
-			ok = xyz(0, bs) && xyz(X - bs, X);
+			// the two boundary sides run side by side (main + bnd stream)
+			HIP_TRY(hipEventRecord(c->ev_bnd, c->stream));
+			HIP_TRY(hipStreamWaitEvent(c->bnd_stream, c->ev_bnd, 0));
+			ok = ok && xyz("fused_xyz_boundary", 0, bs, c->stream, 16) &&
+			     xyz("fused_xyz_boundary", X - bs, X, c->bnd_stream, 16);
+			HIP_TRY(hipEventRecord(c->ev_bnd, c->bnd_stream));
+			HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
 			if (ok) {
 				std::swap(c->cur, c->nxt);  // E_{n+1} exchanges the new layer
 				s = halo_post(c);
 				std::swap(c->cur, c->nxt);
 				if (s) return s;
-				ok = xyz(bs, X - bs);
 			}
+			HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
 		} else {
 			if (halo) {
 				s = halo_exchange_impl(c);
 				if (s) return s;
 			}
-			ok = xyz(0, X);
+			ok = xyz("fused_xyz", 0, X, c->stream, xyz_rows_forced());
 		}
 		if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
 		HIP_TRY(hipGetLastError());

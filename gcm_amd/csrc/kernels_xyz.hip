@@ -47,6 +47,9 @@ namespace gcmx {
 #ifndef GCMX_XYZ_GROUPED
 #define GCMX_XYZ_GROUPED 2
 #endif
+#ifndef GCMX_XYZ_LATE_STORE
+#define GCMX_XYZ_LATE_STORE 0
+#endif
 #ifndef GCMX_XYZ_UNI
 #define GCMX_XYZ_UNI 1
 #endif
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #endif
 	};
 	// (split so that the first pair's loads can be issued ahead of the stores)
-	auto x_stage_grouped_ab = [&](PairWin& wa, PairWin& wb, int r, double (&xr)[9]) {
+	auto x_stage_grouped_ab = [&](PairWin& wa, PairWin& wb, int r, double (&xr)[9], auto&& mid) {
 		const unsigned o = base + (unsigned)r * sty;
 		using P0 = std::integral_constant<int, 0>;
 		using P1 = std::integral_constant<int, 1>;
@@ -220,6 +223,7 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #pragma unroll
 		for (int j = 0; j < 9; j++)
 			if ((CMX >> j) & 1u) cv[j] = src.ld(j, o);
+		mid();
 		pair_update<0, BS, KF0, 2>(AX, pair_acc(P2{}, wa), rr[4], rr[5]);
 		n0[pair_vel(0, 2)] = wa[0][BS];
 		n0[pair_sig(0, 2)] = wa[1][BS];
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 	auto x_stage_grouped_rest = [&](PairWin& wa, int r, double (&xr)[9]) {
 		PairWin wb;
 		pair_load(std::integral_constant<int, 1>{}, wb, base + (unsigned)r * sty);
-		x_stage_grouped_ab(wa, wb, r, xr);
+		x_stage_grouped_ab(wa, wb, r, xr, [] {});
 	};
 	auto x_load_a = [&](PairWin& wa, int r) {
 		pair_load(std::integral_constant<int, 0>{}, wa, base + (unsigned)r * sty);
@@ -298,11 +302,59 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #pragma unroll
 		for (int j = 0; j < 9; j++)
 			if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = live ? yv[j] : 0.0;
+#if GCMX_XYZ_GROUPED >= 2
+		PairWin wa_next;
+#endif
+#if GCMX_XYZ_GROUPED == 4
+		// Early schedule: the next X row's first pair is issued before the
+		// barrier (the Z stage hides its latency), the second pair before this
+		// row's stores, so the waits of both exclude the stores.
+		const int rn = clamp_row(y + BS + 1);
+		sched_fence();
+		x_load_a(wa_next, rn);
+		sched_fence();
+#endif
 #if !GCMX_DIAG_NOBAR
 		__syncthreads();
 #endif
-#if GCMX_XYZ_GROUPED >= 2
-		PairWin wa_next;
+#if GCMX_XYZ_GROUPED == 4
+		{
+			double zv[9];
+			node_update<2, BS, KF0>(
+			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
+			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
+			PairWin wb_next;
+			sched_fence();
+			pair_load(std::integral_constant<int, 1>{}, wb_next, base + (unsigned)rn * sty);
+			sched_fence();
+			const unsigned offo = plane + (unsigned)y * sty + zo;
+			auto stores = [&] {
+#pragma unroll
+				for (int c = 0; c < 9; c++) XYZ_ST(c, offo, live ? zv[c] : 0.0);
+			};
+#if GCMX_XYZ_LATE_STORE == 0
+			stores();
+#endif
+			buf ^= 1;
+#pragma unroll
+			for (int q = 0; q < NWY; q++)
+#pragma unroll
+				for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
+#pragma unroll
+			for (int k = 0; k < BS; k++)
+#pragma unroll
+				for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
+			double xr[9];
+			sched_fence();
+#if GCMX_XYZ_LATE_STORE == 0
+			x_stage_grouped_ab(wa_next, wb_next, rn, xr, [] {});
+#else  // stores after every load of the next row is issued (zv stays live longer)
+			x_stage_grouped_ab(wa_next, wb_next, rn, xr, [&] { sched_fence(); stores(); sched_fence(); });
+#endif
+			push(xr, W - 1);
+			sched_fence();
+		}
+		continue;
 #endif
 #if GCMX_XYZ_GROUPED == 3
 		PairWin wb_next;
@@ -347,7 +399,7 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 			double xr[9];
 #if GCMX_XYZ_GROUPED == 3
 			sched_fence();
-			x_stage_grouped_ab(wa_next, wb_next, clamp_row(y + BS + 1), xr);
+			x_stage_grouped_ab(wa_next, wb_next, clamp_row(y + BS + 1), xr, [] {});
 			push(xr, W - 1);
 			sched_fence();
 #elif GCMX_XYZ_GROUPED == 2
@@ -463,10 +515,22 @@ static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
 
 static int xyz_chunk(int Y) { return Y <= GCMX_XYZ_CHUNK ? Y : GCMX_XYZ_CHUNK; }
 
+// Rows per block: GCMX_XYZ_CHUNK (128) while the launch still has >= 1024 blocks
+// (two rounds of the 512 resident blocks, 2 per CU); thinner slabs (multi-GPU
+// X slabs, the boundary planes) halve it, down to 16 rows, to keep every CU
+// busy.  Each block recomputes 2*BS X rows in its prologue, so a chunk of c
+// rows costs (c + 2*BS) / c of the X stage.  `req` > 0 forces a value.
+static int xyz_chunk_for(int Y, int nplanes, int req) {
+	int chunk = req > 0 ? req : GCMX_XYZ_CHUNK;
+	if (req <= 0)
+		while (chunk > 16 && (long long)((Y + chunk - 1) / chunk) * nplanes < 1024) chunk /= 2;
+	return Y <= chunk ? Y : chunk;
+}
+
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                         int x1, hipStream_t st) {
-	const int chunk = xyz_chunk(g.sizes[1]);
+                         int x1, hipStream_t st, int req_chunk) {
+	const int chunk = xyz_chunk_for(g.sizes[1], x1 - x0, req_chunk);
 	const int nchunks = (g.sizes[1] + chunk - 1) / chunk;
 #if GCMX_XYZ_SWIZZLE && !GCMX_DIAG_HALFZ
 	dim3 grid(nchunks * (x1 - x0));
@@ -489,18 +553,18 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 
 template <int BS>
 static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                          int x1, hipStream_t st) {
+                          int x1, hipStream_t st, int ch) {
 	const int Z = g.sizes[2];
-	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st);
-	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st);
-	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st);
-	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st);
-	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st);
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st, ch);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st, ch);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st, ch);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st, ch);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st, ch);
 	return true;
 }
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                      int x1, hipStream_t st) {
+                      int x1, hipStream_t st, int chunk) {
 	if (!fused_yz_supported(g) || x1 <= x0) return false;
 #ifdef GCMX_TUNE_FAST  // tuning builds: the bench configuration only
 	if (g.bs != 2 || g.sizes[2] <= 256 || g.sizes[2] > 512) return false;
@@ -513,13 +577,13 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 		return true;
 	}
 #endif
-	launch_xyz_t<2, 512>(in, out, g, a, x0, x1, st);
+	launch_xyz_t<2, 512>(in, out, g, a, x0, x1, st, chunk);
 	return true;
 #endif
 	switch (g.bs) {
-	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st);
-	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st);
-	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st);
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st, chunk);
 	default: return false;
 	}
 }

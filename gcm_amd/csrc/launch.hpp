@@ -43,7 +43,8 @@ bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis&
                      const IsoAxis& az, int x0, int x1, hipStream_t st);
 bool fused_yz_supported(const Geo& g);
 // One pass per time step: X, Y, Z stages of planes [x0, x1), `a` = the three axes.
+// `chunk`: y rows per block (0 = automatic, kernels_xyz.hip: xyz_chunk_for).
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                      int x1, hipStream_t st);
+                      int x1, hipStream_t st, int chunk = 0);
 
 }  // namespace gcmx
