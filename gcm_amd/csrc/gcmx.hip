@@ -82,6 +82,8 @@ struct gcmx_ctx {
 	IsoAxis iso[3] = {};           // per-axis values for the fast kernels (tau part in build_tables)
 	bool ghosts_touched = false;   // border fills / contact copies happened
 	gcmx_path path = GCMX_PATH_AUTO;
+	gcmx_schedule sched = GCMX_SCHED_AUTO;
+	int rows_per_block = 0;        // fused kernel y rows per block (0 = automatic)
 	// halo exchange
 	ncclComm_t comm = nullptr;
 	int nranks = 1, rank = 0, left = -1, right = -1;
@@ -91,6 +93,7 @@ struct gcmx_ctx {
 	bool prof = false;
 	std::vector<Bucket> buckets;
 	std::vector<PendingTiming> pending;
+	std::vector<hipEvent_t> event_pool;  // recycled timing events (no create/destroy per launch)
 	// scratch for border fills
 	int* nodes_d = nullptr;
 	size_t nodes_cap = 0;
@@ -108,6 +111,17 @@ int bucket_id(gcmx_ctx* c, const char* name) {
 	return (int)c->buckets.size() - 1;
 }
 
+hipEvent_t take_event(gcmx_ctx* c) {
+	hipEvent_t ev = nullptr;
+	if (!c->event_pool.empty()) {
+		ev = c->event_pool.back();
+		c->event_pool.pop_back();
+	} else {
+		hipEventCreate(&ev);
+	}
+	return ev;
+}
+
 // Bracket one launch with events when profiling.
 struct Timed {
 	gcmx_ctx* c;
@@ -119,8 +133,8 @@ struct Timed {
 	    : c(c_), b(-1), bytes(bytes_), st(s) {
 		if (!c->prof) return;
 		b = bucket_id(c, name);
-		hipEventCreate(&a);
-		hipEventCreate(&e);
+		a = take_event(c);
+		e = take_event(c);
 		hipEventRecord(a, st);
 	}
 	~Timed() {
@@ -138,8 +152,8 @@ void drain_timings(gcmx_ctx* c) {
 		c->buckets[p.bucket].total_ms += ms;
 		c->buckets[p.bucket].launches += 1;
 		c->buckets[p.bucket].bytes += p.bytes;
-		hipEventDestroy(p.a);
-		hipEventDestroy(p.b);
+		c->event_pool.push_back(p.a);
+		c->event_pool.push_back(p.b);
 	}
 	c->pending.clear();
 }
@@ -256,20 +270,28 @@ gcmx_status halo_post(gcmx_ctx* c) {
 	};
 	HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
 	HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-	if (ncclGroupStart() != ncclSuccess) return fail(GCMX_ERR_COMM, "ncclGroupStart");
+	ncclResult_t r = ncclGroupStart();
+	if (r != ncclSuccess) return fail(GCMX_ERR_COMM, std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+	// Every failure inside the group still closes it (an open group would
+	// corrupt every later call on the communicator).
+	std::string what;
 	for (int comp : c->halo_comps) {
-		if (c->left >= 0) {
-			if (ncclSend(plane_ptr(comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream) != ncclSuccess ||
-			    ncclRecv(plane_ptr(comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream) != ncclSuccess)
-				return fail(GCMX_ERR_COMM, "ncclSend/Recv left");
+		if (r == ncclSuccess && c->left >= 0) {
+			what = "ncclSend/Recv left";
+			r = ncclSend(plane_ptr(comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream);
+			if (r == ncclSuccess)
+				r = ncclRecv(plane_ptr(comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream);
 		}
-		if (c->right >= 0) {
-			if (ncclSend(plane_ptr(comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream) != ncclSuccess ||
-			    ncclRecv(plane_ptr(comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream) != ncclSuccess)
-				return fail(GCMX_ERR_COMM, "ncclSend/Recv right");
+		if (r == ncclSuccess && c->right >= 0) {
+			what = "ncclSend/Recv right";
+			r = ncclSend(plane_ptr(comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream);
+			if (r == ncclSuccess)
+				r = ncclRecv(plane_ptr(comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream);
 		}
 	}
-	if (ncclGroupEnd() != ncclSuccess) return fail(GCMX_ERR_COMM, "ncclGroupEnd");
+	const ncclResult_t re = ncclGroupEnd();
+	if (r != ncclSuccess) return fail(GCMX_ERR_COMM, what + ": " + ncclGetErrorString(r));
+	if (re != ncclSuccess) return fail(GCMX_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
 	HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
 	c->halo_pending = true;
 	return GCMX_OK;
@@ -305,7 +327,7 @@ gcmx_path effective_path(gcmx_ctx* c) {
 	if (c->D != 3 || !c->iso_fast || c->bs > 3) return GCMX_PATH_GENERIC;
 	if (c->path == GCMX_PATH_GENERIC) return GCMX_PATH_GENERIC;
 	if (c->path == GCMX_PATH_SPLIT) return GCMX_PATH_SPLIT;
-	if (c->ghosts_touched || !fused_yz_supported(c->geo)) return GCMX_PATH_SPLIT;
+	if (c->ghosts_touched || !fused_supported(c->geo)) return GCMX_PATH_SPLIT;
 	return GCMX_PATH_FUSED;
 }
 
@@ -461,6 +483,7 @@ void gcmx_destroy(gcmx_ctx* c) {
 	if (c->inner_stream) hipStreamSynchronize(c->inner_stream);
 	if (c->bnd_stream) hipStreamSynchronize(c->bnd_stream);
 	drain_timings(c);
+	for (hipEvent_t ev : c->event_pool) hipEventDestroy(ev);
 	if (c->comm) ncclCommDestroy(c->comm);
 	hipFree(c->cur);
 	hipFree(c->nxt);
@@ -653,34 +676,23 @@ gcmx_status gcmx_stage(gcmx_ctx* c, int axis, double tau) {
 	return stage_impl(c, axis, tau);
 }
 
-// GCMX_FUSED_XYZ=0 selects the two-pass fused schedule (march X + fused Y/Z);
-// default is the one-pass k_fused_xyz.
-static bool use_xyz() {
-	static const bool on = [] {
-		const char* e = std::getenv("GCMX_FUSED_XYZ");
-		return !(e && e[0] == '0');
-	}();
-	return on;
-}
-
-// GCMX_SLAB_SCHEDULE=1: run the X-slab step schedule (interior / boundary
-// planes on two streams) without a communicator, to time it on one GPU.
-static int slab_schedule_mode() {
-	static const int m = [] {
-		const char* e = std::getenv("GCMX_SLAB_SCHEDULE");
-		return e ? std::atoi(e) : 0;
-	}();
-	return m;
-}
-
-// GCMX_XYZ_ROWS=<n>: force the fused kernel's rows per block (tuning only).
-static int xyz_rows_forced() {
-	static const int v = [] {
-		const char* e = std::getenv("GCMX_XYZ_ROWS");
-		return e ? std::atoi(e) : 0;
-	}();
-	return v;
-}
+// Joins the side streams of the X-slab schedule back into the context stream
+// on every exit from gcmx_step, error returns included: later calls (download,
+// upload, the next step) are ordered on c->stream only.
+struct SlabJoin {
+	gcmx_ctx* c;
+	bool inner = false, bnd = false;
+	~SlabJoin() {
+		if (bnd) {
+			hipEventRecord(c->ev_bnd, c->bnd_stream);
+			hipStreamWaitEvent(c->stream, c->ev_bnd, 0);
+		}
+		if (inner) {
+			hipEventRecord(c->ev_join, c->inner_stream);
+			hipStreamWaitEvent(c->stream, c->ev_join, 0);
+		}
+	}
+};
 
 gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 	gcmx_status s = check_ctx(c);
@@ -695,108 +707,76 @@ gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 		}
 		return GCMX_OK;
 	}
+	// One pass per step (k_fused_xyz: cur -> nxt, then swap).  Ghost planes of
+	// `cur` must hold E_n; with the X-slab schedule the exchange of the NEW
+	// boundary planes (E_{n+1}, into the ghost planes of `nxt`) runs while the
+	// interior planes are computed.
 	const Geo& g = c->geo;
 	const int X = g.sizes[0], bs = c->bs;
 	const double plane_bytes = node_stage_bytes(c) * (double)g.sizes[1] * g.sizes[2];
-	auto march = [&](int x0, int x1) {
-		Timed t(c, "march_x", plane_bytes * (x1 - x0), c->stream);
-		return launch_march(c->cur, c->nxt, g, 0, c->iso[0], x0, x1, c->stream);
-	};
-	auto fused = [&](int x0, int x1) {
-		Timed t(c, "fused_yz", plane_bytes * (x1 - x0), c->stream);
-		return launch_fused_yz(c->nxt, c->cur, g, c->iso[1], c->iso[2], x0, x1, c->stream);
-	};
 	const bool halo = c->comm && (c->left >= 0 || c->right >= 0);
+	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows) {
+		Timed t(c, name, plane_bytes * (x1 - x0), st);
+		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows);
+	};
+	const gcmx_schedule sched =
+	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_XSLAB : GCMX_SCHED_SINGLE) : c->sched;
 	bool ok = true;
-	if (use_xyz()) {
-		// One pass per step (cur -> nxt, then swap).  Ghost planes of `cur` must
-		// hold E_n; the exchange of the NEW boundary planes (E_{n+1}, into the
-		// ghost planes of `nxt`) runs while the interior planes are computed.
-		auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int chunk) {
-			Timed t(c, name, plane_bytes * (x1 - x0), st);
-			return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, chunk);
-		};
-		if (slab_schedule_mode() == 2 && !halo && X >= 4 * bs) {
-			// A/B reference only (GCMX_SLAB_SCHEDULE=2, no communicator): the
-			// earlier one-stream schedule, boundary planes then interior.
-			ok = xyz("fused_xyz_boundary", 0, bs, c->stream, 0) &&
-			     xyz("fused_xyz_boundary", X - bs, X, c->stream, 0) &&
-			     xyz("fused_xyz", bs, X - bs, c->stream, 0);
-		} else if ((halo || slab_schedule_mode() == 1) && X >= 4 * bs) {
-			// X-slab schedule.  The interior planes [bs, X-bs) read no ghost plane:
-			// they start at once on the low-priority inner stream, ordered only
-			// after the previous step (ev_fork), not after the halo.  The boundary
-			// planes wait for the halo, run on the high-priority main stream in
-			// thin 16-row blocks (they finish early, so the exchange of the NEW
-			// boundary planes overlaps the interior), then the main stream joins
-			// the interior.  Buffers: the interior writes nxt's inner planes only,
-			// the halo writes nxt's ghost planes (no overlap); both read cur.
-			HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-			HIP_TRY(hipStreamWaitEvent(c->inner_stream, c->ev_fork, 0));
-			ok = xyz("fused_xyz", bs, X - bs, c->inner_stream, xyz_rows_forced());
-			HIP_TRY(hipEventRecord(c->ev_join, c->inner_stream));
-			if (ok && halo && !c->halo_pending) {
-				s = halo_post(c);
-				if (s) return s;
-			}
-			s = halo_wait(c);
-			if (s) return s;
-			// the two boundary sides run side by side (main + bnd stream)
-			HIP_TRY(hipEventRecord(c->ev_bnd, c->stream));
-			HIP_TRY(hipStreamWaitEvent(c->bnd_stream, c->ev_bnd, 0));
-			ok = ok && xyz("fused_xyz_boundary", 0, bs, c->stream, 16) &&
-			     xyz("fused_xyz_boundary", X - bs, X, c->bnd_stream, 16);
-			HIP_TRY(hipEventRecord(c->ev_bnd, c->bnd_stream));
-			HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
-			if (ok) {
-				std::swap(c->cur, c->nxt);  // E_{n+1} exchanges the new layer
-				s = halo_post(c);
-				std::swap(c->cur, c->nxt);
-				if (s) return s;
-			}
-			HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
-		} else {
-			if (halo) {
-				s = halo_exchange_impl(c);
-				if (s) return s;
-			}
-			ok = xyz("fused_xyz", 0, X, c->stream, xyz_rows_forced());
-		}
-		if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
-		HIP_TRY(hipGetLastError());
-		std::swap(c->cur, c->nxt);
-		return GCMX_OK;
-	}
-	if (halo && X >= 4 * bs) {
-		// Boundary planes first, exchange overlapped with interior work:
-		//   [E_n in flight] X-stage interior planes [bs, X-bs) need no ghosts;
-		//   wait E_n; X-stage boundary planes; Y/Z boundary planes; post E_{n+1}
-		//   (sends the new boundary planes, receives the next ghosts); Y/Z interior.
-		if (!c->halo_pending) {
+	if (sched == GCMX_SCHED_XSLAB && X >= 4 * bs) {
+		// X-slab schedule.  The interior planes [bs, X-bs) read no ghost plane:
+		// they start at once on the low-priority inner stream, ordered only
+		// after the previous step (ev_fork), not after the halo.  The boundary
+		// planes wait for the halo and run side by side on the high-priority
+		// main and boundary streams in thin 16-row blocks (they finish early, so
+		// the exchange of the NEW boundary planes overlaps the interior); then
+		// the main stream joins both.  Buffers: the interior writes nxt's inner
+		// planes only, the halo writes nxt's ghost planes (no overlap); both read cur.
+		SlabJoin join{c};
+		HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+		HIP_TRY(hipStreamWaitEvent(c->inner_stream, c->ev_fork, 0));
+		join.inner = true;
+		ok = xyz("fused_xyz", bs, X - bs, c->inner_stream, c->rows_per_block);
+		if (ok && halo && !c->halo_pending) {
 			s = halo_post(c);
 			if (s) return s;
 		}
-		ok = march(bs, X - bs);
-		if (ok) {
-			s = halo_wait(c);
-			if (s) return s;
-			ok = march(0, bs) && march(X - bs, X) && fused(0, bs) && fused(X - bs, X);
-		}
-		if (ok) {
+		s = halo_wait(c);
+		if (s) return s;
+		HIP_TRY(hipEventRecord(c->ev_bnd, c->stream));
+		HIP_TRY(hipStreamWaitEvent(c->bnd_stream, c->ev_bnd, 0));
+		join.bnd = true;
+		ok = ok && xyz("fused_xyz_boundary", 0, bs, c->stream, 16) &&
+		     xyz("fused_xyz_boundary", X - bs, X, c->bnd_stream, 16);
+		HIP_TRY(hipEventRecord(c->ev_bnd, c->bnd_stream));
+		HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
+		join.bnd = false;
+		if (ok && halo) {
+			std::swap(c->cur, c->nxt);  // E_{n+1} exchanges the new layer
 			s = halo_post(c);
+			std::swap(c->cur, c->nxt);
 			if (s) return s;
-			ok = fused(bs, X - bs);
 		}
 	} else {
 		if (halo) {
 			s = halo_exchange_impl(c);
 			if (s) return s;
 		}
-		ok = march(0, X) && fused(0, X);
+		ok = xyz("fused_xyz", 0, X, c->stream, c->rows_per_block);
 	}
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
 	HIP_TRY(hipGetLastError());
-	// X: cur -> nxt; fused Y/Z: nxt -> cur.  The state stays in `cur`.
+	std::swap(c->cur, c->nxt);
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_set_step_schedule(gcmx_ctx* c, gcmx_schedule sched, int rows_per_block) {
+	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");
+	if (sched < GCMX_SCHED_AUTO || sched > GCMX_SCHED_XSLAB)
+		return fail(GCMX_ERR_INVALID_ARG, "bad schedule");
+	if (rows_per_block < 0 || rows_per_block > 4096)
+		return fail(GCMX_ERR_INVALID_ARG, "rows_per_block must be 0 (automatic) .. 4096");
+	c->sched = sched;
+	c->rows_per_block = rows_per_block;
 	return GCMX_OK;
 }
 
@@ -1007,6 +987,8 @@ gcmx_status gcmx_sync(gcmx_ctx* c) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
 	HIP_TRY(hipStreamSynchronize(c->comm_stream));
+	HIP_TRY(hipStreamSynchronize(c->inner_stream));
+	HIP_TRY(hipStreamSynchronize(c->bnd_stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	c->halo_pending = false;  // the comm stream has drained
 	drain_timings(c);

@@ -23,10 +23,7 @@
 //                 halo per chunk).
 //   k_line_z    : stage along the contiguous axis Z: 256-node row segment plus its
 //                 BS-node halos in LDS.
-//   k_fused_yz  : Y stage then Z stage of one time step in ONE pass: a block owns one
-//                 x plane, a chunk of y rows and the whole z row, marches y (ring
-//                 window), hands each Y-stage row to the Z stage through
-//                 double-buffered LDS and writes only the Z result.
+// (The one-pass X/Y/Z time step is k_fused_xyz, kernels_xyz.hip.)
 #include "iso.hpp"
 
 namespace gcmx {
@@ -83,12 +80,6 @@ constexpr int kMarchThreads = 256;
 #endif
 #ifndef GCMX_MARCH_CHUNK
 #define GCMX_MARCH_CHUNK 64
-#endif
-#ifndef GCMX_FUSED_MINWAVES
-#define GCMX_FUSED_MINWAVES 4
-#endif
-#ifndef GCMX_FUSED_CHUNK
-#define GCMX_FUSED_CHUNK 64
 #endif
 
 
@@ -201,103 +192,6 @@ __global__ __launch_bounds__(kLineThreads) void k_line_z(const double* __restric
 	for (int c = 0; c < 9; c++) out_p.st(c, row + z, out[c]);
 }
 
-// -------------------------------------------------------------- fused yz --
-
-// Block = one x plane, rows [yb, ye) of a y chunk, all z (blockDim = ZT >= Z).
-// Reads the X-stage output `in` (Y-stage input), writes the Z-stage output into
-// `outl`.  Precondition (the host only picks this path when it holds): every
-// y/z ghost of both layers is zero, so ghost rows and the Z stage's ghost
-// neighbours are the constant 0.0 instead of memory reads.
-template <int BS, int ZT, bool KF0>
-__global__ __launch_bounds__(ZT, (BS <= 2 ? GCMX_FUSED_MINWAVES : 2)) void k_fused_yz(const double* __restrict__ in,
-                                                 double* __restrict__ outl, Geo g, IsoAxis AY,
-                                                 IsoAxis AZ, int x0, int chunk) {
-	constexpr unsigned WMY = iso_window(1);
-	constexpr unsigned CMY = iso_center_only(1);
-	constexpr int NWY = popc9(WMY);
-	constexpr unsigned WMZ = iso_window(2);
-	constexpr int NWZ = popc9(WMZ);
-	constexpr int W = 2 * BS + 1;
-	constexpr int LW = ZT + 2 * BS;
-	__shared__ double lds[2][NWZ][LW];
-
-	const int z = threadIdx.x;
-	const int x = x0 + blockIdx.y;
-	const int Y = g.sizes[1], Z = g.sizes[2];
-	const int yb = blockIdx.x * chunk;
-	const int ye = min(yb + chunk, Y);
-	const bool live = z < Z;
-	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
-	const unsigned st = (unsigned)g.stride[1];
-	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
-	const unsigned base = plane + zc;
-	const Planes src(in, g.cs);
-	const PlanesW out_p(outl, g.cs);
-
-	// zero ghost slots of both LDS row buffers once (never overwritten)
-	if (z < 2 * BS) {
-		const int gslot = (z < BS) ? z : (Z + z);
-#pragma unroll
-		for (int q = 0; q < NWZ; q++) {
-			lds[0][q][gslot] = 0.0;
-			lds[1][q][gslot] = 0.0;
-		}
-	}
-	auto row_ld = [&](int j, int yy) -> double {  // ghost rows are zero
-		return (yy >= 0 && yy < Y) ? src.ld(j, base + (unsigned)yy * st) : 0.0;
-	};
-
-	double win[NWY][W];
-	double pw[NWY], ctr[9];
-#pragma unroll
-	for (int j = 0; j < 9; j++) {
-		if (!((WMY >> j) & 1u)) continue;
-#pragma unroll
-		for (int o = 0; o < W - 1; o++) win[wslot(WMY, j)][o] = row_ld(j, yb - BS + o);
-		pw[wslot(WMY, j)] = row_ld(j, yb + BS);
-	}
-
-	int buf = 0;
-	for (int y = yb; y < ye; y++) {
-#pragma unroll
-		for (int j = 0; j < 9; j++) {
-			if ((WMY >> j) & 1u) win[wslot(WMY, j)][W - 1] = pw[wslot(WMY, j)];
-			// node-only components: loaded here, first used after the window rows
-			if ((CMY >> j) & 1u) ctr[j] = src.ld(j, base + (unsigned)y * st);
-		}
-		if (y + 1 < ye) {
-#pragma unroll
-			for (int j = 0; j < 9; j++)
-				if ((WMY >> j) & 1u) pw[wslot(WMY, j)] = row_ld(j, y + 1 + BS);
-		}
-		double yv[9];
-		node_update<1, BS, KF0>(
-		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
-		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : ctr[j]; }, yv);
-		if (live) {
-#pragma unroll
-			for (int j = 0; j < 9; j++)
-				if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = yv[j];
-		}
-		__syncthreads();
-		if (live) {
-			double zv[9];
-			node_update<2, BS, KF0>(
-			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
-			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; },
-			    zv);
-			const unsigned offo = plane + (unsigned)y * st + z;
-#pragma unroll
-			for (int c = 0; c < 9; c++) out_p.st(c, offo, zv[c]);
-		}
-		buf ^= 1;
-#pragma unroll
-		for (int q = 0; q < NWY; q++)
-#pragma unroll
-			for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
-	}
-}
-
 // ------------------------------------------------------------- launchers --
 
 static int march_chunk(int len) { return len < 2 * GCMX_MARCH_CHUNK ? len : GCMX_MARCH_CHUNK; }
@@ -368,46 +262,8 @@ bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& 
 	}
 }
 
-bool fused_yz_supported(const Geo& g) {
+bool fused_supported(const Geo& g) {
 	return fast_layout_ok(g) && g.sizes[2] <= 1024 && g.sizes[2] >= 2 * g.bs;
-}
-
-static int fused_chunk(int Y) { return Y <= GCMX_FUSED_CHUNK ? Y : GCMX_FUSED_CHUNK; }
-
-template <int BS, int ZT>
-static void launch_fused_t(const double* in, double* out, const Geo& g, const IsoAxis& ay,
-                           const IsoAxis& az, int x0, int x1, hipStream_t st) {
-	const int chunk = fused_chunk(g.sizes[1]);
-	dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0);
-	if (ay.kf1 == 0 && ay.kf2 == 0 && az.kf1 == 0 && az.kf2 == 0)
-		hipLaunchKernelGGL((k_fused_yz<BS, ZT, true>), grid, dim3(ZT), 0, st, in, out, g, ay, az, x0,
-		                   chunk);
-	else
-		hipLaunchKernelGGL((k_fused_yz<BS, ZT, false>), grid, dim3(ZT), 0, st, in, out, g, ay, az, x0,
-		                   chunk);
-}
-
-template <int BS>
-static bool launch_fused_bs(const double* in, double* out, const Geo& g, const IsoAxis& ay,
-                            const IsoAxis& az, int x0, int x1, hipStream_t st) {
-	const int Z = g.sizes[2];
-	if (Z <= 64) launch_fused_t<BS, 64>(in, out, g, ay, az, x0, x1, st);
-	else if (Z <= 128) launch_fused_t<BS, 128>(in, out, g, ay, az, x0, x1, st);
-	else if (Z <= 256) launch_fused_t<BS, 256>(in, out, g, ay, az, x0, x1, st);
-	else if (Z <= 512) launch_fused_t<BS, 512>(in, out, g, ay, az, x0, x1, st);
-	else launch_fused_t<BS, 1024>(in, out, g, ay, az, x0, x1, st);
-	return true;
-}
-
-bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis& ay,
-                     const IsoAxis& az, int x0, int x1, hipStream_t st) {
-	if (!fused_yz_supported(g) || x1 <= x0) return false;
-	switch (g.bs) {
-	case 1: return launch_fused_bs<1>(in, out, g, ay, az, x0, x1, st);
-	case 2: return launch_fused_bs<2>(in, out, g, ay, az, x0, x1, st);
-	case 3: return launch_fused_bs<3>(in, out, g, ay, az, x0, x1, st);
-	default: return false;
-	}
 }
 
 }  // namespace gcmx

@@ -23,68 +23,23 @@ namespace gcmx {
 // HBM traffic: the input layer once, the output layer once (144 B/node/step).
 // Reads `in` (all components, x ghost planes valid), writes `outl`.
 //
-// Schedule (defaults below, measured A/B on MI355X): the loop is
-// rotated (Y, Z, stores, then the X stage of the row that enters the window);
-// the X stage loads one characteristic pair (10 values) at a time with the next
-// pair in flight, which keeps the kernel at 128 VGPRs (two 512-thread blocks per
-// CU); the first pair of the next row is issued before this row's stores, so
-// its vmcnt wait never includes the stores (loads and stores retire in order on
+// Schedule (measured A/B on MI355X): the loop is rotated (Y, Z,
+// stores, then the X stage of the row that enters the window); the X stage
+// loads one characteristic pair (10 values) at a time with the next pair in
+// flight, which keeps the kernel at 128 VGPRs (two 512-thread blocks per CU);
+// the first pair of the next row is issued before this row's stores, so its
+// vmcnt wait never includes the stores (loads and stores retire in order on
 // gfx950); the output is written with non-temporal stores.
-// Precondition as k_fused_yz: every y/z ghost of both layers is zero, so the
-// intermediate results at ghost rows / columns are the constant 0.0.
-#ifndef GCMX_XYZ_MINWAVES
+// Precondition: every y/z ghost of both layers is zero, so the intermediate
+// results at ghost rows / columns are the constant 0.0.
+#ifndef GCMX_XYZ_MINWAVES  // tuning builds only (scripts/ab_build.sh)
 #define GCMX_XYZ_MINWAVES 4
 #endif
 #ifndef GCMX_XYZ_CHUNK
 #define GCMX_XYZ_CHUNK 128
 #endif
-#ifndef GCMX_XYZ_ROTATE
-#define GCMX_XYZ_ROTATE 1
-#endif
 #ifndef GCMX_XYZ_UNROLL
 #define GCMX_XYZ_UNROLL 1
-#endif
-#ifndef GCMX_XYZ_GROUPED
-#define GCMX_XYZ_GROUPED 2
-#endif
-#ifndef GCMX_XYZ_LATE_STORE
-#define GCMX_XYZ_LATE_STORE 0
-#endif
-#ifndef GCMX_XYZ_UNI
-#define GCMX_XYZ_UNI 1
-#endif
-#ifndef GCMX_XYZ_SWIZZLE
-#define GCMX_XYZ_SWIZZLE 1
-#endif
-#ifndef GCMX_XYZ_SCHED_BARRIER
-#define GCMX_XYZ_SCHED_BARRIER 1
-#endif
-#ifndef GCMX_XYZ_PREFETCH
-#define GCMX_XYZ_PREFETCH 1
-#endif
-// Diagnostic builds only (scripts/ab_build.sh; results are wrong by design).
-#ifndef GCMX_DIAG_L2HOT
-#define GCMX_DIAG_L2HOT 0
-#endif
-#ifndef GCMX_DIAG_NOSTORE
-#define GCMX_DIAG_NOSTORE 0
-#endif
-#ifndef GCMX_XYZ_NT_STORE
-#define GCMX_XYZ_NT_STORE 1
-#endif
-#if GCMX_XYZ_NT_STORE
-#define XYZ_ST out_p.st_nt
-#else
-#define XYZ_ST out_p.st
-#endif
-#ifndef GCMX_DIAG_HOTSTORE
-#define GCMX_DIAG_HOTSTORE 0
-#endif
-#ifndef GCMX_DIAG_HALFZ
-#define GCMX_DIAG_HALFZ 0
-#endif
-#ifndef GCMX_DIAG_NOBAR
-#define GCMX_DIAG_NOBAR 0
 #endif
 
 // UNI: the launch has Z == ZT (no idle lanes) and the three axes' tables are
@@ -98,7 +53,6 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 	const IsoAxis& AZ = UNI ? AX : AZ_;
 	constexpr unsigned WMX = iso_window(0);
 	constexpr unsigned CMX = iso_center_only(0);
-	constexpr int NWX = popc9(WMX);
 	constexpr unsigned WMY = iso_window(1);
 	constexpr unsigned CMY = iso_center_only(1);
 	constexpr int NWY = popc9(WMY);
@@ -111,7 +65,6 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 
 	const int z = threadIdx.x;
 	const int Y = g.sizes[1], Z = g.sizes[2];
-#if GCMX_XYZ_SWIZZLE && !GCMX_DIAG_HALFZ
 	// 1-D grid of nchunks * nplanes blocks.  Blocks are dealt round-robin over
 	// the 8 XCDs (b % 8 share one, MI355X_MICROARCH.md §Workgroup dispatch): give
 	// each XCD a contiguous run of (chunk, plane) pairs in chunk-major order, so
@@ -124,33 +77,18 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		x = x0 + p % nx;
 		yb = (p / nx) * chunk;
 	}
-#else
-	const int x = x0 + blockIdx.y;
-	const int yb = blockIdx.x * chunk;
-#endif
 	const int ye = min(yb + chunk, Y);
-#if GCMX_DIAG_HALFZ  // diagnostic: ZT-wide z tiles, no halo (wrong at tile edges)
-	const unsigned zoff = blockIdx.z * ZT;
-	const int ZL = ZT;
-#else
-	const unsigned zoff = 0;
-	const int ZL = Z;
-#endif
-	const bool live = UNI || z < ZL;
+	const bool live = UNI || z < Z;
 	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
 	const unsigned stx = (unsigned)g.stride[0];
 	const unsigned sty = (unsigned)g.stride[1];
-	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]) + zoff;
-#if GCMX_DIAG_L2HOT  // diagnostic: every block reads x plane 2 (L2-resident loads)
-	const unsigned base = (unsigned)(g.origin + 2 * g.stride[0]) + zc;
-#else
+	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
 	const unsigned base = plane + zc;
-#endif
 	const Planes src(in, g.cs);
 	const PlanesW out_p(outl, g.cs);
 
 	if (z < 2 * BS) {  // ghost slots of both LDS row buffers: zero, never overwritten
-		const int gslot = (z < BS) ? z : (ZL + z);
+		const int gslot = (z < BS) ? z : (Z + z);
 #pragma unroll
 		for (int q = 0; q < NWZ; q++) {
 			lds[0][q][gslot] = 0.0;
@@ -158,34 +96,8 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		}
 	}
 
-	// X-stage input of one row: window components at x-BS..x+BS, the rest at x
-	struct XIn {
-		double w[NWX][W];
-		double c[9];
-	};
-	auto x_load = [&](XIn& v, int r) {
-		const unsigned o = base + (unsigned)r * sty;
-#pragma unroll
-		for (int j = 0; j < 9; j++) {
-			if ((WMX >> j) & 1u) {
-#pragma unroll
-				for (int k = 0; k < W; k++) v.w[wslot(WMX, j)][k] = src.ld(j, o + (unsigned)(k - BS) * stx);
-			}
-			if ((CMX >> j) & 1u) v.c[j] = src.ld(j, o);
-		}
-	};
-	auto x_stage = [&](const XIn& v, double (&xr)[9]) {
-		node_update<0, BS, KF0>(
-		    AX, [&](int j, int o) { return v.w[wslot(WMX, j)][BS + o]; },
-		    [&](int j) { return ((WMX >> j) & 1u) ? v.w[wslot(WMX, j)][BS] : v.c[j]; }, xr);
-	};
-	auto in_rows = [&](int r) { return r >= 0 && r < Y; };
-
-	// Grouped X stage (GCMX_XYZ_GROUPED): the row's 33 inputs are loaded one
-	// characteristic pair at a time (10 values), the next pair's loads in flight
-	// while the current pair is computed, so at most two pairs are live in
-	// registers (instead of all 33 values): the kernel fits 128 VGPRs, i.e. two
-	// 512-thread blocks per CU.  Same node_update arithmetic (iso.hpp).
+	// X stage of row r, loaded one characteristic pair (10 values) at a time with
+	// the next pair in flight: at most two pairs are live in registers.
 	typedef double PairWin[2][W];
 	auto pair_load = [&](auto PC, PairWin& w, unsigned o) {
 		constexpr int P = decltype(PC)::value;
@@ -199,17 +111,16 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		constexpr int P = decltype(PC)::value;
 		return [&w](int j, int o) { return j == pair_vel(0, P) ? w[0][BS + o] : w[1][BS + o]; };
 	};
-	auto sched_fence = [] {
-#if GCMX_XYZ_SCHED_BARRIER
-		__builtin_amdgcn_sched_barrier(0);
-#endif
-	};
-	// (split so that the first pair's loads can be issued ahead of the stores)
-	auto x_stage_grouped_ab = [&](PairWin& wa, PairWin& wb, int r, double (&xr)[9], auto&& mid) {
+	auto sched_fence = [] { __builtin_amdgcn_sched_barrier(0); };
+	using P0 = std::integral_constant<int, 0>;
+	using P1 = std::integral_constant<int, 1>;
+	using P2 = std::integral_constant<int, 2>;
+	// wa holds pair 0 of row r (already issued); loads pairs 1, 2 and the
+	// node-only components as it goes.
+	auto x_stage_rest = [&](PairWin& wa, int r, double (&xr)[9]) {
 		const unsigned o = base + (unsigned)r * sty;
-		using P0 = std::integral_constant<int, 0>;
-		using P1 = std::integral_constant<int, 1>;
-		using P2 = std::integral_constant<int, 2>;
+		PairWin wb;
+		pair_load(P1{}, wb, o);
 		double rr[9], n0[9], cv[9];
 		pair_update<0, BS, KF0, 0>(AX, pair_acc(P0{}, wa), rr[0], rr[1]);
 		n0[pair_vel(0, 0)] = wa[0][BS];
@@ -223,7 +134,6 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #pragma unroll
 		for (int j = 0; j < 9; j++)
 			if ((CMX >> j) & 1u) cv[j] = src.ld(j, o);
-		mid();
 		pair_update<0, BS, KF0, 2>(AX, pair_acc(P2{}, wa), rr[4], rr[5]);
 		n0[pair_vel(0, 2)] = wa[0][BS];
 		n0[pair_sig(0, 2)] = wa[1][BS];
@@ -231,20 +141,7 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		center_update<0>(AX, [&](int j) { return ((WMX >> j) & 1u) ? n0[j] : cv[j]; }, rr);
 		u1_apply<0>(AX, rr, xr);
 	};
-	auto x_stage_grouped_rest = [&](PairWin& wa, int r, double (&xr)[9]) {
-		PairWin wb;
-		pair_load(std::integral_constant<int, 1>{}, wb, base + (unsigned)r * sty);
-		x_stage_grouped_ab(wa, wb, r, xr, [] {});
-	};
-	auto x_load_a = [&](PairWin& wa, int r) {
-		pair_load(std::integral_constant<int, 0>{}, wa, base + (unsigned)r * sty);
-	};
-	auto x_stage_grouped = [&](int r, double (&xr)[9]) {
-		PairWin wa;
-		x_load_a(wa, r);
-		sched_fence();
-		x_stage_grouped_rest(wa, r, xr);
-	};
+	auto x_load_a = [&](PairWin& wa, int r) { pair_load(P0{}, wa, base + (unsigned)r * sty); };
 
 	// Y window over X results of rows y-BS..y+BS; node-only components of rows
 	// y..y+BS wait in a small delay line.
@@ -259,7 +156,6 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 			}
 		}
 	};
-#if GCMX_XYZ_ROTATE
 	// Rotated schedule: the loads of an X row are issued at the END of an
 	// iteration and consumed after the next iteration's stores, so in every path
 	// into the loop they are older than 9 stores and the compiler's vmcnt waits
@@ -272,10 +168,10 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 	for (int k = 0; k < W; k++) {
 		const int r = yb - BS + k;
 		double xr[9];
-		if (in_rows(r)) {
-			XIn v;
-			x_load(v, r);
-			x_stage(v, xr);
+		if (r >= 0 && r < Y) {
+			PairWin wa;
+			x_load_a(wa, r);
+			x_stage_rest(wa, r, xr);
 		} else {
 #pragma unroll
 			for (int j = 0; j < 9; j++) xr[j] = 0.0;
@@ -283,16 +179,10 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 		push(xr, k);
 	}
 	auto clamp_row = [&](int r) { return r < Y + BS - 1 ? r : Y + BS - 1; };
-#if !GCMX_XYZ_GROUPED
-	XIn nxt_in;
-	x_load(nxt_in, clamp_row(yb + BS + 1));
-#endif
 	const unsigned zo = live ? (unsigned)z : (unsigned)Z;
 
 	int buf = 0;
-#if GCMX_XYZ_UNROLL > 1
 #pragma unroll GCMX_XYZ_UNROLL
-#endif
 	for (int y = yb; y < ye; y++) {
 		double yv[9];
 		node_update<1, BS, KF0>(
@@ -302,89 +192,20 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #pragma unroll
 		for (int j = 0; j < 9; j++)
 			if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = live ? yv[j] : 0.0;
-#if GCMX_XYZ_GROUPED >= 2
 		PairWin wa_next;
-#endif
-#if GCMX_XYZ_GROUPED == 4
-		// Early schedule: the next X row's first pair is issued before the
-		// barrier (the Z stage hides its latency), the second pair before this
-		// row's stores, so the waits of both exclude the stores.
-		const int rn = clamp_row(y + BS + 1);
-		sched_fence();
-		x_load_a(wa_next, rn);
-		sched_fence();
-#endif
-#if !GCMX_DIAG_NOBAR
 		__syncthreads();
-#endif
-#if GCMX_XYZ_GROUPED == 4
 		{
 			double zv[9];
 			node_update<2, BS, KF0>(
 			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
 			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
-			PairWin wb_next;
-			sched_fence();
-			pair_load(std::integral_constant<int, 1>{}, wb_next, base + (unsigned)rn * sty);
-			sched_fence();
 			const unsigned offo = plane + (unsigned)y * sty + zo;
-			auto stores = [&] {
-#pragma unroll
-				for (int c = 0; c < 9; c++) XYZ_ST(c, offo, live ? zv[c] : 0.0);
-			};
-#if GCMX_XYZ_LATE_STORE == 0
-			stores();
-#endif
-			buf ^= 1;
-#pragma unroll
-			for (int q = 0; q < NWY; q++)
-#pragma unroll
-				for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
-#pragma unroll
-			for (int k = 0; k < BS; k++)
-#pragma unroll
-				for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
-			double xr[9];
-			sched_fence();
-#if GCMX_XYZ_LATE_STORE == 0
-			x_stage_grouped_ab(wa_next, wb_next, rn, xr, [] {});
-#else  // stores after every load of the next row is issued (zv stays live longer)
-			x_stage_grouped_ab(wa_next, wb_next, rn, xr, [&] { sched_fence(); stores(); sched_fence(); });
-#endif
-			push(xr, W - 1);
-			sched_fence();
-		}
-		continue;
-#endif
-#if GCMX_XYZ_GROUPED == 3
-		PairWin wb_next;
-#endif
-		{
-			double zv[9];
-			node_update<2, BS, KF0>(
-			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
-			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
-#if GCMX_DIAG_HOTSTORE  // diagnostic: every block stores into x plane 2 (L2-resident)
-			const unsigned offo = (unsigned)(g.origin + 2 * g.stride[0]) + zoff + (unsigned)y * sty + zo;
-#else
-			const unsigned offo = plane + (unsigned)y * sty + zo;
-#endif
-#if GCMX_XYZ_GROUPED == 2  // next row's first pair: loads older than this row's stores
+			// next row's first pair: loads older than this row's stores
 			sched_fence();
 			x_load_a(wa_next, clamp_row(y + BS + 1));
 			sched_fence();
-#elif GCMX_XYZ_GROUPED == 3  // first two pairs ahead of the stores
-			sched_fence();
-			x_load_a(wa_next, clamp_row(y + BS + 1));
-			pair_load(std::integral_constant<int, 1>{}, wb_next,
-			          base + (unsigned)clamp_row(y + BS + 1) * sty);
-			sched_fence();
-#endif
-#if GCMX_DIAG_NOSTORE  // diagnostic: keep the work, drop the stores
-			if (zv[0] == 1234.5678)
-#endif
 #pragma unroll
-			for (int c = 0; c < 9; c++) XYZ_ST(c, offo, live ? zv[c] : 0.0);
+			for (int c = 0; c < 9; c++) out_p.st_nt(c, offo, live ? zv[c] : 0.0);
 		}
 		buf ^= 1;
 #pragma unroll
@@ -397,113 +218,12 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
 		{  // X stage of row y+BS+1 (zero ghost rows give zero) -> window slot W-1
 			double xr[9];
-#if GCMX_XYZ_GROUPED == 3
 			sched_fence();
-			x_stage_grouped_ab(wa_next, wb_next, clamp_row(y + BS + 1), xr, [] {});
+			x_stage_rest(wa_next, clamp_row(y + BS + 1), xr);
 			push(xr, W - 1);
 			sched_fence();
-#elif GCMX_XYZ_GROUPED == 2
-			sched_fence();
-			x_stage_grouped_rest(wa_next, clamp_row(y + BS + 1), xr);
-			push(xr, W - 1);
-			sched_fence();
-#elif GCMX_XYZ_GROUPED
-			sched_fence();
-			x_stage_grouped(clamp_row(y + BS + 1), xr);
-			push(xr, W - 1);
-			sched_fence();
-#else
-#if GCMX_XYZ_SCHED_BARRIER  // keep the next row's loads behind this row's stores
-			__builtin_amdgcn_sched_barrier(0);
-#endif
-			x_stage(nxt_in, xr);
-			push(xr, W - 1);
-#if GCMX_XYZ_SCHED_BARRIER
-			__builtin_amdgcn_sched_barrier(0);
-#endif
-			x_load(nxt_in, clamp_row(y + BS + 2));
-#endif
 		}
 	}
-#else
-	// prologue: X results of rows yb-BS .. yb+BS-1
-#pragma unroll
-	for (int k = 0; k < W - 1; k++) {
-		const int r = yb - BS + k;
-		double xr[9];
-		if (in_rows(r)) {
-			XIn v;
-			x_load(v, r);
-			x_stage(v, xr);
-		} else {
-#pragma unroll
-			for (int j = 0; j < 9; j++) xr[j] = 0.0;
-		}
-		push(xr, k);
-	}
-#if GCMX_XYZ_PREFETCH
-	XIn nxt_in;
-	if (in_rows(yb + BS)) x_load(nxt_in, yb + BS);
-#endif
-
-	int buf = 0;
-	for (int y = yb; y < ye; y++) {
-		{  // X stage of row y+BS -> window slot W-1
-			const int r = y + BS;
-			double xr[9];
-			if (in_rows(r)) {
-#if GCMX_XYZ_PREFETCH
-				x_stage(nxt_in, xr);
-#else
-				XIn v;
-				x_load(v, r);
-				x_stage(v, xr);
-#endif
-			} else {
-#pragma unroll
-				for (int j = 0; j < 9; j++) xr[j] = 0.0;
-			}
-			push(xr, W - 1);
-#if GCMX_XYZ_PREFETCH
-			if (y + 1 < ye && in_rows(r + 1)) x_load(nxt_in, r + 1);
-#endif
-		}
-		double yv[9];
-		node_update<1, BS, KF0>(
-		    AY, [&](int j, int o) { return win[wslot(WMY, j)][BS + o]; },
-		    [&](int j) { return ((WMY >> j) & 1u) ? win[wslot(WMY, j)][BS] : cen[0][wslot(CMY, j)]; },
-		    yv);
-		if (live) {
-#pragma unroll
-			for (int j = 0; j < 9; j++)
-				if ((WMZ >> j) & 1u) lds[buf][wslot(WMZ, j)][BS + z] = yv[j];
-		}
-#if !GCMX_DIAG_NOBAR
-		__syncthreads();
-#endif
-		if (live) {
-			double zv[9];
-			node_update<2, BS, KF0>(
-			    AZ, [&](int j, int o) { return lds[buf][wslot(WMZ, j)][BS + z + o]; },
-			    [&](int j) { return ((WMZ >> j) & 1u) ? lds[buf][wslot(WMZ, j)][BS + z] : yv[j]; }, zv);
-			const unsigned offo = plane + (unsigned)y * sty + z;
-#if GCMX_DIAG_NOSTORE  // diagnostic: keep the work, drop the stores
-			if (zv[0] == 1234.5678)
-#endif
-#pragma unroll
-			for (int c = 0; c < 9; c++) XYZ_ST(c, offo, zv[c]);
-		}
-		buf ^= 1;
-#pragma unroll
-		for (int q = 0; q < NWY; q++)
-#pragma unroll
-			for (int o = 0; o < W - 1; o++) win[q][o] = win[q][o + 1];
-#pragma unroll
-		for (int k = 0; k < BS; k++)
-#pragma unroll
-			for (int q = 0; q < (NCY > 0 ? NCY : 1); q++) cen[k][q] = cen[k + 1][q];
-	}
-#endif
 }
 
 // ------------------------------------------------------------- launchers --
@@ -512,8 +232,6 @@ static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
 	static_assert(sizeof(IsoAxis) == 12 * 8 + 2 * 4, "IsoAxis has padding");
 	return std::memcmp(&p, &q, sizeof(IsoAxis)) == 0;
 }
-
-static int xyz_chunk(int Y) { return Y <= GCMX_XYZ_CHUNK ? Y : GCMX_XYZ_CHUNK; }
 
 // Rows per block: GCMX_XYZ_CHUNK (128) while the launch still has >= 1024 blocks
 // (two rounds of the 512 resident blocks, 2 per CU); thinner slabs (multi-GPU
@@ -532,14 +250,10 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
                          int x1, hipStream_t st, int req_chunk) {
 	const int chunk = xyz_chunk_for(g.sizes[1], x1 - x0, req_chunk);
 	const int nchunks = (g.sizes[1] + chunk - 1) / chunk;
-#if GCMX_XYZ_SWIZZLE && !GCMX_DIAG_HALFZ
 	dim3 grid(nchunks * (x1 - x0));
-#else
-	dim3 grid(nchunks, x1 - x0);
-#endif
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
-	const bool uni = GCMX_XYZ_UNI && kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
+	const bool uni = kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
 	if (uni)
 		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true, true>), grid, dim3(ZT), 0, st, in, out, g, a[0],
 		                   a[1], a[2], x0, chunk, x1 - x0);
@@ -565,21 +279,7 @@ static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const Iso
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk) {
-	if (!fused_yz_supported(g) || x1 <= x0) return false;
-#ifdef GCMX_TUNE_FAST  // tuning builds: the bench configuration only
-	if (g.bs != 2 || g.sizes[2] <= 256 || g.sizes[2] > 512) return false;
-#if GCMX_DIAG_HALFZ
-	{
-		const int chunk = xyz_chunk(g.sizes[1]);
-		dim3 grid((g.sizes[1] + chunk - 1) / chunk, x1 - x0, 2);
-		hipLaunchKernelGGL((k_fused_xyz<2, 256, true, false>), grid, dim3(256), 0, st, in, out, g, a[0], a[1],
-		                   a[2], x0, chunk, x1 - x0);
-		return true;
-	}
-#endif
-	launch_xyz_t<2, 512>(in, out, g, a, x0, x1, st, chunk);
-	return true;
-#endif
+	if (!fused_supported(g) || x1 <= x0) return false;
 	switch (g.bs) {
 	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk);
 	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk);
@@ -587,6 +287,5 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	default: return false;
 	}
 }
-
 
 }  // namespace gcmx

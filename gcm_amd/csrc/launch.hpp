@@ -39,9 +39,8 @@ bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const Iso
                   int x0, int x1, hipStream_t st);
 bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& A, int x0,
                    int x1, hipStream_t st);
-bool launch_fused_yz(const double* in, double* out, const Geo& g, const IsoAxis& ay,
-                     const IsoAxis& az, int x0, int x1, hipStream_t st);
-bool fused_yz_supported(const Geo& g);
+// The one-pass step needs 2*bs <= Z <= 1024 (one block spans a whole z row).
+bool fused_supported(const Geo& g);
 // One pass per time step: X, Y, Z stages of planes [x0, x1), `a` = the three axes.
 // `chunk`: y rows per block (0 = automatic, kernels_xyz.hip: xyz_chunk_for).
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,

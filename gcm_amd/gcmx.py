@@ -25,6 +25,7 @@ STATUS_NAMES = {0: "GCMX_OK", 1: "GCMX_ERR_INVALID_ARG", 2: "GCMX_ERR_CFL", 3: "
                 7: "GCMX_ERR_COMM"}
 PATH_AUTO, PATH_GENERIC, PATH_SPLIT, PATH_FUSED = 0, 1, 2, 3
 PATH_NAMES = {0: "auto", 1: "generic", 2: "split", 3: "fused"}
+SCHED_AUTO, SCHED_SINGLE, SCHED_XSLAB = 0, 1, 2
 UNIQUE_ID_BYTES = 128
 
 # Exported symbols, in header order (checked by tests/test_abi.py).
@@ -32,7 +33,7 @@ SYMBOLS = [
     "gcmx_abi_version", "gcmx_last_error", "gcmx_pde_size", "gcmx_status_string",
     "gcmx_create", "gcmx_destroy", "gcmx_set_materials", "gcmx_set_material_ids",
     "gcmx_upload", "gcmx_download", "gcmx_fill_random", "gcmx_stage", "gcmx_step",
-    "gcmx_set_kernel_path", "gcmx_effective_path", "gcmx_border_fill", "gcmx_copy_box",
+    "gcmx_set_kernel_path", "gcmx_set_step_schedule", "gcmx_effective_path", "gcmx_border_fill", "gcmx_copy_box",
     "gcmx_ode_maxwell",
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_sync", "gcmx_stream",
@@ -91,6 +92,7 @@ def lib() -> ctypes.CDLL:
     L.gcmx_stage.argtypes = [vp, ctypes.c_int, ctypes.c_double]
     L.gcmx_step.argtypes = [vp, ctypes.c_double]
     L.gcmx_set_kernel_path.argtypes = [vp, ctypes.c_int]
+    L.gcmx_set_step_schedule.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.gcmx_effective_path.argtypes = [vp]
     L.gcmx_border_fill.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int,
                                    ip, dp]
@@ -217,6 +219,10 @@ class Context:
 
     def set_path(self, path: int):
         _check(lib().gcmx_set_kernel_path(self._ptr, path))
+
+    def set_schedule(self, sched: int, rows_per_block: int = 0):
+        """gcmx_set_step_schedule: SCHED_AUTO / SCHED_SINGLE / SCHED_XSLAB."""
+        _check(lib().gcmx_set_step_schedule(self._ptr, sched, rows_per_block))
 
     @property
     def effective_path(self) -> str:

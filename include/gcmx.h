@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GCMX_ABI_VERSION 1
+#define GCMX_ABI_VERSION 2
 
 typedef enum gcmx_status {
 	GCMX_OK = 0,
@@ -58,8 +58,17 @@ typedef enum gcmx_path {
 	GCMX_PATH_AUTO = 0,    /* fastest path the configuration admits                */
 	GCMX_PATH_GENERIC = 1, /* one thread per node, any D / borderSize / materials  */
 	GCMX_PATH_SPLIT = 2,   /* per-axis tuned kernels (march / LDS line), 3-D only  */
-	GCMX_PATH_FUSED = 3    /* X march + fused Y/Z pass, 3-D only                   */
+	GCMX_PATH_FUSED = 3    /* the whole step in one pass (k_fused_xyz), 3-D only  */
 } gcmx_path;
+
+/* How gcmx_step issues the fused pass (gcmx_set_step_schedule). */
+typedef enum gcmx_schedule {
+	GCMX_SCHED_AUTO = 0,   /* X-slab schedule when a halo exchange is configured   */
+	GCMX_SCHED_SINGLE = 1, /* halo (if any) first, then one launch over all planes */
+	GCMX_SCHED_XSLAB = 2   /* interior planes on a low-priority stream beside the
+	                          boundary planes, the next halo posted before the
+	                          interior joins; needs X >= 4*bs     */
+} gcmx_schedule;
 
 /* ---- library ------------------------------------------------------------ */
 int         gcmx_abi_version(void);
@@ -110,6 +119,10 @@ gcmx_status gcmx_stage(gcmx_ctx* ctx, int axis, double tau);
  * identical to dim consecutive gcmx_stage calls. */
 gcmx_status gcmx_step(gcmx_ctx* ctx, double tau);
 gcmx_status gcmx_set_kernel_path(gcmx_ctx* ctx, gcmx_path path);
+/* Step schedule of the fused path and the fused kernel's y rows per block
+ * (0 = automatic).  Results do not depend on either (tests/test_gpu_parity.py);
+ * only the overlap of the X-slab halo exchange with compute does. */
+gcmx_status gcmx_set_step_schedule(gcmx_ctx* ctx, gcmx_schedule sched, int rows_per_block);
 /* Which path gcmx_step would take now (after materials are set). */
 gcmx_path   gcmx_effective_path(gcmx_ctx* ctx);
 

@@ -205,10 +205,12 @@ def test_adhesion_contact_two_contexts_bitwise(G):
     assert np.array_equal(ia, one.bodies[0].inner_view())
 
 
-def test_x_slabs_with_copy_halo_equal_single(G):
+@pytest.mark.parametrize("sched", ["single", "xslab"])
+def test_x_slabs_with_copy_halo_equal_single(G, sched):
     """Slab decomposition along X (the multi-GPU layout) on one device: two
     slabs whose X ghosts are refreshed from the neighbour before every step
-    (gcmx_halo_exchange_group) == one context, bitwise, on the fused path."""
+    (gcmx_halo_exchange_group) == one context, bitwise, on the fused path, with
+    the one-launch and the three-stream X-slab step schedules."""
     N, bs, seed = 40, 2, 0x5EED
     import gcm_amd
     from gcm_amd.host import isotropic_elastic_matrices
@@ -219,6 +221,7 @@ def test_x_slabs_with_copy_halo_equal_single(G):
     for r, (x0, X) in enumerate(((0, 17), (17, N - 17))):
         c = gcm_amd.Context(3, bs, [X, N, N], start=[x0, 0, 0])
         c.set_materials(U[None], U1[None], L[None]); c.fill_random([N, N, N], seed)
+        c.set_schedule(G.SCHED_XSLAB if sched == "xslab" else G.SCHED_SINGLE)
         halves.append(c)
     a, b = halves
     from gcm_amd.gcmx import halo_exchange_group
@@ -232,7 +235,88 @@ def test_x_slabs_with_copy_halo_equal_single(G):
     assert np.array_equal(F[:17], sh(a, ga)) and np.array_equal(F[17:], sh(b, gb))
 
 
+def _slab_contexts(G, X, Y, Z, nslabs, seed, sched, rows=0):
+    import gcm_amd
+    from gcm_amd.host import isotropic_elastic_matrices
+    U, U1, L = isotropic_elastic_matrices(3, 4, 2, 1)
+    out = []
+    for r in range(nslabs):
+        c = gcm_amd.Context(3, 2, [X, Y, Z], start=[r * X, 0, 0])
+        c.set_materials(U[None], U1[None], L[None])
+        c.fill_random([X * nslabs, Y, Z], seed)
+        c.set_schedule(sched, rows)
+        out.append(c)
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_xslab_schedule_64x512x512_slabs_match_oracle(G):
+    """BASELINE config 3's slab shape (512^3 over 8 GPUs = 64 x 512 x 512 per
+    GPU) on one device: two in-process X slabs under the three-stream X-slab
+    schedule (interior planes on the low-priority stream with the adaptive
+    16-row chunk, both 16-row boundary sides on their own streams), halos
+    refreshed by gcmx_halo_exchange_group before each step, == the oracle run
+    on the undivided 128 x 512 x 512 box, bitwise (TestMPI.cpp:92-155 idea,
+    ASSERT_EQ at :150)."""
+    import os
+    from gcm_amd.gcmx import halo_exchange_group
+    X, Y, Z, bs, seed, nsteps = 64, 512, 512, 2, 0x5EED, 2
+    slabs = _slab_contexts(G, X, Y, Z, 2, seed, G.SCHED_XSLAB)
+    for _ in range(nsteps):
+        halo_exchange_group(slabs)
+        for c in slabs:
+            c.step(0.9)
+    assert all(c.effective_path == "fused" for c in slabs)
+    got = [c.download().reshape(X + 2 * bs, Y + 2 * bs, Z + 2 * bs, 9)[bs:-bs, bs:-bs, bs:-bs]
+           for c in slabs]
+    for c in slabs:
+        c.close()
+    b = oracle_body(3, bs, [2 * X, Y, Z])
+    O.fill_random(b, [2 * X, Y, Z], seed)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    for _ in range(nsteps):
+        for s in range(3):
+            b.stage(s, 0.9, threads)
+    want = b.inner_view()
+    for r in range(2):
+        assert np.array_equal(got[r], want[r * X:(r + 1) * X]), f"slab {r}"
+
+
+@pytest.mark.parametrize("rows", [1, 7, 16, 128, 1000])
+def test_fused_rows_per_block_any_value(G, rows):
+    """The fused kernel's y chunk (gcmx_set_step_schedule rows_per_block) does
+    not change results: prologue recompute of 2*BS X rows per chunk, partial
+    last chunk, chunk > Y."""
+    b = oracle_body(3, 2, [6, 40, 64])
+    random_state(b, seed=rows, ghosts=False)
+    ctx = context_for(b, path=G.PATH_AUTO)
+    ctx.set_schedule(G.SCHED_SINGLE, rows)
+    for step in range(2):
+        for s in range(3):
+            b.stage(s, 0.9)
+        ctx.step(0.9)
+        assert_same(ctx, b, f"rows {rows} step {step}")
+
+
+@pytest.mark.parametrize("sizes", [[6, 24, 512], [5, 20, 256], [4, 12, 1024], [7, 9, 128]])
+def test_fused_uni_instance_matches_oracle(G, sizes):
+    """The benched specialisation k_fused_xyz<BS=2, ZT=Z, KF0, UNI> (Z == ZT,
+    isotropic (4,2,1) with h = 1 on every axis: one IsoAxis for all three
+    stages); [6, 24, 512] is the 512^3 bench instance (ZT = 512), three steps
+    against the oracle, bitwise."""
+    b = oracle_body(3, 2, sizes)
+    random_state(b, seed=sum(sizes), ghosts=False)
+    ctx = context_for(b, path=G.PATH_AUTO)
+    assert ctx.effective_path == "fused"
+    for step in range(3):
+        for s in range(3):
+            b.stage(s, 0.9)
+        ctx.step(0.9)
+        assert_same(ctx, b, f"uni sizes={sizes} step {step}")
+
+
 @pytest.mark.slow
+@pytest.mark.timeout(600)
 def test_full_size_256_paths_agree_and_match_oracle(G):
     """256^3 (BASELINE config 2): one step on the fused path == split == oracle."""
     import gcm_amd
@@ -253,3 +337,28 @@ def test_full_size_256_paths_agree_and_match_oracle(G):
     for s in range(3):
         b.stage(s, 0.9, 16)
     assert np.array_equal(b.inner_view(outs[G.PATH_FUSED]), b.inner_view())
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_full_size_512_step_matches_oracle(G):
+    """512^3 (the headline bench configuration): one step on the default path
+    (k_fused_xyz<2, 512, KF0, UNI>) == the oracle at all host threads, bitwise."""
+    import os
+    import gcm_amd
+    from gcm_amd.host import isotropic_elastic_matrices
+    N, seed = 512, 0x5EED
+    U, U1, L = isotropic_elastic_matrices(3, 4, 2, 1)
+    c = gcm_amd.Context(3, 2, [N, N, N])
+    c.set_materials(U[None], U1[None], L[None])
+    c.fill_random([N, N, N], seed)
+    assert c.effective_path == "fused"
+    c.step(0.9)
+    got = c.download()
+    c.close()
+    b = oracle_body(3, 2, [N, N, N])
+    O.fill_random(b, [N, N, N], seed)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    for s in range(3):
+        b.stage(s, 0.9, threads)
+    assert np.array_equal(b.inner_view(got), b.inner_view())
