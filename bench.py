@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0,
                    help="bound on each of the two CPU baseline samples")
+    p.add_argument("--rows-per-block", type=int, default=0,
+                   help="fused-step y rows per block (0 = the library's automatic choice)")
     p.add_argument("--no-profile", action="store_true",
                    help="no hipEvent bracketing of the launches in the timed repetitions")
     return p.parse_args()
@@ -164,6 +166,8 @@ def main():
     ctx = gcm_amd.Context(3, 2, [X, N, N], start=[x0, 0, 0], device=device)
     ctx.set_materials(U[None], U1[None], L[None])
     ctx.set_path(paths[a.path])
+    if a.rows_per_block:
+        ctx.set_schedule(gcmx.SCHED_AUTO, a.rows_per_block)
     ctx.fill_random([N, N, N], 0x5EED)
     if world > 1:
         uid = gcm_amd.unique_id() if rank == 0 else None

@@ -16,6 +16,7 @@
 #include "launch.hpp"
 
 using namespace gcmx;
+static_assert(GCMX_MAX_BORDER_Q == kMaxBorderQ, "border quantity limit");
 
 namespace {
 
@@ -80,9 +81,11 @@ struct gcmx_ctx {
 	double tabs_tau = NAN;
 	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso structure)
 	IsoAxis iso[3] = {};           // per-axis values for the fast kernels (tau part in build_tables)
-	bool ghosts_touched = false;   // border fills / contact copies happened
+	bool ghosts_touched = false;   // node-list border fills / contact copies / ghost uploads happened
+	unsigned faces_written = 0;    // faces (bit 2*axis + side) whose ghosts a face fill wrote
 	gcmx_path path = GCMX_PATH_AUTO;
 	gcmx_schedule sched = GCMX_SCHED_AUTO;
+	gcmx_path last_path = GCMX_PATH_AUTO;  // what the last step / stage ran
 	int rows_per_block = 0;        // fused kernel y rows per block (0 = automatic)
 	// halo exchange
 	ncclComm_t comm = nullptr;
@@ -94,12 +97,16 @@ struct gcmx_ctx {
 	std::vector<Bucket> buckets;
 	std::vector<PendingTiming> pending;
 	std::vector<hipEvent_t> event_pool;  // recycled timing events (no create/destroy per launch)
-	// scratch for border fills
+	// scratch for gcmx_border_fill (the node list of one call)
 	int* nodes_d = nullptr;
 	size_t nodes_cap = 0;
-	int* qs_d = nullptr;
-	double* vals_d = nullptr;
 	double* ode_d = nullptr;  // per-material ODE factors (256)
+};
+
+struct gcmx_border_nodes {
+	gcmx_ctx* ctx = nullptr;
+	int axis = 0, side = 0, n = 0;
+	int* nodes_d = nullptr;
 };
 
 namespace {
@@ -333,6 +340,32 @@ gcmx_path effective_path(gcmx_ctx* c) {
 
 double node_stage_bytes(const gcmx_ctx* c) { return 2.0 * c->M * sizeof(double); }
 
+// PhysicalQuantities code -> component of the D-dimensional PDE vector
+// (VelocitySigmaVariables.cpp:51-66); -1 if absent (PRESSURE: 12, handled apart).
+int quantity_comp(int D, int q) {
+	if (q >= 2 && q <= 4) return (q - 2) < D ? q - 2 : -1;
+	if (q >= 5 && q <= 10) {
+		static const int ii[6] = {0, 0, 0, 1, 1, 2}, jj[6] = {0, 1, 2, 1, 2, 2};
+		const int i = ii[q - 5], j = jj[q - 5];
+		if (i >= D || j >= D) return -1;
+		return D + (i * D - ((i - 1) * i) / 2 + j - i);
+	}
+	return -1;
+}
+
+gcmx_status border_q(const gcmx_ctx* c, int n_q, const int* qs, const double* vals, BorderQ& bq) {
+	if (n_q < 0 || n_q > kMaxBorderQ || (n_q > 0 && (!qs || !vals)))
+		return fail(GCMX_ERR_INVALID_ARG, "bad border quantities (at most 16)");
+	bq.n = n_q;
+	for (int k = 0; k < n_q; k++) {
+		if (qs[k] != 12 && quantity_comp(c->D, qs[k]) < 0)
+			return fail(GCMX_ERR_INVALID_ARG, "quantity not in this PDE vector");
+		bq.q[k] = qs[k];
+		bq.v[k] = vals[k];
+	}
+	return GCMX_OK;
+}
+
 gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	gcmx_status s = build_tables(c, tau);
 	if (s != GCMX_OK) return s;
@@ -359,6 +392,7 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "no kernel variant for this configuration");
 	HIP_TRY(hipGetLastError());
 	std::swap(c->cur, c->nxt);
+	c->last_path = p == GCMX_PATH_GENERIC ? GCMX_PATH_GENERIC : GCMX_PATH_SPLIT;
 	return GCMX_OK;
 }
 
@@ -490,8 +524,6 @@ void gcmx_destroy(gcmx_ctx* c) {
 	hipFree(c->tabs_d);
 	hipFree(c->mat_d);
 	hipFree(c->nodes_d);
-	hipFree(c->qs_d);
-	hipFree(c->vals_d);
 	hipFree(c->ode_d);
 	if (c->ev_ready) hipEventDestroy(c->ev_ready);
 	if (c->ev_halo) hipEventDestroy(c->ev_halo);
@@ -694,19 +726,10 @@ struct SlabJoin {
 	}
 };
 
-gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
-	gcmx_status s = check_ctx(c);
-	if (s) return s;
-	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
-	s = build_tables(c, tau);
-	if (s) return s;
-	if (effective_path(c) != GCMX_PATH_FUSED) {
-		for (int a = 0; a < c->D; a++) {
-			s = stage_impl(c, a, tau);
-			if (s) return s;
-		}
-		return GCMX_OK;
-	}
+// One fused step (k_step_tx2 / k_fused_xyz): the caller checked the path.
+// `fb`: y/z face conditions (x faces already filled in memory), or null.
+gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
+	gcmx_status s = GCMX_OK;
 	// One pass per step (k_fused_xyz: cur -> nxt, then swap).  Ghost planes of
 	// `cur` must hold E_n; with the X-slab schedule the exchange of the NEW
 	// boundary planes (E_{n+1}, into the ghost planes of `nxt`) runs while the
@@ -717,7 +740,7 @@ gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 	const bool halo = c->comm && (c->left >= 0 || c->right >= 0);
 	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows) {
 		Timed t(c, name, plane_bytes * (x1 - x0), st);
-		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows);
+		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb);
 	};
 	const gcmx_schedule sched =
 	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_XSLAB : GCMX_SCHED_SINGLE) : c->sched;
@@ -766,6 +789,87 @@ gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
 	HIP_TRY(hipGetLastError());
 	std::swap(c->cur, c->nxt);
+	c->last_path = GCMX_PATH_FUSED;
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	s = build_tables(c, tau);
+	if (s) return s;
+	if (effective_path(c) != GCMX_PATH_FUSED || c->faces_written != 0) {
+		for (int a = 0; a < c->D; a++) {
+			s = stage_impl(c, a, tau);
+			if (s) return s;
+		}
+		return GCMX_OK;
+	}
+	return fused_step(c, nullptr);
+}
+
+gcmx_status gcmx_step_faces(gcmx_ctx* c, double tau, const gcmx_face* faces) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	if (!faces) return fail(GCMX_ERR_INVALID_ARG, "null faces");
+	const int D = c->D;
+	BorderQ bq[6] = {};
+	unsigned on = 0;
+	for (int f = 0; f < 2 * D; f++) {
+		if (!faces[f].enabled) continue;
+		s = border_q(c, faces[f].n_quantities, faces[f].quantities, faces[f].values, bq[f]);
+		if (s) return s;
+		on |= 1u << f;
+	}
+	s = build_tables(c, tau);
+	if (s) return s;
+	// One pass: x faces in memory, y/z faces as FaceBC; the y/z faces must be
+	// free of PRESSURE (its trace needs components the fused ghosts do not form)
+	// and no face may hold ghosts written earlier but not refreshed now.
+	bool fused = D == 3 && effective_path(c) == GCMX_PATH_FUSED && fused_faces_supported(c->geo) &&
+	             (c->faces_written & ~on) == 0;
+	FaceBC fb{};
+	for (int f = 2; f < 6 && fused; f++) {
+		if (!((on >> f) & 1u)) continue;
+		fb.on |= 1u << (f - 2);
+		for (int k = 0; k < bq[f].n; k++) {
+			const int comp = quantity_comp(D, bq[f].q[k]);
+			if (comp < 0) {
+				fused = false;  // PRESSURE
+				break;
+			}
+			fb.mask[f - 2] |= 1u << comp;
+			fb.two_v[f - 2][comp] = 2 * bq[f].v[k];  // the last setting of a component wins
+		}
+	}
+	auto fill = [&](int f) -> gcmx_status {
+		s = halo_wait(c);
+		if (s) return s;
+		Timed t(c, "face_fill", 0.0, c->stream);
+		launch_face_fill(c->cur, c->geo, f / 2, (f & 1) ? 1 : -1, bq[f], c->stream);
+		HIP_TRY(hipGetLastError());
+		c->faces_written |= 1u << f;
+		return GCMX_OK;
+	};
+	if (fused) {
+		for (int f = 0; f < 2; f++)
+			if ((on >> f) & 1u) {
+				s = fill(f);
+				if (s) return s;
+			}
+		return fused_step(c, fb.on ? &fb : nullptr);
+	}
+	for (int a = 0; a < D; a++) {
+		for (int f = 2 * a; f < 2 * a + 2; f++)
+			if ((on >> f) & 1u) {
+				s = fill(f);
+				if (s) return s;
+			}
+		s = stage_impl(c, a, tau);
+		if (s) return s;
+	}
 	return GCMX_OK;
 }
 
@@ -788,13 +892,10 @@ gcmx_status gcmx_set_kernel_path(gcmx_ctx* c, gcmx_path p) {
 }
 
 gcmx_path gcmx_effective_path(gcmx_ctx* c) { return c ? effective_path(c) : GCMX_PATH_GENERIC; }
+gcmx_path gcmx_last_step_path(gcmx_ctx* c) { return c ? c->last_path : GCMX_PATH_AUTO; }
 
-gcmx_status gcmx_border_fill(gcmx_ctx* c, int axis, int side, int n_nodes, const int* nodes,
-                             int n_q, const int* qs, const double* vals) {
-	gcmx_status s = check_ctx(c);
-	if (s) return s;
-	if (axis < 0 || axis >= c->D || (side != 1 && side != -1) || n_nodes < 0 || n_q < 0 ||
-	    n_q > 32 || (n_nodes > 0 && !nodes) || (n_q > 0 && (!qs || !vals)))
+static gcmx_status check_face_nodes(gcmx_ctx* c, int axis, int side, int n_nodes, const int* nodes) {
+	if (axis < 0 || axis >= c->D || (side != 1 && side != -1) || n_nodes < 0 || (n_nodes > 0 && !nodes))
 		return fail(GCMX_ERR_INVALID_ARG, "bad border-fill arguments");
 	const int D = c->D;
 	for (int i = 0; i < n_nodes; i++) {
@@ -805,37 +906,88 @@ gcmx_status gcmx_border_fill(gcmx_ctx* c, int axis, int side, int n_nodes, const
 		const int want = side > 0 ? c->geo.sizes[axis] - 1 : 0;
 		if (nodes[i * D + axis] != want) return fail(GCMX_ERR_INVALID_ARG, "node not on the face");
 	}
-	for (int k = 0; k < n_q; k++) {
-		const int q = qs[k];
-		const bool ok = (q == 12) || (q >= 2 && q <= 4 && q - 2 < D) ||
-		                (q >= 5 && q <= 10 && (D == 3 || (D == 2 && (q == 5 || q == 6 || q == 8)) ||
-		                                      (D == 1 && q == 5)));
-		if (!ok) return fail(GCMX_ERR_INVALID_ARG, "quantity not in this PDE vector");
-	}
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_border_fill(gcmx_ctx* c, int axis, int side, int n_nodes, const int* nodes,
+                             int n_q, const int* qs, const double* vals) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if ((s = check_face_nodes(c, axis, side, n_nodes, nodes)) != GCMX_OK) return s;
+	BorderQ bq;
+	if ((s = border_q(c, n_q, qs, vals, bq)) != GCMX_OK) return s;
 	c->ghosts_touched = true;
 	s = halo_wait(c);
 	if (s) return s;
 	if (n_nodes == 0) return GCMX_OK;
-	const size_t need = (size_t)n_nodes * D;
-	HIP_TRY(hipStreamSynchronize(c->stream));  // scratch reuse
+	const size_t need = (size_t)n_nodes * c->D;
+	HIP_TRY(hipStreamSynchronize(c->stream));  // scratch reuse (gcmx_border_apply has none)
 	if (need > c->nodes_cap) {
 		hipFree(c->nodes_d);
+		c->nodes_d = nullptr;
+		c->nodes_cap = 0;
 		HIP_TRY(hipMalloc(&c->nodes_d, need * sizeof(int)));
 		c->nodes_cap = need;
 	}
-	if (!c->qs_d) {
-		HIP_TRY(hipMalloc(&c->qs_d, 32 * sizeof(int)));
-		HIP_TRY(hipMalloc(&c->vals_d, 32 * sizeof(double)));
-	}
 	HIP_TRY(hipMemcpy(c->nodes_d, nodes, need * sizeof(int), hipMemcpyHostToDevice));
-	if (n_q) {
-		HIP_TRY(hipMemcpy(c->qs_d, qs, n_q * sizeof(int), hipMemcpyHostToDevice));
-		HIP_TRY(hipMemcpy(c->vals_d, vals, n_q * sizeof(double), hipMemcpyHostToDevice));
-	}
-	launch_border_fill(c->cur, c->geo, axis, side > 0 ? -1 : 1, n_nodes, c->nodes_d, n_q, c->qs_d,
-	                   c->vals_d, c->stream);
+	launch_border_fill(c->cur, c->geo, axis, side > 0 ? -1 : 1, n_nodes, c->nodes_d, bq, c->stream);
 	HIP_TRY(hipGetLastError());
 	return GCMX_OK;
+}
+
+gcmx_status gcmx_border_nodes_create(gcmx_ctx* c, int axis, int side, int n_nodes, const int* nodes,
+                                     gcmx_border_nodes** out) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!out) return fail(GCMX_ERR_INVALID_ARG, "null output");
+	*out = nullptr;
+	if ((s = check_face_nodes(c, axis, side, n_nodes, nodes)) != GCMX_OK) return s;
+	auto* h = new gcmx_border_nodes();
+	h->ctx = c;
+	h->axis = axis;
+	h->side = side;
+	h->n = n_nodes;
+	if (n_nodes > 0) {
+		const size_t bytes = (size_t)n_nodes * c->D * sizeof(int);
+		if (hipMalloc(&h->nodes_d, bytes) != hipSuccess) {
+			delete h;
+			return fail(GCMX_ERR_OOM, "device allocation failed");
+		}
+		if (hipMemcpy(h->nodes_d, nodes, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+			hipFree(h->nodes_d);
+			delete h;
+			return fail(GCMX_ERR_HIP, "node list upload failed");
+		}
+	}
+	*out = h;
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_border_apply(gcmx_ctx* c, const gcmx_border_nodes* h, int n_q, const int* qs,
+                              const double* vals) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!h || h->ctx != c) return fail(GCMX_ERR_INVALID_ARG, "node list of another context");
+	BorderQ bq;
+	if ((s = border_q(c, n_q, qs, vals, bq)) != GCMX_OK) return s;
+	c->ghosts_touched = true;
+	s = halo_wait(c);
+	if (s) return s;
+	if (h->n == 0) return GCMX_OK;
+	Timed t(c, "border_fill", 0.0, c->stream);
+	launch_border_fill(c->cur, c->geo, h->axis, h->side > 0 ? -1 : 1, h->n, h->nodes_d, bq, c->stream);
+	HIP_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
+void gcmx_border_nodes_destroy(gcmx_border_nodes* h) {
+	if (!h) return;
+	if (h->ctx) {
+		hipSetDevice(h->ctx->device);
+		hipStreamSynchronize(h->ctx->stream);  // a pending fill may still read the list
+	}
+	hipFree(h->nodes_d);
+	delete h;
 }
 
 gcmx_status gcmx_ode_maxwell(gcmx_ctx* c, double tau, const double* tau0, int n_mat) {

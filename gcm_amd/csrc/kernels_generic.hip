@@ -134,20 +134,14 @@ __device__ __forceinline__ int quantity_component(int D, int q) {
 	return -1;
 }
 
-__global__ __launch_bounds__(64) void k_border_fill(double* __restrict__ cur, Geo g, int axis,
-                                                    int inner_sign, int n_nodes,
-                                                    const int* __restrict__ nodes, int n_q,
-                                                    const int* __restrict__ qs,
-                                                    const double* __restrict__ vals) {
-	const int i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n_nodes) return;
+// One border node: its bs ghost nodes along `axis` become the mirrored inner
+// nodes, then the condition's quantities are applied in order (std::map order in
+// the reference): ghost = -inner + 2 f(t); PRESSURE clears the vector and sets
+// the diagonal stresses.  base: element offset of the border node.
+__device__ __forceinline__ void border_point(double* __restrict__ cur, const Geo& g, long long base,
+                                             int axis, int inner_sign, const BorderQ& bq) {
 	const int D = g.D, M = g.M;
-	long long base = g.origin;
-	for (int d = 0; d < D; d++) base += (long long)nodes[i * D + d] * g.stride[d];
 	const long long st = g.stride[axis];
-	// Nodes of one face are distinct, and each thread owns its node's ghost
-	// column, so threads never race.  Quantities are applied in the caller's
-	// order (std::map order in the reference).
 	for (int a = 1; a <= g.bs; a++) {
 		const long long oi = base + inner_sign * a * st;
 		const long long og = base - inner_sign * a * st;
@@ -155,9 +149,9 @@ __global__ __launch_bounds__(64) void k_border_fill(double* __restrict__ cur, Ge
 		for (int c = 0; c < M; c++) v[c] = cur[c * g.cs + oi];
 		double w[kMaxM];
 		for (int c = 0; c < M; c++) w[c] = v[c];
-		for (int k = 0; k < n_q; k++) {
-			const int q = qs[k];
-			const double two_f = 2 * vals[k];
+		for (int k = 0; k < bq.n; k++) {
+			const int q = bq.q[k];
+			const double two_f = 2 * bq.v[k];
 			if (q == 12) {  // PRESSURE: get = -trace/D ; set clears the vector
 				double tr = 0;
 				for (int d = 0; d < D; d++) tr += v[D + (d * D - ((d - 1) * d) / 2)];
@@ -173,6 +167,37 @@ __global__ __launch_bounds__(64) void k_border_fill(double* __restrict__ cur, Ge
 		}
 		for (int c = 0; c < M; c++) cur[c * g.cs + og] = w[c];
 	}
+}
+
+// A list of face nodes (D ints each, device-resident).  Nodes of one face are
+// distinct and each thread owns its node's ghost column: no races.
+__global__ __launch_bounds__(64) void k_border_fill(double* __restrict__ cur, Geo g, int axis,
+                                                    int inner_sign, int n_nodes,
+                                                    const int* __restrict__ nodes, BorderQ bq) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n_nodes) return;
+	long long base = g.origin;
+	for (int d = 0; d < g.D; d++) base += (long long)nodes[i * g.D + d] * g.stride[d];
+	border_point(cur, g, base, axis, inner_sign, bq);
+}
+
+// Every node of the face (axis, side): the inner extent of the other axes, the
+// fastest remaining axis on the thread index (coalesced for the x and y faces).
+__global__ __launch_bounds__(256) void k_face_fill(double* __restrict__ cur, Geo g, int axis,
+                                                   int side, BorderQ bq) {
+	int ext[2] = {1, 1}, ax[2] = {0, 0}, n = 0;
+	for (int d = 0; d < g.D; d++)
+		if (d != axis) {
+			ax[n] = d;
+			ext[n] = g.sizes[d];
+			n++;
+		}
+	const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= (long long)ext[0] * ext[1]) return;
+	long long base = g.origin + (long long)(side > 0 ? g.sizes[axis] - 1 : 0) * g.stride[axis];
+	if (n == 1) base += i * g.stride[ax[0]];
+	if (n == 2) base += (i / ext[1]) * g.stride[ax[0]] + (i % ext[1]) * g.stride[ax[1]];
+	border_point(cur, g, base, axis, side > 0 ? -1 : 1, bq);
 }
 
 // ---------------------------------------------------------------- launchers --
@@ -257,11 +282,19 @@ void launch_scale_stress(double* cur, const Geo& g, const uint8_t* mat_d, const 
 }
 
 void launch_border_fill(double* cur, const Geo& g, int axis, int inner_sign, int n_nodes,
-                        const int* nodes_d, int n_q, const int* qs_d, const double* vals_d,
-                        hipStream_t st) {
+                        const int* nodes_d, const BorderQ& bq, hipStream_t st) {
 	if (n_nodes <= 0) return;
 	hipLaunchKernelGGL(k_border_fill, dim3((n_nodes + 63) / 64), dim3(64), 0, st, cur, g, axis,
-	                   inner_sign, n_nodes, nodes_d, n_q, qs_d, vals_d);
+	                   inner_sign, n_nodes, nodes_d, bq);
+}
+
+void launch_face_fill(double* cur, const Geo& g, int axis, int side, const BorderQ& bq,
+                      hipStream_t st) {
+	long long n = 1;
+	for (int d = 0; d < g.D; d++)
+		if (d != axis) n *= g.sizes[d];
+	hipLaunchKernelGGL(k_face_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cur, g, axis,
+	                   side, bq);
 }
 
 }  // namespace gcmx

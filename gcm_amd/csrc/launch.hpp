@@ -19,9 +19,20 @@ void launch_copy_box(double* dst, const Geo& gd, const double* src, const Geo& g
                      const int dmin[3], const int smin[3], const int ext[3], hipStream_t st);
 void launch_scale_stress(double* cur, const Geo& g, const uint8_t* mat_d, const double* f_d,
                          double f0, hipStream_t st);
+// The quantities of one cubic border condition, by value (kernel arguments):
+// PhysicalQuantities codes and timeDependency(t), in the reference's map order.
+constexpr int kMaxBorderQ = 16;
+struct BorderQ {
+	int n;
+	int q[kMaxBorderQ];
+	double v[kMaxBorderQ];
+};
+// BorderConditions::handleBorderPoint over a device-resident list of face nodes.
 void launch_border_fill(double* cur, const Geo& g, int axis, int inner_sign, int n_nodes,
-                        const int* nodes_d, int n_q, const int* qs_d, const double* vals_d,
-                        hipStream_t st);
+                        const int* nodes_d, const BorderQ& bq, hipStream_t st);
+// The same over every node of the face (axis, side = -1 / +1).
+void launch_face_fill(double* cur, const Geo& g, int axis, int side, const BorderQ& bq,
+                      hipStream_t st);
 
 // kernels_fast.hip -- 3-D, homogeneous, structured isotropic-elastic matrices.
 // Per-axis values the fast kernels receive by value (kernel arguments, i.e.
@@ -41,9 +52,21 @@ bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& 
                    int x1, hipStream_t st);
 // The one-pass step needs 2*bs <= Z <= 1024 (one block spans a whole z row).
 bool fused_supported(const Geo& g);
+// Uniform cubic border conditions on the y/z faces, as the one-pass step consumes
+// them (face f: 0 y-, 1 y+, 2 z-, 3 z+): the ghosts are the mirrored inner nodes
+// with the components in mask[f] set to -inner + two_v[f][c]
+// (BorderConditions.hpp:94-114; two_v = 2 * timeDependency(t)).
+struct FaceBC {
+	unsigned on;          // bit f: face f has a condition
+	unsigned mask[4];     // overridden components
+	double two_v[4][9];
+};
+// The one-pass step with FaceBC needs bs <= 2, Z <= 512 and Y, Z >= 2*bs + 2.
+bool fused_faces_supported(const Geo& g);
 // One pass per time step: X, Y, Z stages of planes [x0, x1), `a` = the three axes.
 // `chunk`: y rows per block (0 = automatic, kernels_xyz.hip: xyz_chunk_for).
+// `faces`: y/z face conditions (null: y/z ghosts of both layers are zero).
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                      int x1, hipStream_t st, int chunk = 0);
+                      int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr);
 
 }  // namespace gcmx

@@ -27,13 +27,19 @@ PATH_AUTO, PATH_GENERIC, PATH_SPLIT, PATH_FUSED = 0, 1, 2, 3
 PATH_NAMES = {0: "auto", 1: "generic", 2: "split", 3: "fused"}
 SCHED_AUTO, SCHED_SINGLE, SCHED_XSLAB = 0, 1, 2
 UNIQUE_ID_BYTES = 128
+MAX_BORDER_Q = 16
+QUANTITY_CODES = {"Vx": 2, "Vy": 3, "Vz": 4, "Sxx": 5, "Sxy": 6, "Sxz": 7, "Syy": 8, "Syz": 9,
+                  "Szz": 10, "PRESSURE": 12}
 
 # Exported symbols, in header order (checked by tests/test_abi.py).
 SYMBOLS = [
     "gcmx_abi_version", "gcmx_last_error", "gcmx_pde_size", "gcmx_status_string",
     "gcmx_create", "gcmx_destroy", "gcmx_set_materials", "gcmx_set_material_ids",
     "gcmx_upload", "gcmx_download", "gcmx_fill_random", "gcmx_stage", "gcmx_step",
-    "gcmx_set_kernel_path", "gcmx_set_step_schedule", "gcmx_effective_path", "gcmx_border_fill", "gcmx_copy_box",
+    "gcmx_set_kernel_path", "gcmx_set_step_schedule", "gcmx_effective_path", "gcmx_last_step_path",
+    "gcmx_border_fill",
+    "gcmx_border_nodes_create", "gcmx_border_apply", "gcmx_border_nodes_destroy", "gcmx_step_faces",
+    "gcmx_copy_box",
     "gcmx_ode_maxwell",
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_sync", "gcmx_stream",
@@ -51,6 +57,13 @@ class GcmxError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
         self.status = status
+
+
+class Face(ctypes.Structure):
+    """gcmx_face: one face's uniform cubic border condition."""
+    _fields_ = [("enabled", ctypes.c_int), ("n_quantities", ctypes.c_int),
+                ("quantities", ctypes.c_int * MAX_BORDER_Q),
+                ("values", ctypes.c_double * MAX_BORDER_Q)]
 
 
 class GridDesc(ctypes.Structure):
@@ -94,8 +107,15 @@ def lib() -> ctypes.CDLL:
     L.gcmx_set_kernel_path.argtypes = [vp, ctypes.c_int]
     L.gcmx_set_step_schedule.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.gcmx_effective_path.argtypes = [vp]
+    L.gcmx_last_step_path.argtypes = [vp]
     L.gcmx_border_fill.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int,
                                    ip, dp]
+    L.gcmx_border_nodes_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip,
+                                           ctypes.POINTER(vp)]
+    L.gcmx_border_apply.argtypes = [vp, vp, ctypes.c_int, ip, dp]
+    L.gcmx_border_nodes_destroy.argtypes = [vp]
+    L.gcmx_border_nodes_destroy.restype = None
+    L.gcmx_step_faces.argtypes = [vp, ctypes.c_double, ctypes.POINTER(Face)]
     L.gcmx_copy_box.argtypes = [vp, ip, ip, vp, ip]
     L.gcmx_ode_maxwell.argtypes = [vp, ctypes.c_double, dp, ctypes.c_int]
     L.gcmx_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
@@ -228,6 +248,11 @@ class Context:
     def effective_path(self) -> str:
         return PATH_NAMES[lib().gcmx_effective_path(self._ptr)]
 
+    @property
+    def last_path(self) -> str:
+        """The path the last step / stage ran (gcmx_last_step_path)."""
+        return PATH_NAMES[lib().gcmx_last_step_path(self._ptr)]
+
     def border_fill(self, axis: int, side: int, nodes: np.ndarray, quantities: Sequence[int],
                     values: Sequence[float]):
         nodes = np.ascontiguousarray(nodes, dtype=np.int32).reshape(-1, self.dim)
@@ -236,6 +261,29 @@ class Context:
         _check(lib().gcmx_border_fill(self._ptr, axis, side, nodes.shape[0],
                                       nodes.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
                                       len(quantities), q, v))
+
+    def border_nodes(self, axis: int, side: int, nodes: np.ndarray) -> "BorderNodes":
+        """gcmx_border_nodes_create: a device-resident face-node list."""
+        return BorderNodes(self, axis, side, nodes)
+
+    def border_apply(self, handle: "BorderNodes", quantities: Sequence[int], values: Sequence[float]):
+        q = _ip(quantities)
+        v = (ctypes.c_double * max(1, len(values)))(*values)
+        _check(lib().gcmx_border_apply(self._ptr, handle.ptr, len(quantities), q, v))
+
+    def step_faces(self, tau: float, faces: Sequence[Optional[Sequence[tuple]]]):
+        """gcmx_step_faces: faces[2*axis + (side > 0)] is None (no condition) or a
+        list of (quantity code, value) in the reference's application order."""
+        arr = (Face * (2 * self.dim))()
+        for f, lst in enumerate(faces[:2 * self.dim]):
+            if lst is None:
+                continue
+            arr[f].enabled = 1
+            arr[f].n_quantities = len(lst)
+            for k, (q, v) in enumerate(lst):
+                arr[f].quantities[k] = q
+                arr[f].values[k] = v
+        _check(lib().gcmx_step_faces(self._ptr, tau, arr))
 
     def copy_box(self, dst_min, dst_max, src: "Context", src_min):
         pad = lambda s: list(s) + [0] * (3 - len(s))
@@ -287,6 +335,29 @@ class Context:
     @property
     def device_bytes(self) -> int:
         return lib().gcmx_device_bytes(self._ptr)
+
+
+class BorderNodes:
+    """gcmx_border_nodes: face nodes uploaded once, applied without host sync."""
+
+    def __init__(self, ctx: Context, axis: int, side: int, nodes: np.ndarray):
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32).reshape(-1, ctx.dim)
+        self.ptr = ctypes.c_void_p()
+        self._ctx = ctx  # keeps the context alive
+        _check(lib().gcmx_border_nodes_create(ctx.ptr, axis, side, nodes.shape[0],
+                                              nodes.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                              ctypes.byref(self.ptr)))
+
+    def close(self):
+        if self.ptr and self.ptr.value:
+            lib().gcmx_border_nodes_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def halo_exchange_group(slabs: Sequence["Context"]):

@@ -92,6 +92,15 @@ struct PyEngine {
 		static const char* names[] = {"auto", "generic", "split", "fused"};
 		return names[gcmx_effective_path(c)];
 	}
+	/// The path the body's last step actually ran (gcmx_last_step_path).
+	std::string lastPath(size_t id) {
+		gcmx_ctx* c = nullptr;
+		if (D == 1) c = as<1>().getMesh(id)->ctx();
+		else if (D == 2) c = as<2>().getMesh(id)->ctx();
+		else c = as<3>().getMesh(id)->ctx();
+		static const char* names[] = {"auto", "generic", "split", "fused"};
+		return names[gcmx_last_step_path(c)];
+	}
 	real maximalEigenvalue(size_t id) {
 		if (D == 1) return as<1>().getMesh(id)->getMaximalEigenvalue();
 		if (D == 2) return as<2>().getMesh(id)->getMaximalEigenvalue();
@@ -507,6 +516,7 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    .def("run_steps", &PyEngine::runSteps)
 	    .def("pde", &PyEngine::pde, "current layer of a body, all nodes incl. ghosts [..., M]")
 	    .def("path", &PyEngine::path)
+	    .def("last_path", &PyEngine::lastPath)
 	    .def("sync", &PyEngine::sync, py::arg("body") = 0)
 	    .def("maximal_eigenvalue", &PyEngine::maximalEigenvalue)
 	    .def_property_readonly("steps", [](PyEngine& p) { return p.e->stepsDone(); })

@@ -309,7 +309,19 @@ static int quantityCode(PhysicalQuantities::T q) { return static_cast<int>(q); }
 template <int D>
 HipBorderConditions<D>::HipBorderConditions(const Task& task, const HipMesh<D>& mesh) {
 	const auto found = task.cubicBorderConditions.find(mesh.id);
-	if (found == task.cubicBorderConditions.end()) return;
+	if (found == task.cubicBorderConditions.end()) {
+		uniform = true;  // no face has a condition
+		return;
+	}
+	// per face, per face node (forEachInner order): the last condition whose
+	// area contains the node (later conditions overwrite the whole ghost)
+	std::array<std::vector<int>, 6> effective;
+	for (int f = 0; f < 2 * D; f++) {
+		size_t n = 1;
+		for (int d = 0; d < D; d++)
+			if (d != f / 2) n *= (size_t)mesh.sizes[d];
+		effective[f].assign(n, -1);
+	}
 	for (const auto& bc : found->second) {
 		Condition c;
 		c.direction = bc.direction;
@@ -318,15 +330,40 @@ HipBorderConditions<D>::HipBorderConditions(const Task& task, const HipMesh<D>& 
 			if (!hasQuantity(D, q.first)) throw Exception("border quantity not in the PDE vector");
 			c.values.push_back({q.first, q.second});  // std::map order == reference order
 		}
-		auto collect = [&](int index, std::vector<int>& out) {
+		if (c.values.size() > GCMX_MAX_BORDER_Q) throw Exception("too many border quantities");
+		const int index = (int)conditions.size();
+		auto collect = [&](int side, std::vector<int>& out) {
+			std::vector<int>& eff = effective[2 * bc.direction + side];
+			size_t k = 0;
 			forEachInner<D>(mesh.sizes, [&](const std::array<int, D>& it) {
-				if (bc.area->contains(mesh.coords(it)))
+				if (bc.area->contains(mesh.coords(it))) {
 					for (int d = 0; d < D; d++) out.push_back(it[d]);
-			}, bc.direction, index);
+					eff[k] = index;
+				}
+				k++;
+			}, bc.direction, side ? mesh.sizes[bc.direction] - 1 : 0);
 		};
 		collect(0, c.leftNodes);
-		collect(mesh.sizes[bc.direction] - 1, c.rightNodes);
+		collect(1, c.rightNodes);
+		gcmxCheck(gcmx_border_nodes_create(mesh.ctx(), c.direction, -1, (int)(c.leftNodes.size() / D),
+		                                   c.leftNodes.data(), &c.leftD), "gcmx_border_nodes_create");
+		gcmxCheck(gcmx_border_nodes_create(mesh.ctx(), c.direction, +1, (int)(c.rightNodes.size() / D),
+		                                   c.rightNodes.data(), &c.rightD), "gcmx_border_nodes_create");
 		conditions.push_back(std::move(c));
+	}
+	uniform = true;
+	for (int f = 0; f < 2 * D; f++) {
+		const std::vector<int>& eff = effective[f];
+		for (int e : eff) uniform = uniform && e == eff[0];
+		faceCondition[f] = eff.empty() ? -1 : eff[0];
+	}
+}
+
+template <int D>
+HipBorderConditions<D>::~HipBorderConditions() {
+	for (auto& c : conditions) {
+		gcmx_border_nodes_destroy(c.leftD);
+		gcmx_border_nodes_destroy(c.rightD);
 	}
 }
 
@@ -341,12 +378,25 @@ void HipBorderConditions<D>::apply(AbstractGrid& mesh_, const int direction) con
 			qs.push_back(quantityCode(v.first));
 			vals.push_back(v.second(Clock::Time()));
 		}
-		gcmxCheck(gcmx_border_fill(mesh.ctx(), direction, -1, (int)(c.leftNodes.size() / D),
-		                           c.leftNodes.data(), (int)qs.size(), qs.data(), vals.data()),
-		          "gcmx_border_fill");
-		gcmxCheck(gcmx_border_fill(mesh.ctx(), direction, +1, (int)(c.rightNodes.size() / D),
-		                           c.rightNodes.data(), (int)qs.size(), qs.data(), vals.data()),
-		          "gcmx_border_fill");
+		gcmxCheck(gcmx_border_apply(mesh.ctx(), c.leftD, (int)qs.size(), qs.data(), vals.data()),
+		          "gcmx_border_apply");
+		gcmxCheck(gcmx_border_apply(mesh.ctx(), c.rightD, (int)qs.size(), qs.data(), vals.data()),
+		          "gcmx_border_apply");
+	}
+}
+
+template <int D>
+void HipBorderConditions<D>::faces(gcmx_face* out) const {
+	for (int f = 0; f < 2 * D; f++) {
+		out[f] = gcmx_face{};
+		if (faceCondition[f] < 0) continue;
+		const Condition& c = conditions[(size_t)faceCondition[f]];
+		out[f].enabled = 1;
+		out[f].n_quantities = (int)c.values.size();
+		for (size_t k = 0; k < c.values.size(); k++) {
+			out[f].quantities[k] = quantityCode(c.values[k].first);
+			out[f].values[k] = c.values[k].second(Clock::Time());
+		}
 	}
 }
 
@@ -449,14 +499,31 @@ void Engine<D>::createGridsAndContacts(const Task& task) {
 // Engine.cpp:90-121
 template <int D>
 void Engine<D>::nextTimeStep() {
-	bool plain = true;
-	for (const Body& b : bodies) plain = plain && b.border->empty() && b.contacts.empty();
+	bool plain = true, faces = true;
+	for (const Body& b : bodies) {
+		plain = plain && b.border->empty() && b.contacts.empty();
+		faces = faces && b.border->uniformFaces() && b.contacts.empty();
+	}
 	if (plain) {
 		// No border or contact work between the stages: one gcmx_step per body
 		// (identical results; lets the library use its fused kernels).
 		for (Body& b : bodies)
 			std::static_pointer_cast<HipGridCharacteristicMethod<D>>(b.gcm)->step(
 			    Clock::TimeStep(), dynamic_cast<HipMesh<D>&>(*b.mesh));
+		applyOdes();
+		return;
+	}
+	if (faces) {
+		// Whole-face border conditions and no contacts: every stage's
+		// BorderConditions::apply is a function of the face only, so the library
+		// runs the step (fused where admissible) with the faces' values at
+		// Clock::Time() -- the time all D stages of the reference step see.
+		for (Body& b : bodies) {
+			gcmx_face f[6];
+			b.border->faces(f);
+			gcmxCheck(gcmx_step_faces(dynamic_cast<HipMesh<D>&>(*b.mesh).ctx(), Clock::TimeStep(), f),
+			          "gcmx_step_faces");
+		}
 		applyOdes();
 		return;
 	}

@@ -201,24 +201,40 @@ public:
 	virtual ~AbstractBorderConditions() = default;
 	virtual void apply(AbstractGrid& mesh, const int direction) const = 0;
 	virtual bool empty() const = 0;
+	/// Every face uniform: each node of a face has the same last-applying
+	/// condition, or none has any (then gcmx_step_faces runs the whole step).
+	virtual bool uniformFaces() const { return false; }
+	/// gcmx_face per face (2*D entries, faces[2*axis + side]) at Clock::Time().
+	virtual void faces(gcmx_face*) const {}
 };
 
 /// BorderConditions<Mesh> (BorderConditions.hpp:23-121): node lists found on the
-/// host at construction, ghost fills on the device per stage.
+/// host at construction (:46-78) and uploaded to the device once; ghost fills
+/// on the device per stage (:81-114), enqueued without host synchronisation.
+/// When every face is uniform the engine runs whole steps (gcmx_step_faces).
 template <int D>
 class HipBorderConditions : public AbstractBorderConditions {
 public:
 	HipBorderConditions(const Task& task, const HipMesh<D>& mesh);
+	~HipBorderConditions() override;
+	HipBorderConditions(const HipBorderConditions&) = delete;
+	HipBorderConditions& operator=(const HipBorderConditions&) = delete;
 	void apply(AbstractGrid& mesh, const int direction) const override;
 	bool empty() const override { return conditions.empty(); }
+	bool uniformFaces() const override { return uniform; }
+	void faces(gcmx_face* out) const override;
 
 private:
 	struct Condition {
 		int direction;
 		std::vector<int> leftNodes, rightNodes;  // D ints per node
+		gcmx_border_nodes* leftD = nullptr;      // the same lists on the device
+		gcmx_border_nodes* rightD = nullptr;
 		std::vector<std::pair<PhysicalQuantities::T, Task::TimeDependency>> values;
 	};
 	std::vector<Condition> conditions;
+	bool uniform = false;
+	std::array<int, 6> faceCondition{{-1, -1, -1, -1, -1, -1}};  // per face: condition or -1
 };
 
 /// engine/cubic/ContactConditions.hpp:20-68 (adhesion: plain copy)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GCMX_ABI_VERSION 2
+#define GCMX_ABI_VERSION 3
 
 typedef enum gcmx_status {
 	GCMX_OK = 0,
@@ -125,6 +125,9 @@ gcmx_status gcmx_set_kernel_path(gcmx_ctx* ctx, gcmx_path path);
 gcmx_status gcmx_set_step_schedule(gcmx_ctx* ctx, gcmx_schedule sched, int rows_per_block);
 /* Which path gcmx_step would take now (after materials are set). */
 gcmx_path   gcmx_effective_path(gcmx_ctx* ctx);
+/* The path the last gcmx_step / gcmx_step_faces / gcmx_stage ran
+ * (GCMX_PATH_AUTO before the first). */
+gcmx_path   gcmx_last_step_path(gcmx_ctx* ctx);
 
 /* ---- sibling plugin points ----------------------------------------------------
  * Replaces cubic::BorderConditions::handleBorderPoint
@@ -140,6 +143,39 @@ gcmx_path   gcmx_effective_path(gcmx_ctx* ctx);
 gcmx_status gcmx_border_fill(gcmx_ctx* ctx, int axis, int side, int n_nodes,
                              const int* face_nodes, int n_quantities,
                              const int* quantities, const double* values);
+/* The same with the face-node list uploaded ONCE (BorderConditions' constructor
+ * collects the nodes, BorderConditions.hpp:46-78; apply() reuses them every
+ * stage, :81-91): gcmx_border_nodes_create copies the list to the device;
+ * gcmx_border_apply enqueues the fill on the context stream with the quantities
+ * passed by value (at most GCMX_MAX_BORDER_Q) -- no host synchronisation, no
+ * copies per call.  A node list belongs to the context it was created on. */
+#define GCMX_MAX_BORDER_Q 16
+typedef struct gcmx_border_nodes gcmx_border_nodes;
+gcmx_status gcmx_border_nodes_create(gcmx_ctx* ctx, int axis, int side, int n_nodes,
+                                     const int* face_nodes, gcmx_border_nodes** out);
+gcmx_status gcmx_border_apply(gcmx_ctx* ctx, const gcmx_border_nodes* nodes, int n_quantities,
+                              const int* quantities, const double* values);
+void        gcmx_border_nodes_destroy(gcmx_border_nodes* nodes);
+
+/* One time step of a body whose cubic border conditions are UNIFORM on each face
+ * (every node of the face has the same last-applying condition, or none):
+ * equivalent to, for stage s = 0..dim-1, BorderConditions::apply(mesh, s) on the
+ * faces of axis s (BorderConditions.hpp:81-114) followed by gcmx_stage(s)
+ * (Engine::nextTimeStep, Engine.cpp:90-121, for a body without contacts).
+ * faces[2*axis + (side > 0 ? 1 : 0)], 2*dim entries; quantities as in
+ * gcmx_border_fill, values evaluated at Clock::Time().  In 3-D this keeps the
+ * one-pass step (ghost rows and columns of the intermediate stages formed in
+ * registers / LDS, x faces filled in memory first) when borderSize <= 2,
+ * Z <= 512, Y, Z >= 2*borderSize + 2 and no y/z face sets PRESSURE; otherwise it
+ * runs the stages with device-side face fills.  Results are identical either way. */
+typedef struct gcmx_face {
+	int    enabled;                       /* 0: no condition on this face      */
+	int    n_quantities;                  /* <= GCMX_MAX_BORDER_Q              */
+	int    quantities[GCMX_MAX_BORDER_Q]; /* PhysicalQuantities codes, in order */
+	double values[GCMX_MAX_BORDER_Q];     /* timeDependency(Clock::Time())      */
+} gcmx_face;
+gcmx_status gcmx_step_faces(gcmx_ctx* ctx, double tau, const gcmx_face* faces);
+
 /* Replaces ContactCopier::apply (engine/cubic/ContactConditions.hpp:56-68):
  * copy a box of `dst`'s current layer from a same-sized box of `src`'s current
  * layer (boxes as local multi-indices [min, max), may include ghosts).  Both

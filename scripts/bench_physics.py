@@ -2,8 +2,9 @@
 BorderConditions, engine/cubic/BorderConditions.hpp:81-114), optionally the
 Maxwell viscosity ODE (rheology/ode/MaxwellViscosityOde.hpp), through the C++
 engine (cubic::Engine<3>::nextTimeStep: border fill -> stage -> swap per axis,
-then the ODEs).  Border conditions change the ghosts every stage, so the engine
-runs the per-stage kernels (split path) instead of the one-pass fused step.
+then the ODEs).  The conditions cover whole faces, so the engine runs each step
+as one gcmx_step_faces call: the one-pass kernel with the y/z ghost rows and
+columns formed in registers / LDS and the x faces filled in memory first.
 
     python scripts/bench_physics.py [--n 256] [--steps 10] [--maxwell]
 """

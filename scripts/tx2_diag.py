@@ -27,7 +27,7 @@ for _ in range(steps):
 c.sync()
 assert lib.gcmx_diag_tx2(buf) == 0
 a = np.array(buf[:], dtype=np.float64).reshape(16, 8)
-names = ["Y stage", "barrier 1", "zl write+barrier 2", "Z stage", "stores(+load issue)", "X stage", "-", "-"]
+names = ["Y stage", "barrier 1", "zl write+barrier 2", "Z stages+stores", "ahead-load issue", "X stage", "-", "-"]
 tot = a.sum(axis=1)
 print("per wave-in-block: share of cycles by phase")
 for w in range(8):

@@ -37,7 +37,7 @@ def test_cpu_only_calls_fail_loudly():
     if torch.cuda.device_count() > 0:
         pytest.skip("GPU present")
     import gcm_amd
-    assert gcm_amd.lib().gcmx_abi_version() == 2
+    assert gcm_amd.lib().gcmx_abi_version() == 3
     assert gcm_amd.lib().gcmx_pde_size(3) == 9
     with pytest.raises(gcm_amd.GcmxError):
         gcm_amd.Context(3, 2, [8, 8, 8])

@@ -1,0 +1,250 @@
+"""Whole-face cubic border conditions on the device (gcmx_step_faces) and the
+device-resident face-node lists (gcmx_border_nodes_create / gcmx_border_apply),
+bitwise against the oracle's BorderConditions::apply + stage sequence
+(engine/cubic/BorderConditions.hpp:81-114, Engine.cpp:90-121).
+
+The one-pass step forms the ghost rows / columns of the intermediate Y and Z
+stages from mirrored X / Y results (kernels_xyz.hip, k_step_tx2<FACES>); these
+tests check it against the reference semantics, in which every stage's ghosts
+are written into the intermediate layer in memory before the stage runs."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import assert_same, assert_same_inner, context_for, random_state
+from tests.taskspec import host_task, oracle_task, spec
+
+pytestmark = pytest.mark.gpu
+
+QCODE = {"Vx": 2, "Vy": 3, "Vz": 4, "Sxx": 5, "Sxy": 6, "Sxz": 7, "Syy": 8, "Syz": 9, "Szz": 10,
+         "PRESSURE": 12}
+FREE = {0: ("Sxx", "Sxy", "Sxz"), 1: ("Syy", "Sxy", "Syz"), 2: ("Szz", "Sxz", "Syz")}  # ndi.hpp:30-55
+
+
+@pytest.fixture(scope="module")
+def G():
+    import gcm_amd
+    gcm_amd.lib()
+    return gcm_amd
+
+
+def face_area(D, sizes, axis, side):
+    """An axis-aligned box holding exactly the nodes of one face (h = 1, start 0)."""
+    lo = [-1e3] * 3
+    hi = [1e3] * 3
+    c = 0.0 if side < 0 else float(sizes[axis] - 1)
+    lo[axis], hi[axis] = c - 0.5, c + 0.5
+    return ("box", tuple(lo), tuple(hi))
+
+
+def face_body(D, bs, sizes, conditions):
+    """conditions: list of (axis, side or 0 for both faces, {quantity: f(t)})."""
+    bcs = []
+    for axis, side, vals in conditions:
+        area = ("infinite",) if side == 0 else face_area(D, sizes, axis, side)
+        bcs.append(O.BorderCondition(axis, area, vals))
+    t = O.Task(D=D, border_size=bs, h=[1.0] * D, cubics={0: (list(sizes), [0] * D)}, courant=0.9,
+               default_material=O.Material(4.0, 2.0, 1.0), number_of_snaps=1,
+               border_conditions={0: bcs})
+    return O.Engine(t).bodies[0]
+
+
+def faces_at(D, conditions, time):
+    """gcmx_step_faces argument: per face the last condition covering it, its
+    quantities in the reference's std::map order evaluated at `time`."""
+    faces = [None] * (2 * D)
+    for axis, side, vals in conditions:
+        lst = sorted(vals.items(), key=lambda kv: O.QUANTITY_ORDER.index(kv[0]))
+        entry = [(QCODE[q], f(time)) for q, f in lst]
+        for s in ((0, 1) if side == 0 else ((0,) if side < 0 else (1,))):
+            faces[2 * axis + s] = entry
+    return faces
+
+
+def free(axis, normal=lambda t: 0.0):
+    q = FREE[axis]
+    return {q[0]: normal, q[1]: lambda t: 0.0, q[2]: lambda t: 0.0}
+
+
+FACE_CASES = {
+    # free surfaces on all six faces, odd X, Z = 70 (idle lanes), Courant 0.9
+    "free_all": (2, [9, 40, 70], [(0, 0, free(0)), (1, 0, free(1)), (2, 0, free(2))], 0.9, "fused"),
+    # some faces only, time-dependent normal force on y+ and z-, Z = ZT (no idle lanes)
+    "some_faces": (2, [8, 30, 64], [(1, 1, free(1, lambda t: 0.3 * math.sin(2 * t))),
+                                    (2, -1, free(2, lambda t: -0.2 + 0.1 * t)),
+                                    (0, -1, {"Vx": lambda t: 0.05})], 0.9, "fused"),
+    # an overriding later condition on one face (the last one covering a face wins)
+    "override": (2, [10, 22, 33], [(1, 0, free(1)), (1, -1, {"Vy": lambda t: 0.1, "Sxy": lambda t: 0.0}),
+                                   (2, 0, {"Vz": lambda t: -0.3})], 0.9, "fused"),
+    # borderSize 1
+    "bs1": (1, [7, 12, 20], [(0, 0, free(0)), (1, 0, free(1)), (2, 0, free(2))], 0.9, "fused"),
+    # Courant 1.5 with borderSize 2: floor(q) = 1 on the fast waves (no shared x differences)
+    "courant15": (2, [10, 12, 16], [(1, 0, free(1)), (2, 1, free(2, lambda t: 0.5))], 1.5, "fused"),
+    # PRESSURE on a y face: its trace needs node-only components -> per-stage path
+    "pressure_y": (2, [6, 20, 40], [(1, -1, {"PRESSURE": lambda t: 0.25}), (2, 0, free(2))], 0.9, "split"),
+    # PRESSURE on an x face is filled in memory: still one pass
+    "pressure_x": (2, [6, 20, 40], [(0, 1, {"PRESSURE": lambda t: 0.25}), (2, 0, free(2))], 0.9, "fused"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FACE_CASES))
+def test_step_faces_matches_oracle(G, name):
+    bs, sizes, conds, tau, path = FACE_CASES[name]
+    b = face_body(3, bs, sizes, conds)
+    random_state(b, seed=len(name) + sizes[2], ghosts=False)
+    ctx = context_for(b)
+    t = 0.0
+    for step in range(3):
+        for s in range(3):
+            b.apply_border(s, t)
+            b.stage(s, tau)
+        ctx.step_faces(tau, faces_at(3, conds, t))
+        assert ctx.last_path == path, f"{name}: ran {ctx.last_path}"
+        assert_same_inner(ctx, b, f"faces {name} step {step}")
+        t += tau
+
+
+def test_step_faces_512_slab_headline_instance(G):
+    """The benchmark kernel instance (bs 2, Z = ZT = 512, uniform axes) with free
+    surfaces on every face, a thin slab of the 512^3 grid."""
+    conds = [(0, 0, free(0)), (1, 0, free(1, lambda t: 0.1)), (2, 0, free(2))]
+    b = face_body(3, 2, [4, 24, 512], conds)
+    random_state(b, seed=512, ghosts=False)
+    ctx = context_for(b)
+    for step in range(2):
+        for s in range(3):
+            b.apply_border(s, 0.0)
+            b.stage(s, 0.9)
+        ctx.step_faces(0.9, faces_at(3, conds, 0.0))
+        assert ctx.last_path == "fused"
+        assert_same_inner(ctx, b, f"512 slab step {step}")
+
+
+def test_step_faces_2d_and_1d(G):
+    """gcmx_step_faces in 2-D and 1-D (per-stage path, device face fills)."""
+    for D, sizes, conds in ((2, [15, 11], [(0, 0, {"Sxx": lambda t: 0.2, "Sxy": lambda t: 0.0}),
+                                          (1, 1, {"Vy": lambda t: -0.1})]),
+                            (1, [40], [(0, 0, {"Sxx": lambda t: 0.5})])):
+        bcs = [O.BorderCondition(a, ("infinite",) if s == 0 else face_area(D, sizes, a, s), v)
+               for a, s, v in conds]
+        task = O.Task(D=D, border_size=2, h=[1.0] * D, cubics={0: (sizes, [0] * D)}, courant=0.9,
+                      default_material=O.Material(4.0, 2.0, 1.0), number_of_snaps=1,
+                      border_conditions={0: bcs})
+        b = O.Engine(task).bodies[0]
+        random_state(b, seed=D, ghosts=False)
+        ctx = context_for(b)
+        for step in range(3):
+            for s in range(D):
+                b.apply_border(s, 0.0)
+                b.stage(s, 0.9)
+            ctx.step_faces(0.9, faces_at(D, conds, 0.0))
+            assert_same_inner(ctx, b, f"D={D} step {step}")
+
+
+def test_step_faces_after_split_fills_keeps_parity(G):
+    """A face filled in memory by an earlier per-stage step and disabled later keeps
+    its stale ghosts, as in the reference: the library must not run the one-pass
+    step then (it would read zeros there)."""
+    conds = [(1, 0, free(1)), (2, 0, free(2))]
+    b = face_body(3, 2, [6, 12, 20], conds)
+    random_state(b, seed=5, ghosts=False)
+    ctx = context_for(b)
+    ctx.set_path(G.PATH_SPLIT)
+    for s in range(3):
+        b.apply_border(s, 0.0)
+        b.stage(s, 0.9)
+    ctx.step_faces(0.9, faces_at(3, conds, 0.0))
+    assert ctx.last_path == "split"
+    ctx.set_path(G.PATH_AUTO)
+    only_z = [(2, 0, free(2))]  # the y faces drop out; their ghost rows keep old values
+    b.border = [e for e in b.border if e[0] == 2]
+    for s in range(3):
+        b.apply_border(s, 0.0)
+        b.stage(s, 0.9)
+    ctx.step_faces(0.9, faces_at(3, only_z, 0.0))
+    assert ctx.last_path == "split"
+    assert_same(ctx, b, "stale y ghosts")
+
+
+def test_border_nodes_apply_matches_oracle(G):
+    """Device-resident node lists: uploaded once, applied per stage."""
+    D, bs = 3, 2
+    sizes = [7, 9, 8]
+    conds = [O.BorderCondition(0, ("box", (-1, 1.5, -1), (100, 5.5, 100)),
+                               {"Sxx": lambda t: 0.5, "Sxy": lambda t: -0.25}),
+             O.BorderCondition(1, ("infinite",), {"PRESSURE": lambda t: 0.125}),
+             O.BorderCondition(2, ("sphere", 4, (3, 4, 0)), {"Vz": lambda t: 0.3})]
+    t = O.Task(D=D, border_size=bs, h=[1.0] * D, cubics={0: (sizes, [0] * D)}, courant=0.9,
+               default_material=O.Material(4, 2, 1), number_of_snaps=1, border_conditions={0: conds})
+    b = O.Engine(t).bodies[0]
+    random_state(b, seed=9, ghosts=True)
+    ctx = context_for(b)
+    handles = [(d, ctx.border_nodes(d, -1, left), ctx.border_nodes(d, +1, right), vals)
+               for d, left, right, vals in b.border]
+    for rep in range(2):
+        for direction in range(D):
+            b.apply_border(direction, 0.1 * rep)
+            for d, hl, hr, vals in handles:
+                if d != direction:
+                    continue
+                qs = [QCODE[q] for q, _ in vals]
+                vs = [f(0.1 * rep) for _, f in vals]
+                ctx.border_apply(hl, qs, vs)
+                ctx.border_apply(hr, qs, vs)
+            assert_same(ctx, b, f"border nodes direction {direction} rep {rep}")
+            b.stage(direction, 0.9)
+            ctx.stage(direction, 0.9)
+            assert_same(ctx, b, f"stage {direction} rep {rep}")
+
+
+@pytest.fixture(scope="module")
+def H():
+    from gcm_amd import _gcm_host
+    return _gcm_host
+
+
+def run_both(H, s):
+    oe = O.Engine(oracle_task(s))
+    he = H.Engine(host_task(s))
+    oe.run()
+    he.run()
+    assert he.steps == oe.steps_done
+    return oe, he
+
+
+def test_engine_free_surfaces_one_pass(H):
+    """The cube task's free surfaces (launcher/main.cpp:209-220: FIXED_FORCE zero on
+    every face) plus a time-dependent normal load on the top face, through
+    Task -> Engine::run: whole-face conditions, so every step is one pass."""
+    f = lambda t: -0.4 * math.exp(-(t - 1.0) ** 2)
+    N = 16
+    s = spec(3, 2, [1, 1, 1], {0: ([N, N + 2, N + 4], [0, 0, 0])}, 0.9, (4, 2, 1), snaps=6,
+             quantities=[(("sphere", 4, (8, 9, 10)), "PRESSURE", 1.0)],
+             borders={0: [(0, ("infinite",), {q: (lambda t: 0.0) for q in FREE[0]}),
+                          (1, ("infinite",), {q: (lambda t: 0.0) for q in FREE[1]}),
+                          (2, ("infinite",), {q: (lambda t: 0.0) for q in FREE[2]}),
+                          (1, ("box", (-1e3, N + 0.5, -1e3), (1e3, N + 1.5, 1e3)),
+                           {"Syy": f, "Sxy": lambda t: 0.0, "Syz": lambda t: 0.0})]})
+    oe, he = run_both(H, s)
+    assert he.last_path(0) == "fused"
+    b = oe.bodies[0]
+    got = b.inner_view(he.pde(0).reshape(b.pde.shape))
+    want = b.inner_view(b.pde)
+    assert np.array_equal(got, want), f"{int((got != want).sum())} inner values differ"
+
+
+def test_engine_partial_face_uses_node_lists(H):
+    """A condition covering part of a face (titan's cylinder, ndi.hpp:309-315) keeps
+    the per-stage path with device-resident node lists."""
+    N = 12
+    s = spec(3, 2, [1, 1, 1], {0: ([N, N, N], [0, 0, 0])}, 0.9, (4, 2, 1), snaps=4,
+             quantities=[(("sphere", 3, (6, 6, 6)), "PRESSURE", 1.0)],
+             borders={0: [(1, ("infinite",), {q: (lambda t: 0.0) for q in FREE[1]}),
+                          (1, ("cylinder", 2.5, (6, -5, 6), (6, 20, 6)), {"Vy": lambda t: -0.3})]})
+    oe, he = run_both(H, s)
+    assert he.last_path(0) == "split"
+    got = he.pde(0)
+    want = oe.bodies[0].pde.reshape(got.shape)
+    assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"
