@@ -36,8 +36,9 @@ def main(prof_dir, out, n=512):
                            "read8_fetch_bytes": r8, "fetch_factor": ff,
                            "write8_write_bytes": w8, "write_factor": wf},
            "kernels": {}}
+    # bench.py's bucket "fused_xyz" is the one-pass step: k_step_tx2 (default) or k_fused_xyz
     for short, frag in (("march_x", "k_march<0, 2"), ("fused_yz", "k_fused_yz<2, 512"),
-                        ("fused_xyz", "k_fused_xyz<2, 512")):
+                        ("fused_xyz", "k_fused_xyz<2, 512"), ("fused_xyz", "k_step_tx2<2, 512")):
         fks = [v for k, v in f.items() if frag in k]
         wks = [v for k, v in w.items() if frag in k]
         if not fks or not wks:
