@@ -220,6 +220,7 @@ int main() {
 	family<1, 1>(in, out, 128);
 	family_tx<1>(in, out, 128);
 	family_tx<2>(in, out, 128);
+	family_tx<4>(in, out, 128);
 	ops_tx<2, 180>(in, out, 128);
 	ops_tx<2, 360>(in, out, 128);
 	ops_tx<2, 540>(in, out, 128);
