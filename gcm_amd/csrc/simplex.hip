@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "../../include/gcmx.h"
@@ -42,10 +43,10 @@ gcmx_status fail(gcmx_status s, const std::string& msg) {
 			return fail(GCMX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
 	} while (0)
 
-struct BorderArgs {  // per-condition data passed by value with every launch
+struct BorderArgs {  // static per-condition data passed by value with every launch
 	int type[GSX_MAX_BORDER_CONDITIONS];
 	double minDet[GSX_MAX_BORDER_CONDITIONS][3];
-	double b[GSX_MAX_BORDER_CONDITIONS][3];
+	const double* b;  // device [condition][3]: b(t) of the step, written per step
 };
 
 struct BorderDev {
@@ -96,6 +97,48 @@ struct gsx_ctx {
 	int* corrOf = nullptr;               // node -> border-plan entry or -1
 	char* deferred = nullptr;            // node in a contact: the contact kernel finalizes it
 	std::vector<char> hostDeferred;
+	double* bvals = nullptr;             // [GSX_MAX_BORDER_CONDITIONS][3] border values b(t)
+	std::unique_ptr<struct StepGraphs> graphs;  // gsx_step's replayed steps (this ctx leads)
+};
+
+// The host-side state a simplex step changes (pointer swaps, chaining flag).
+struct BodyState {
+	double *u, *un, *w, *wnext;
+	bool chained;
+	bool operator==(const BodyState& o) const {
+		return u == o.u && un == o.un && w == o.w && wnext == o.wnext && chained == o.chained;
+	}
+};
+static BodyState body_state(const gsx_ctx* c) { return {c->u, c->un, c->w, c->wnext, c->chained}; }
+static void set_body_state(gsx_ctx* c, const BodyState& b) {
+	c->u = b.u;
+	c->un = b.un;
+	c->w = b.w;
+	c->wnext = b.wnext;
+	c->chained = b.chained;
+}
+
+// One captured step per entry state: a step swaps u/un, so two graphs alternate.
+struct StepGraphs {
+	std::vector<gsx_ctx*> bodies;
+	std::vector<gsx_contact*> contacts;
+	struct Entry {
+		std::vector<BodyState> before, after;
+		hipGraph_t graph = nullptr;
+		hipGraphExec_t exec = nullptr;
+	};
+	std::vector<Entry> entries;
+	hipEvent_t evFork = nullptr, evJoin = nullptr;
+	std::vector<hipEvent_t> evBody;
+	~StepGraphs() {
+		for (auto& e : entries) {
+			if (e.exec) (void)hipGraphExecDestroy(e.exec);
+			if (e.graph) (void)hipGraphDestroy(e.graph);
+		}
+		if (evFork) (void)hipEventDestroy(evFork);
+		if (evJoin) (void)hipEventDestroy(evJoin);
+		for (hipEvent_t e : evBody) (void)hipEventDestroy(e);
+	}
 };
 
 struct gsx_contact {
@@ -387,7 +430,7 @@ __device__ void border_correct(double (&w)[kM], int t, const int* __restrict__ c
 	const int c = cond[t];
 	const int code = outer[(size_t)stage * count + t];
 	const double* B = Bm + 27 * (size_t)t;
-	const double b[3] = {args.b[c][0], args.b[c][1], args.b[c][2]};
+	const double b[3] = {args.b[3 * c], args.b[3 * c + 1], args.b[3 * c + 2]};
 	const double minValid = args.minDet[c][stage];
 	double u[kM];
 	mat_vec(U1, w, u);
@@ -480,6 +523,15 @@ __global__ __launch_bounds__(256) void k_sx_inner(
 	finalize(n, out, U1, Unext, un, wnext, N);
 }
 
+// The step's border values b(t) into device memory (gsx_set_border_values).
+struct BorderValues {
+	double b[3 * GSX_MAX_BORDER_CONDITIONS];
+};
+__global__ __launch_bounds__(64) void k_sx_set_border_values(double* __restrict__ dst, BorderValues v,
+                                                             int n) {
+	for (int i = threadIdx.x; i < n; i += 64) dst[i] = v.b[i];
+}
+
 // BorderCorrectorInPdeVectors::applyPlainCorrection (BorderCorrector.hpp:167-178) on
 // the current layer.
 __global__ __launch_bounds__(64) void k_sx_plain(const int* __restrict__ nodes,
@@ -489,7 +541,7 @@ __global__ __launch_bounds__(64) void k_sx_plain(const int* __restrict__ nodes,
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int n = nodes[t], c = cond[t];
-	const double b[3] = {args.b[c][0], args.b[c][1], args.b[c][2]};
+	const double b[3] = {args.b[3 * c], args.b[3 * c + 1], args.b[3 * c + 2]};
 	double u[kM];
 	for (int k = 0; k < kM; k++) u[k] = u_[k * N + n];
 	plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
@@ -668,6 +720,11 @@ gcmx_status gsx_create(int device, int n_nodes, const double* coords, gsx_ctx** 
 		gsx_destroy(c);
 		return s;
 	}
+	if (hipMalloc(&c->bvals, 3 * GSX_MAX_BORDER_CONDITIONS * sizeof(double)) != hipSuccess ||
+	    hipMemset(c->bvals, 0, 3 * GSX_MAX_BORDER_CONDITIONS * sizeof(double)) != hipSuccess) {
+		gsx_destroy(c);
+		return fail(GCMX_ERR_OOM, "simplex border-value allocation failed");
+	}
 	*out = c;
 	return GCMX_OK;
 }
@@ -676,6 +733,8 @@ void gsx_destroy(gsx_ctx* c) {
 	if (!c) return;
 	(void)hipSetDevice(c->device);
 	if (c->stream) (void)hipStreamSynchronize(c->stream);
+	c->graphs.reset();
+	if (c->bvals) (void)hipFree(c->bvals);
 	void* ptrs[] = {c->coords, c->u, c->un, c->w, c->wn, c->grad, c->wnext, c->corrOf, c->deferred,
 	                c->mats, c->gOff, c->gNb,
 	                c->gRows, c->gW, c->gM, c->gDet};
@@ -850,6 +909,7 @@ gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const d
 	bd.n = n;
 	bd.nCond = n_cond;
 	bd.args = BorderArgs{};
+	bd.args.b = c->bvals;
 	for (int i = 0; i < n_cond; i++) {
 		bd.args.type[i] = type[i];
 		for (int st = 0; st < 3; st++) bd.args.minDet[i][st] = min_det[i * 3 + st];
@@ -864,8 +924,16 @@ gcmx_status gsx_set_border_values(gsx_ctx* c, const double* b) {
 	if (s) return s;
 	if (!c->bd.set) return fail(GCMX_ERR_STATE, "border plan not set");
 	if (c->bd.nCond && !b) return fail(GCMX_ERR_INVALID_ARG, "null border values");
-	for (int i = 0; i < c->bd.nCond; i++)
-		for (int k = 0; k < 3; k++) c->bd.args.b[i][k] = b[i * 3 + k];
+	// written by a one-block kernel whose arguments carry the values: ordered on
+	// the context stream before the step that reads them, with no host buffer
+	// that must outlive the call
+	if (c->bd.nCond) {
+		BorderValues v{};
+		for (int i = 0; i < 3 * c->bd.nCond; i++) v.b[i] = b[i];
+		hipLaunchKernelGGL(k_sx_set_border_values, dim3(1), dim3(64), 0, c->stream, c->bvals, v,
+		                   3 * c->bd.nCond);
+		SX_TRY(hipGetLastError());
+	}
 	c->bd.valuesSet = true;
 	return GCMX_OK;
 }
@@ -1043,6 +1111,108 @@ gcmx_status gsx_contact_correct(gsx_contact* c, int stage) {
 		                   c->minDet[stage][1], nextU(c->a, stage), nextU(c->b, stage), c->a->un,
 		                   c->b->un, c->a->wnext, c->b->wnext);
 	});
+}
+
+namespace {
+// The step body: Engine::nextTimeStep after setBorderValues (simplex/Engine.cpp:95-116,
+// 119-143): plain corrections (contacts, then bodies), then per stage the bodies'
+// beforeStage + contactAndBorderStage, the contact correctors, the bodies' finish.
+gcmx_status step_body(const std::vector<gsx_ctx*>& bodies, const std::vector<gsx_contact*>& contacts) {
+	gcmx_status s;
+	for (gsx_contact* k : contacts)
+		if ((s = gsx_contact_plain(k))) return s;
+	for (gsx_ctx* b : bodies)
+		if (b->bd.set && b->bd.n && (s = gsx_plain_correction(b))) return s;
+	for (int stage = 0; stage < 3; stage++) {
+		for (gsx_ctx* b : bodies)
+			if ((s = gsx_stage_nodes(b, stage))) return s;
+		for (gsx_contact* k : contacts)
+			if ((s = gsx_contact_correct(k, stage))) return s;
+		for (gsx_ctx* b : bodies)
+			if ((s = gsx_stage_finish(b, stage))) return s;
+	}
+	return GCMX_OK;
+}
+}  // namespace
+
+gcmx_status gsx_step(gsx_ctx* const* bodies_, int n_bodies, gsx_contact* const* contacts_,
+                     int n_contacts) {
+	if (!bodies_ || n_bodies < 1 || n_contacts < 0 || (n_contacts > 0 && !contacts_))
+		return fail(GCMX_ERR_INVALID_ARG, "bad gsx_step arguments");
+	std::vector<gsx_ctx*> bodies(bodies_, bodies_ + n_bodies);
+	std::vector<gsx_contact*> contacts(contacts_, contacts_ + n_contacts);
+	gsx_ctx* lead = bodies[0];
+	gcmx_status s;
+	for (gsx_ctx* b : bodies) {
+		if ((s = check(b))) return s;
+		if (b->device != lead->device) return fail(GCMX_ERR_INVALID_ARG, "bodies on different devices");
+		if (b->bd.set && b->bd.n && !b->bd.valuesSet) return fail(GCMX_ERR_STATE, "border values not set");
+	}
+	for (gsx_contact* k : contacts) {
+		bool in = false;
+		for (gsx_ctx* b : bodies) in = in || (k && (k->a == b || k->b == b));
+		if (!k || !in) return fail(GCMX_ERR_INVALID_ARG, "contact of a body outside the group");
+	}
+	SX_TRY(hipSetDevice(lead->device));
+	if (!lead->graphs || lead->graphs->bodies != bodies || lead->graphs->contacts != contacts) {
+		lead->graphs.reset(new StepGraphs());
+		StepGraphs& g = *lead->graphs;
+		g.bodies = bodies;
+		g.contacts = contacts;
+		g.evBody.assign(bodies.size(), nullptr);
+		SX_TRY(hipEventCreateWithFlags(&g.evFork, hipEventDisableTiming));
+		SX_TRY(hipEventCreateWithFlags(&g.evJoin, hipEventDisableTiming));
+		for (auto& e : g.evBody) SX_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+	}
+	StepGraphs& g = *lead->graphs;
+	std::vector<BodyState> now;
+	for (gsx_ctx* b : bodies) now.push_back(body_state(b));
+	StepGraphs::Entry* hit = nullptr;
+	for (auto& e : g.entries)
+		if (e.before == now) hit = &e;
+	if (!hit) {
+		// Capture the step: the other bodies' streams join the capture through an
+		// event of the lead stream and rejoin it at the end.  Kernels do not run
+		// during capture; the host-side swaps do, and are restored afterwards.
+		StepGraphs::Entry e;
+		e.before = now;
+		SX_TRY(hipStreamBeginCapture(lead->stream, hipStreamCaptureModeRelaxed));
+		s = GCMX_OK;
+		if (hipEventRecord(g.evFork, lead->stream) != hipSuccess) s = fail(GCMX_ERR_HIP, "capture fork");
+		for (size_t i = 1; i < bodies.size() && !s; i++)
+			if (hipStreamWaitEvent(bodies[i]->stream, g.evFork, 0) != hipSuccess) s = fail(GCMX_ERR_HIP, "capture fork");
+		if (!s) s = step_body(bodies, contacts);
+		for (size_t i = 1; i < bodies.size() && !s; i++)
+			if (hipEventRecord(g.evBody[i], bodies[i]->stream) != hipSuccess ||
+			    hipStreamWaitEvent(lead->stream, g.evBody[i], 0) != hipSuccess)
+				s = fail(GCMX_ERR_HIP, "capture join");
+		hipGraph_t graph = nullptr;
+		const hipError_t ec = hipStreamEndCapture(lead->stream, &graph);
+		for (gsx_ctx* b : bodies) e.after.push_back(body_state(b));
+		for (size_t i = 0; i < bodies.size(); i++) set_body_state(bodies[i], e.before[i]);
+		if (s || ec != hipSuccess || !graph) {
+			if (graph) (void)hipGraphDestroy(graph);
+			return s ? s : fail(GCMX_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+		}
+		e.graph = graph;
+		if (hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0) != hipSuccess) {
+			(void)hipGraphDestroy(graph);
+			return fail(GCMX_ERR_HIP, "hipGraphInstantiate failed");
+		}
+		g.entries.push_back(e);
+		hit = &g.entries.back();
+	}
+	// The other bodies' pending work (border values, uploads) precedes the graph,
+	// and their later work follows it.
+	for (size_t i = 1; i < bodies.size(); i++) {
+		SX_TRY(hipEventRecord(g.evBody[i], bodies[i]->stream));
+		SX_TRY(hipStreamWaitEvent(lead->stream, g.evBody[i], 0));
+	}
+	SX_TRY(hipGraphLaunch(hit->exec, lead->stream));
+	SX_TRY(hipEventRecord(g.evJoin, lead->stream));
+	for (size_t i = 1; i < bodies.size(); i++) SX_TRY(hipStreamWaitEvent(bodies[i]->stream, g.evJoin, 0));
+	for (size_t i = 0; i < bodies.size(); i++) set_body_state(bodies[i], hit->after[i]);
+	return GCMX_OK;
 }
 
 gcmx_status gsx_sync(gsx_ctx* c) {

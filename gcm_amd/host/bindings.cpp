@@ -500,6 +500,8 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    .def("number_of_vertices", [](PySimplexEngine& p, size_t body) { return p.e->mesh(body).nVertices(); },
 	         py::arg("body") = 0)
 	    .def("sync", [](PySimplexEngine& p) { p.e->sync(); }, "wait for the bodies' streams")
+	    .def("set_replay_steps", [](PySimplexEngine& p, bool on) { p.e->setReplaySteps(on); },
+	         "gsx_step graph replay or the individual stage calls (default)", py::arg("on"))
 	    .def_property_readonly("steps", [](PySimplexEngine& p) { return p.e->stepsDone(); })
 	    .def_property_readonly("time_step", [](PySimplexEngine& p) { return p.e->timeStepValue(); })
 	    .def_property_readonly("required_time", [](PySimplexEngine& p) { return p.e->getRequiredTime(); });

@@ -1241,6 +1241,13 @@ real Engine::estimateTimeStep() { return tau; }
 // correctors, then (per body) its border correctors, innerStage, afterStage, swap.
 void Engine::nextTimeStep() {
 	setBorderValues(Clock::Time() + Clock::TimeStep());
+	if (replaySteps) {  // the same calls, captured once per layer state and replayed
+		std::vector<gsx_ctx*> ctxs;
+		for (auto& b : bodies) ctxs.push_back(b.ctx);
+		gcmxCheck(gsx_step(ctxs.data(), (int)ctxs.size(), contacts.data(), (int)contacts.size()),
+		          "gsx_step");
+		return;
+	}
 	plainCorrections();
 	for (int stage = 0; stage < 3; stage++) {
 		for (auto& b : bodies) gcmxCheck(gsx_stage_nodes(b.ctx, stage), "gsx_stage_nodes");

@@ -320,6 +320,17 @@ gcmx_status gsx_contact_plain(gsx_contact* c);
 /* applyInGlobalBasis at stage `stage` (ContactCorrector.hpp:333-348, 150-247) on the
  * new-layer invariants; call between gsx_stage_nodes and gsx_stage_finish of both bodies. */
 gcmx_status gsx_contact_correct(gsx_contact* c, int stage);
+/* One whole time step of a group of bodies and their contacts
+ * (simplex::Engine::nextTimeStep after setBorderValues, engine/simplex/Engine.cpp:95-143:
+ * plain corrections of the contacts then of the bodies, then for each stage every
+ * body's gsx_stage_nodes, every contact's gsx_contact_correct, every body's
+ * gsx_stage_finish) -- the same kernels as those calls, captured once per layer
+ * state into a HIP graph and replayed, so a step costs one launch instead of
+ * ~12 (the reference's mesh sizes are launch-bound).  Border values are read
+ * from device memory written by gsx_set_border_values, so they may change
+ * every step.  Results are identical to the individual calls. */
+gcmx_status gsx_step(gsx_ctx* const* bodies, int n_bodies, gsx_contact* const* contacts,
+                     int n_contacts);
 gcmx_status gsx_sync(gsx_ctx* ctx);
 
 /* ---- synchronisation and timing ------------------------------------------- */

@@ -156,3 +156,28 @@ def test_inm_mesh_engine_matches_oracle(H, tmp_path):
     for i in range(2):
         got, want = e.pde(i), np.array(o.bodies[i].u)
         assert np.array_equal(got, want), f"body {i}: {int((got != want).sum())} values differ"
+
+
+@pytest.mark.parametrize("workload", ["cube", "layered"])
+def test_graph_replayed_steps_equal_individual_calls(H, workload):
+    """gsx_step (one step captured into a HIP graph per layer state and replayed)
+    == the individual gsx_stage_nodes / gsx_contact_correct / gsx_stage_finish
+    calls, bitwise, over enough steps to replay both layer parities, with
+    time-dependent border values, and for two bodies with a contact (streams of
+    both bodies in one graph)."""
+    from tests.simplex_spec import MIXED_BORDER, host_task, layered_task
+    import numpy as np
+    mk = (lambda: host_task(6, 1.0, 0.1, 7, border=MIXED_BORDER)) if workload == "cube" else \
+        (lambda: layered_task(5, 1.0))
+    def run(replay):  # one engine at a time: Clock is process-global, as in the reference
+        e = H.SimplexEngine(mk())
+        e.set_replay_steps(replay)
+        out = []
+        for chunk in (1, 2, 3):
+            e.run_steps(chunk)
+            out.append([e.pde(body) for body in range(e.number_of_bodies)])
+        return out
+    a, b = run(True), run(False)
+    for k, (xa, xb) in enumerate(zip(a, b)):
+        for body, (pa, pb) in enumerate(zip(xa, xb)):
+            assert np.array_equal(pa, pb), f"{workload} body {body} after chunk {k}"
