@@ -537,7 +537,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	unsigned long long dt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
 #endif
-	for (int y = yb; y < ye; y++) {
+	auto row = [&](int y) {
 		double yv[2][9];
 		const int ring = (y + BS) % (BS + 1);
 #pragma unroll
@@ -620,7 +620,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			}
 		}
 		TX2_T(5);
-	}
+	};
+	for (int y = yb; y < ye; y++) row(y);
 #if GCMX_TX2_DIAG
 	if ((threadIdx.x & 63) == 0) {
 		const int wv = threadIdx.x / 64;

@@ -2,13 +2,17 @@
 """Per-GPU time of one X slab of the 512^3 strong-scaling run, on ONE GPU.
 
 For each slab thickness X (512 / N for N = 1, 2, 4, 8) a [X, 512, 512] context
-runs the fused step; with GCMX_SLAB_SCHEDULE=1 in the environment it runs the
-multi-GPU step schedule (interior planes on the low-priority stream, 16-row
-boundary blocks on the main stream) without a communicator, i.e. everything an
-N-rank run does per GPU except the RCCL transfers (which it overlaps).
+runs the fused step; with --sched xslab it runs the multi-GPU step schedule
+(gcmx_set_step_schedule(GCMX_SCHED_XSLAB): interior planes on the low-priority
+stream, 16-row boundary blocks beside them) without a communicator, i.e.
+everything an N-rank run does per GPU except the RCCL transfers (which it
+overlaps).  --rows sets the interior's y rows per block (0: automatic).
 Also checks the slab step bitwise against the generic per-stage path on a
 [64, 512, 512] slab.  One JSON line per size on stdout.
+
+    python scripts/bench_slab.py [--sched single|xslab] [--rows R] [--ranks 1,2,4,8]
 """
+import argparse
 import json
 import os
 import sys
@@ -20,33 +24,43 @@ import gcm_amd  # noqa: E402
 from gcm_amd import gcmx  # noqa: E402
 from gcm_amd.host import isotropic_elastic_matrices  # noqa: E402
 
+ap = argparse.ArgumentParser()
+ap.add_argument("--sched", default="xslab", choices=["single", "xslab"])
+ap.add_argument("--rows", type=int, default=0)
+ap.add_argument("--ranks", default="1,2,4,8")
+ap.add_argument("--n", type=int, default=512)
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--no-check", action="store_true")
+args = ap.parse_args()
 U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
-N = int(os.environ.get("SLAB_N", "512"))
-STEPS = int(os.environ.get("SLAB_STEPS", "20"))
+N, STEPS = args.n, args.steps
+SCHED = gcmx.SCHED_XSLAB if args.sched == "xslab" else gcmx.SCHED_SINGLE
 
 
 def make(X, path=gcmx.PATH_AUTO, x0=0):
     c = gcm_amd.Context(3, 2, [X, N, N], start=[x0, 0, 0], device=0)
     c.set_materials(U[None], U1[None], L[None])
     c.set_path(path)
+    c.set_schedule(SCHED, args.rows)
     c.fill_random([N, N, N], 0x5EED)
     return c
 
 
-outs = {}
-for name, path in (("fused", gcmx.PATH_FUSED), ("generic", gcmx.PATH_GENERIC)):
-    c = make(64, path, x0=128)
-    for _ in range(2):
-        c.step(0.9)
-    outs[name] = c.download()
-    c.close()
-bad = int(np.sum(outs["fused"] != outs["generic"]))
-print(json.dumps({"check": "slab 64x512x512 fused vs generic, 2 steps", "mismatches": bad,
-                  "slab_schedule": os.environ.get("GCMX_SLAB_SCHEDULE", "0")}), flush=True)
-if bad:
-    sys.exit(1)
+if not args.no_check:
+    outs = {}
+    for name, path in (("fused", gcmx.PATH_FUSED), ("generic", gcmx.PATH_GENERIC)):
+        c = make(64, path, x0=128)
+        for _ in range(2):
+            c.step(0.9)
+        outs[name] = c.download()
+        c.close()
+    bad = int(np.sum(outs["fused"] != outs["generic"]))
+    print(json.dumps({"check": "slab 64x512x512 fused vs generic, 2 steps", "mismatches": bad,
+                      "sched": args.sched, "rows": args.rows}), flush=True)
+    if bad:
+        sys.exit(1)
 
-for ranks in (1, 2, 4, 8):
+for ranks in [int(r) for r in args.ranks.split(",")]:
     X = N // ranks
     c = make(X)
     for _ in range(3):
@@ -72,5 +86,4 @@ for ranks in (1, 2, 4, 8):
                       "projected_job_rate_no_comm": round(rate * ranks, 1),
                       "kernels": {n: round(v["total_ms"] / max(1, v["launches"]), 4)
                                   for n, v in k.items()},
-                      "slab_schedule": os.environ.get("GCMX_SLAB_SCHEDULE", "0"),
-                      "rows": os.environ.get("GCMX_XYZ_ROWS", "auto")}), flush=True)
+                      "sched": args.sched, "rows": args.rows}), flush=True)
