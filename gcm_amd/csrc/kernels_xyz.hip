@@ -234,8 +234,20 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #ifndef GCMX_TX2_MINWAVES
 #define GCMX_TX2_MINWAVES 2
 #endif
-#ifndef GCMX_TX2_ZS2  // split the ahead-loads around the two nodes' Z stage + stores
-#define GCMX_TX2_ZS2 1
+#ifndef GCMX_TX2_ZS2  // split the ahead-loads around the two nodes' Z stage + stores (-1: unless NB)
+#define GCMX_TX2_ZS2 -1
+#endif
+#ifndef GCMX_TX2_LA  // tuning: where the ahead-loads of the next X stage are issued (0: after barrier 2)
+#define GCMX_TX2_LA 0
+#endif
+#ifndef GCMX_TX2_NB  // UNI launches: Z exchange without block barriers (per-wave regions + edge ring)
+#define GCMX_TX2_NB 1
+#endif
+#ifndef GCMX_TX2_SLEEP  // NB: s_sleep argument while a neighbour wave's edges are not there yet
+#define GCMX_TX2_SLEEP 1
+#endif
+#ifndef GCMX_TX2_XALL  // every X-stage load issued ahead (with the ahead pairs)
+#define GCMX_TX2_XALL 0
 #endif
 #ifndef GCMX_TX2_DIAG  // tuning builds only: per-wave phase cycle counters (s_memtime)
 #define GCMX_TX2_DIAG 0
@@ -326,7 +338,19 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	constexpr int WX = W + 1;  // planes x-BS .. x+1+BS
 	constexpr int LW = ZT + 2 * BS;
 	static_assert(NCX >= 1 && NCY >= 1, "isotropic structure");
-	__shared__ double zl[2][NWZ][LW];          // Y results of both nodes (Z stage input)
+	// NB: Z == ZT, a multiple of 64.  Each wave keeps its own Y results in a region
+	// of 64 + 2 BS slots; only the BS edge values per side cross to the neighbour
+	// waves, through a two-row ring `eg` and a per-wave row counter `rdy` (no block
+	// barrier: the waves of a block drift apart and overlap their memory phases).
+	constexpr bool NB = UNI && GCMX_TX2_NB;
+	constexpr int NW = ZT / 64;
+	constexpr int RW = 64 + 2 * BS;
+	static_assert(!NB || ZT % 64 == 0, "NB needs whole waves");
+	constexpr bool ZS2 = GCMX_TX2_ZS2 < 0 ? !NB : GCMX_TX2_ZS2 != 0;
+	__shared__ double zl[NB ? 1 : 2][NB ? 1 : NWZ][NB ? 1 : LW];  // Y results of both nodes (Z stage input)
+	__shared__ double rg[NB ? NW : 1][NB ? 2 : 1][NB ? NWZ : 1][NB ? RW : 1];
+	__shared__ double eg[NB ? 2 : 1][NB ? NW : 1][2][NB ? 2 : 1][NB ? NWZ : 1][BS];  // [row&1][wave][side][node][comp][k]
+	__shared__ int rdy[NB ? NW : 1];                                               // last row whose edges are in eg
 	__shared__ double cl[BS + 1][2][NCY][ZT];  // node-only Y components, rows y..y+BS (ring)
 
 	const int z = threadIdx.x;
@@ -356,7 +380,18 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// ghost value of component j on face f: -inner + 2 f(t) if overridden, else the mirror
 	auto ghost = [&](int f, int j, double v) { return ((fb.mask[f] >> j) & 1u) ? -v + fb.two_v[f][j] : v; };
 
-	if (z < 2 * BS) {
+	const int wv = z >> 6, ln = z & 63;  // wave in block, lane
+	if constexpr (NB) {  // zero halos (z ghosts stay zero without a z face); counters
+		if (ln < BS || ln >= 64 - BS) {
+			const int hs = ln < BS ? ln : ln + 2 * BS;
+#pragma unroll
+			for (int t = 0; t < 2; t++)
+#pragma unroll
+				for (int q = 0; q < NWZ; q++) rg[wv][t][q][hs] = 0.0;
+		}
+		if (z < NW) rdy[z] = yb - 1;
+		__syncthreads();
+	} else if (z < 2 * BS) {
 		const int gslot = (z < BS) ? z : (Z + z);
 #pragma unroll
 		for (int t = 0; t < 2; t++)
@@ -435,23 +470,37 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// X-stage inputs issued ahead of the X stage: load pairs 0 and 1.
 	struct XPre {
 		PairWin a, b;
+		PairWin c;         // GCMX_TX2_XALL only
+		double cv[2][9];   // GCMX_TX2_XALL only (node-only components)
 	};
-	auto x_load_ahead = [&](XPre& pre, int r) {
-		pair_load(P0{}, pre.a, base + (unsigned)r * sty);
-		pair_load(P1{}, pre.b, base + (unsigned)r * sty);
-	};
-	// X stage of row r for both nodes: pair 2 and the node-only components are
-	// issued first, then the pairs are consumed in order.
-	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9]) {
-		const unsigned o = base + (unsigned)r * sty;
-		double rr[2][9], n0[2][9], cv[2][9];
-		PairWin wc;
-		pair_load(P2{}, wc, o);
+	auto cv_load = [&](double (&cv)[2][9], unsigned o) {
 #pragma unroll
 		for (int t = 0; t < 2; t++)
 #pragma unroll
 			for (int j = 0; j < 9; j++)
 				if ((CMX >> j) & 1u) cv[t][j] = src.ld(j, o + (unsigned)t * stx);
+	};
+	auto x_load_ahead = [&](XPre& pre, int r) {
+		pair_load(P0{}, pre.a, base + (unsigned)r * sty);
+		pair_load(P1{}, pre.b, base + (unsigned)r * sty);
+		if constexpr (GCMX_TX2_XALL) {
+			pair_load(P2{}, pre.c, base + (unsigned)r * sty);
+			cv_load(pre.cv, base + (unsigned)r * sty);
+		}
+	};
+	// X stage of row r for both nodes: pair 2 and the node-only components are
+	// issued first, then the pairs are consumed in order.
+	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9]) {
+		const unsigned o = base + (unsigned)r * sty;
+		double rr[2][9], n0[2][9];
+		PairWin wc_;
+		double cv_[2][9];
+		if constexpr (!GCMX_TX2_XALL) {
+			pair_load(P2{}, wc_, o);
+			cv_load(cv_, o);
+		}
+		const PairWin& wc = GCMX_TX2_XALL ? pre.c : wc_;
+		const double(&cv)[2][9] = GCMX_TX2_XALL ? pre.cv : cv_;
 		sched_fence();
 		pair_rows(P0{}, pre.a, rr);
 		pair_rows(P1{}, pre.b, rr);
@@ -540,37 +589,81 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	auto row = [&](int y) {
 		double yv[2][9];
 		const int ring = (y + BS) % (BS + 1);
+		XPre pre;
+		const int rn = clamp_row(y + BS + 1);
+		// GCMX_TX2_LA 1: pair 0 at the row start; 2: pair 0 at the row start and pair 1
+		// between the barriers; 3: both at the row start; 4: pair 0 after the Y stage
+		if constexpr (GCMX_TX2_LA == 1 || GCMX_TX2_LA == 2 || GCMX_TX2_LA == 3) {
+			sched_fence();
+			pair_load(P0{}, pre.a, base + (unsigned)rn * sty);
+			if constexpr (GCMX_TX2_LA == 3) pair_load(P1{}, pre.b, base + (unsigned)rn * sty);
+			sched_fence();
+		}
 #pragma unroll
 		for (int t = 0; t < 2; t++)
 			node_update<1, BS, KF0>(
 			    AY, [&](int j, int o) { return win[t][wslot(WMY, j)][BS + o]; },
 			    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cl[ring][t][wslot(CMY, j)][z]; },
 			    yv[t]);
+		if constexpr (GCMX_TX2_LA == 4) {
+			sched_fence();
+			pair_load(P0{}, pre.a, base + (unsigned)rn * sty);
+			sched_fence();
+		}
 		TX2_T(0);
-		__syncthreads();  // every wave has finished reading zl (previous row's Z stage)
-		TX2_T(1);
+		const int es = y & 1;  // NB: edge ring slot of this row
+		if constexpr (NB) {
+			TX2_T(1);
+			asm volatile("" ::: "memory");  // after the previous row's Z-stage reads of rg
 #pragma unroll
-		for (int t = 0; t < 2; t++)
+			for (int t = 0; t < 2; t++)
 #pragma unroll
-			for (int j = 0; j < 9; j++)
-				if ((WMZ >> j) & 1u) {
-					const int q = wslot(WMZ, j);
-					if constexpr (FACES) {
-						// idle lanes leave the z ghost slots to the face (or their zero)
-						if (UNI || z < Z || z >= Z + BS) zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
-						if ((fb.on & 4u) && z >= 1 && z <= BS) zl[t][q][BS - z] = ghost(2, j, yv[t][j]);
-						if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
-							zl[t][q][BS + 2 * (Z - 1) - z] = ghost(3, j, yv[t][j]);
-					} else {
-						zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
+				for (int j = 0; j < 9; j++)
+					if ((WMZ >> j) & 1u) {
+						const int q = wslot(WMZ, j);
+						rg[wv][t][q][BS + ln] = yv[t][j];
+						if constexpr (FACES) {  // z ghosts: wave 0's left halo, the last wave's right halo
+							if ((fb.on & 4u) && z >= 1 && z <= BS) rg[0][t][q][BS - z] = ghost(2, j, yv[t][j]);
+							if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
+								rg[NW - 1][t][q][BS + 2 * (Z - 1) - z - 64 * (NW - 1)] = ghost(3, j, yv[t][j]);
+						}
+						if (ln < BS) eg[es][wv][0][t][q][ln] = yv[t][j];
+						if (ln >= 64 - BS) eg[es][wv][1][t][q][ln - (64 - BS)] = yv[t][j];
 					}
-				}
-		__syncthreads();
-		TX2_T(2);
-		XPre pre;
+			// edges in LDS before the counter says so (LDS only: global memory keeps flowing)
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			__hip_atomic_store(&rdy[wv], y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			TX2_T(2);
+		} else {
+			__syncthreads();  // every wave has finished reading zl (previous row's Z stage)
+			TX2_T(1);
+			if constexpr (GCMX_TX2_LA == 2) {
+				sched_fence();
+				pair_load(P1{}, pre.b, base + (unsigned)rn * sty);
+				sched_fence();
+			}
+#pragma unroll
+			for (int t = 0; t < 2; t++)
+#pragma unroll
+				for (int j = 0; j < 9; j++)
+					if ((WMZ >> j) & 1u) {
+						const int q = wslot(WMZ, j);
+						if constexpr (FACES) {
+							// idle lanes leave the z ghost slots to the face (or their zero)
+							if (UNI || z < Z || z >= Z + BS) zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
+							if ((fb.on & 4u) && z >= 1 && z <= BS) zl[t][q][BS - z] = ghost(2, j, yv[t][j]);
+							if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
+								zl[t][q][BS + 2 * (Z - 1) - z] = ghost(3, j, yv[t][j]);
+						} else {
+							zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
+						}
+					}
+			__syncthreads();
+			TX2_T(2);
+		}
 		const unsigned offo = plane + (unsigned)y * sty + zo;
-		const int rn = clamp_row(y + BS + 1);
-		if constexpr (GCMX_TX2_ZS2) {
+		if constexpr (GCMX_TX2_LA != 0) {
+		} else if constexpr (ZS2) {
 			sched_fence();
 			pair_load(P0{}, pre.a, base + (unsigned)rn * sty);
 			sched_fence();
@@ -579,10 +672,36 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			x_load_ahead(pre, rn);
 			sched_fence();
 		}
+		TX2_T(6);
+		if constexpr (NB) {
+			if constexpr (NW > 1) {  // neighbours' edges of this row -> own halo slots
+				for (;;) {
+					const int a = wv > 0 ? __hip_atomic_load(&rdy[wv - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
+					const int b =
+					    wv < NW - 1 ? __hip_atomic_load(&rdy[wv + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
+					if (__builtin_amdgcn_readfirstlane(min(a, b)) >= y) break;
+					if constexpr (GCMX_TX2_SLEEP > 0) __builtin_amdgcn_s_sleep(GCMX_TX2_SLEEP);
+				}
+				asm volatile("" ::: "memory");
+				if (ln < BS && wv > 0) {
+#pragma unroll
+					for (int t = 0; t < 2; t++)
+#pragma unroll
+						for (int q = 0; q < NWZ; q++) rg[wv][t][q][ln] = eg[es][wv - 1][1][t][q][ln];
+				}
+				if (ln >= 64 - BS && wv < NW - 1) {
+#pragma unroll
+					for (int t = 0; t < 2; t++)
+#pragma unroll
+						for (int q = 0; q < NWZ; q++) rg[wv][t][q][ln + 2 * BS] = eg[es][wv + 1][0][t][q][ln - (64 - BS)];
+				}
+			}
+			asm volatile("" ::: "memory");
+		}
 		TX2_T(4);
 #pragma unroll
 		for (int t = 0; t < 2; t++) {  // each node's stores right after its Z stage
-			if constexpr (GCMX_TX2_ZS2) {
+			if constexpr (ZS2 && GCMX_TX2_LA != 2 && GCMX_TX2_LA != 3) {
 				if (t == 1) {
 					sched_fence();
 					pair_load(P1{}, pre.b, base + (unsigned)rn * sty);
@@ -590,9 +709,14 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				}
 			}
 			double zv[9];
-			node_update<2, BS, KF0>(
-			    AZ, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
-			    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
+			if constexpr (NB)
+				node_update<2, BS, KF0>(
+				    AZ, [&](int j, int o) { return rg[wv][t][wslot(WMZ, j)][BS + ln + o]; },
+				    [&](int j) { return ((WMZ >> j) & 1u) ? rg[wv][t][wslot(WMZ, j)][BS + ln] : yv[t][j]; }, zv);
+			else
+				node_update<2, BS, KF0>(
+				    AZ, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
+				    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
 			if (t == 0 || two) {
 #pragma unroll
 				for (int c = 0; c < 9; c++) out_p.st_nt(c, offo + (unsigned)t * stx, live ? zv[c] : 0.0);
@@ -658,7 +782,11 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 	if constexpr (BS <= 2 && ZT <= 512) {
 		if (GCMX_XYZ_TX2 || fb) {
 			const int npair = (x1 - x0 + 1) / 2;
-			const int chunk = xyz_chunk_for(g.sizes[1], npair, req_chunk);
+			// one block per CU: 256-row blocks while that still gives two rounds of blocks
+			const int Y = g.sizes[1];
+			const int chunk = (req_chunk <= 0 && Y > 256 && (long long)((Y + 255) / 256) * npair >= 512)
+			                      ? 256
+			                      : xyz_chunk_for(Y, npair, req_chunk);
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair);
 			const FaceBC none{};
 			const FaceBC& f = fb ? *fb : none;

@@ -27,10 +27,13 @@ for _ in range(steps):
 c.sync()
 assert lib.gcmx_diag_tx2(buf) == 0
 a = np.array(buf[:], dtype=np.float64).reshape(16, 8)
-names = ["Y stage", "barrier 1", "zl write+barrier 2", "Z stages+stores", "ahead-load issue", "X stage", "-", "-"]
+# barrier kernel (GCMX_TX2_NB=0): 1 = barrier 1, 2 = zl writes + barrier 2, 4 = ahead loads;
+# NB kernel: 2 = region/edge writes + counter, 6 = ahead loads, 4 = neighbour wait + halo copy
+names = ["Y stage", "barrier 1", "zl/rg writes (+barrier 2)", "Z stages+stores", "wait+halo (NB) / ahead loads",
+         "X stage", "ahead loads (NB)", "-"]
 tot = a.sum(axis=1)
 print("per wave-in-block: share of cycles by phase")
 for w in range(8):
-    print(f"wave {w}: " + "  ".join(f"{names[i]} {a[w, i] / tot[w]:.3f}" for i in range(6)))
+    print(f"wave {w}: " + "  ".join(f"{names[i]} {a[w, i] / tot[w]:.3f}" for i in range(7)))
 blocks = (N // 128) * (N // 2)
 print(f"mean cycles per wave per row: {tot[:8].mean() / (blocks * 128 * steps):.0f}")

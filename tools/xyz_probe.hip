@@ -89,10 +89,13 @@ __global__ __launch_bounds__(512 / VEC * PL) void k_probe(const double* __restri
 }
 
 // Each thread: TX adjacent planes at one z; 6 components at TX+4 planes, 3 at the TX nodes.
-template <int TX, bool STORE, int KOPS = 0>
+// BAR: the fused kernel's Z exchange per row -- two barriers around 12 LDS row
+// writes (6 components x 2 nodes), then 4 neighbour reads per component.
+template <int TX, bool STORE, int KOPS = 0, bool BAR = false>
 __global__ __launch_bounds__(512, 2) void k_probe_tx(const double* __restrict__ in,
                                                      double* __restrict__ out, int chunk) {
 	extern __shared__ double dyn_lds[];
+	__shared__ double zl[BAR ? TX : 1][6][BAR ? 516 : 1];
 	const int z = threadIdx.x;
 	if (z == 1023) dyn_lds[0] = 0.0;  // never true: keeps the dynamic LDS request
 	const int T_ = gridDim.x, b = blockIdx.x;
@@ -125,6 +128,19 @@ __global__ __launch_bounds__(512, 2) void k_probe_tx(const double* __restrict__ 
 #pragma unroll
 					for (int c = 0; c < 9; c++) v[t][c] = v[t][c] * 0.999 + 0.001;
 		}
+		if constexpr (BAR) {
+			__syncthreads();
+#pragma unroll
+			for (int t = 0; t < TX; t++)
+#pragma unroll
+				for (int c = 0; c < 6; c++) zl[t][c][2 + z] = v[t][c];
+			__syncthreads();
+#pragma unroll
+			for (int t = 0; t < TX; t++)
+#pragma unroll
+				for (int c = 0; c < 6; c++)
+					v[t][c] += (zl[t][c][z] + zl[t][c][z + 1]) + (zl[t][c][z + 3] + zl[t][c][z + 4]);
+		}
 #pragma unroll
 		for (int t = 0; t < TX; t++)
 #pragma unroll
@@ -136,7 +152,7 @@ __global__ __launch_bounds__(512, 2) void k_probe_tx(const double* __restrict__ 
 	if (!STORE && acc == 1234.5) out[0] = acc;
 }
 
-template <int TX, int KOPS>
+template <int TX, int KOPS, bool BAR = false>
 void ops_tx(const double* in, double* out, int chunk, size_t shm = 0) {
 	const double nodes = (double)N * N * N;
 	dim3 grid((N / chunk) * (N / TX));
@@ -145,15 +161,16 @@ void ops_tx(const double* in, double* out, int chunk, size_t shm = 0) {
 	CK(hipEventCreate(&b));
 	for (int r = 0; r < 11; r++) {
 		if (r == 1) CK(hipEventRecord(a));
-		hipLaunchKernelGGL((k_probe_tx<TX, true, KOPS>), grid, dim3(512), shm, 0, in, out, chunk);
+		hipLaunchKernelGGL((k_probe_tx<TX, true, KOPS, BAR>), grid, dim3(512), shm, 0, in, out, chunk);
 	}
 	CK(hipEventRecord(b));
 	CK(hipEventSynchronize(b));
 	float ms = 0;
 	CK(hipEventElapsedTime(&ms, a, b));
 	ms /= 10;
-	std::printf("TX %d planes/thread chunk %3d + %d fp64 ops/node%s: %.3f ms (%.0f GB/s)\n", TX, chunk, KOPS,
-	            shm ? " (1 block/CU)" : "", ms, 144.0 * nodes / (ms * 1e6));
+	std::printf("TX %d planes/thread chunk %3d + %d fp64 ops/node%s%s: %.3f ms (%.0f GB/s)\n", TX, chunk, KOPS,
+	            BAR ? " + Z exchange (2 barriers/row)" : "", shm ? " (1 block/CU)" : "", ms,
+	            144.0 * nodes / (ms * 1e6));
 }
 
 template <int TX>
@@ -218,6 +235,8 @@ int main() {
 	CK(hipMemset(in, 0, bytes));
 	CK(hipMemset(out, 0, bytes));
 	family<1, 1>(in, out, 128);
+	family<2, 1>(in, out, 128);
+	family<2, 2>(in, out, 128);
 	family_tx<1>(in, out, 128);
 	family_tx<2>(in, out, 128);
 	family_tx<4>(in, out, 128);
@@ -225,6 +244,10 @@ int main() {
 	ops_tx<2, 360>(in, out, 128);
 	ops_tx<2, 540>(in, out, 128);
 	ops_tx<2, 720>(in, out, 128);
+	ops_tx<2, 540, true>(in, out, 128);
+	ops_tx<2, 0, true>(in, out, 128, 96 * 1024);
+	ops_tx<2, 540, true>(in, out, 128, 96 * 1024);
+	ops_tx<2, 720, true>(in, out, 128, 96 * 1024);
 	ops_tx<2, 0>(in, out, 128, 96 * 1024);
 	ops_tx<2, 360>(in, out, 128, 96 * 1024);
 	ops_tx<2, 540>(in, out, 128, 96 * 1024);
