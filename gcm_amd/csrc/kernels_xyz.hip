@@ -761,15 +761,15 @@ static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
 	return std::memcmp(&p, &q, sizeof(IsoAxis)) == 0;
 }
 
-// Rows per block: GCMX_XYZ_CHUNK (128) while the launch still has >= 1024 blocks
+// Rows per block (k_fused_xyz): GCMX_XYZ_CHUNK (128) while the launch still has >= 1024 blocks
 // (two rounds of the 512 resident blocks, 2 per CU); thinner slabs (multi-GPU
 // X slabs, the boundary planes) halve it, down to 16 rows, to keep every CU
 // busy.  Each block recomputes 2*BS X rows in its prologue, so a chunk of c
 // rows costs (c + 2*BS) / c of the X stage.  `req` > 0 forces a value.
-static int xyz_chunk_for(int Y, int nplanes, int req) {
-	int chunk = req > 0 ? req : GCMX_XYZ_CHUNK;
+static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK, int min_blocks = 1024) {
+	int chunk = req > 0 ? req : start;
 	if (req <= 0)
-		while (chunk > 16 && (long long)((Y + chunk - 1) / chunk) * nplanes < 1024) chunk /= 2;
+		while (chunk > 16 && (long long)((Y + chunk - 1) / chunk) * nplanes < min_blocks) chunk /= 2;
 	return Y <= chunk ? Y : chunk;
 }
 
@@ -782,11 +782,9 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 	if constexpr (BS <= 2 && ZT <= 512) {
 		if (GCMX_XYZ_TX2 || fb) {
 			const int npair = (x1 - x0 + 1) / 2;
-			// one block per CU: 256-row blocks while that still gives two rounds of blocks
-			const int Y = g.sizes[1];
-			const int chunk = (req_chunk <= 0 && Y > 256 && (long long)((Y + 255) / 256) * npair >= 512)
-			                      ? 256
-			                      : xyz_chunk_for(Y, npair, req_chunk);
+			// one block per CU: the longest blocks (<= 256 rows) that still give two
+			// rounds of the 256 resident blocks (512^3: 256 rows, 256^3: 64)
+			const int chunk = xyz_chunk_for(g.sizes[1], npair, req_chunk, 256, 512);
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair);
 			const FaceBC none{};
 			const FaceBC& f = fb ? *fb : none;
