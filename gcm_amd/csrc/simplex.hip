@@ -56,6 +56,7 @@ struct BorderDev {
 	signed char* outer = nullptr;
 	BorderArgs args{};
 	bool set = false, valuesSet = false;
+	double lastValues[3 * GSX_MAX_BORDER_CONDITIONS] = {};  // what bvals holds once valuesSet
 };
 
 struct StageShift {  // crossingPoints' shift of every invariant: direction * (-tau L(k))
@@ -87,13 +88,14 @@ struct gsx_ctx {
 	       *grad = nullptr;
 	double* mats = nullptr;  // [2][3][81]: U then U1
 	bool matsSet = false;
+	int nodeLanes = 0;  // gsx_set_node_lanes: 0 auto, 1, 8
 	int *gOff = nullptr, *gNb = nullptr;
 	double *gRows = nullptr, *gW = nullptr, *gM = nullptr, *gDet = nullptr;
 	bool gradSet = false;
 	StageDev st[3];
 	BorderDev bd;
 	double* wnext = nullptr;             // next stage's invariants, node-major [n][9]
-	bool chained = false;                // w already holds this stage's invariants
+	int wStage = -1;                     // w already holds the invariants of this stage (-1: none)
 	int* corrOf = nullptr;               // node -> border-plan entry or -1
 	char* deferred = nullptr;            // node in a contact: the contact kernel finalizes it
 	std::vector<char> hostDeferred;
@@ -104,18 +106,18 @@ struct gsx_ctx {
 // The host-side state a simplex step changes (pointer swaps, chaining flag).
 struct BodyState {
 	double *u, *un, *w, *wnext;
-	bool chained;
+	int wStage;
 	bool operator==(const BodyState& o) const {
-		return u == o.u && un == o.un && w == o.w && wnext == o.wnext && chained == o.chained;
+		return u == o.u && un == o.un && w == o.w && wnext == o.wnext && wStage == o.wStage;
 	}
 };
-static BodyState body_state(const gsx_ctx* c) { return {c->u, c->un, c->w, c->wnext, c->chained}; }
+static BodyState body_state(const gsx_ctx* c) { return {c->u, c->un, c->w, c->wnext, c->wStage}; }
 static void set_body_state(gsx_ctx* c, const BodyState& b) {
 	c->u = b.u;
 	c->un = b.un;
 	c->w = b.w;
 	c->wnext = b.wnext;
-	c->chained = b.chained;
+	c->wStage = b.wStage;
 }
 
 // One captured step per entry state: a step swaps u/un, so two graphs alternate.
@@ -207,22 +209,44 @@ __global__ __launch_bounds__(256) void k_sx_gradient(const double* __restrict__ 
 	for (int c = 0; c < kG; c++) wc[c] = w[(size_t)n * kM + c];
 	const double x0 = coords[3 * (size_t)n], x1 = coords[3 * (size_t)n + 1],
 	             x2 = coords[3 * (size_t)n + 2];
-	for (int i = 0; i < K; i++) {
-		const int e = b0 + i;
-		const int nb = nbs[e];
-		const double* wn = w + (size_t)nb * kM;
-		const double a0 = coords[3 * (size_t)nb] - x0, a1 = coords[3 * (size_t)nb + 1] - x1,
-		             a2 = coords[3 * (size_t)nb + 2] - x2;
-		const double we = wts[e];
+	// Latency layout: all neighbour indices in one round trip, then the
+	// neighbours' records in batches of kGB (their loads issued together); the
+	// sums still run in neighbour order.
+	constexpr int kGB = 5;
+	int nbv[kMaxNb];
 #pragma unroll
-		for (int c = 0; c < kG; c++) {
-			const double bi = wn[c] - wc[c];  // b(i) = pde(neighbor) - pde(it)
-			const double wb = we * bi;        // (W * b)(i)
-			const double t0 = a0 * wb, t1 = a1 * wb, t2 = a2 * wb;
-			if (i == 0) {
-				r0[c] = t0; r1[c] = t1; r2[c] = t2;
-			} else {
-				r0[c] += t0; r1[c] += t1; r2[c] += t2;
+	for (int i = 0; i < kMaxNb; i++) nbv[i] = i < K ? nbs[b0 + i] : n;
+#pragma unroll
+	for (int i0 = 0; i0 < kMaxNb; i0 += kGB) {
+		if (i0 >= K) break;
+		double wb_[kGB][kG], a_[kGB][3], we_[kGB];
+#pragma unroll
+		for (int j = 0; j < kGB; j++) {
+			const int nb = nbv[i0 + j];
+			const double* wn = w + (size_t)nb * kM;
+#pragma unroll
+			for (int c = 0; c < kG; c++) wb_[j][c] = wn[c];
+#pragma unroll
+			for (int r = 0; r < 3; r++) a_[j][r] = coords[3 * (size_t)nb + r];
+			we_[j] = i0 + j < K ? wts[b0 + i0 + j] : 0.0;
+		}
+#pragma unroll
+		for (int j = 0; j < kGB; j++) {
+			const int i = i0 + j;
+			if (i < K) {
+				const double a0 = a_[j][0] - x0, a1 = a_[j][1] - x1, a2 = a_[j][2] - x2;
+				const double we = we_[j];
+#pragma unroll
+				for (int c = 0; c < kG; c++) {
+					const double bi = wb_[j][c] - wc[c];  // b(i) = pde(neighbor) - pde(it)
+					const double wb = we * bi;            // (W * b)(i)
+					const double t0 = a0 * wb, t1 = a1 * wb, t2 = a2 * wb;
+					if (i == 0) {
+						r0[c] = t0; r1[c] = t1; r2[c] = t2;
+					} else {
+						r0[c] += t0; r1[c] += t1; r2[c] += t2;
+					}
+				}
 			}
 		}
 	}
@@ -250,6 +274,11 @@ __device__ __forceinline__ double std_min(double a, double b) { return (b < a) ?
 __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
 
 // interpolateValuesAround (hpp:156-198) for the listed nodes, feet resolved on the host.
+// Latency layout: the six feet's records are read first, then every foot's
+// gathers are issued without branches (all foot vertex indices are valid nodes,
+// gsx_set_stage_plan checks them; a foot that needs no gradient still reads one
+// it ignores), so one node costs three dependent memory round trips, not three
+// per foot.  The arithmetic of the selected kind is unchanged.
 __device__ __forceinline__ void node_invariants(int n, const int4* __restrict__ fv,
                                                 const double4* __restrict__ flam,
                                                 const int* __restrict__ fmeta, const StageShift& sh,
@@ -260,60 +289,60 @@ __device__ __forceinline__ void node_invariants(int n, const int4* __restrict__ 
                                                 double (&out)[kM]) {
 	const double x0 = coords[3 * (size_t)n + 0], x1 = coords[3 * (size_t)n + 1],
 	             x2 = coords[3 * (size_t)n + 2];
+	int meta[6];
+	int4 fvv[6];
+	double4 lv[6];
 #pragma unroll
-	for (int k = 0; k < kM; k++) {
+	for (int k = 0; k < 6; k++) {
+		const size_t e = (size_t)k * N + n;
+		meta[k] = fmeta[e];
+		fvv[k] = fv[e];
+		lv[k] = flam[e];
+	}
+#pragma unroll
+	for (int k = 6; k < kM; k++) out[k] = w[(size_t)n * kM + k];  // dx(k) == 0: exact hit (hpp:166-170)
+#pragma unroll
+	for (int k = 0; k < 6; k++) {
+		const int kind = meta[k] & 15;
+		const int vs[4] = {fvv[k].x, fvv[k].y, fvv[k].z, fvv[k].w};
+		const double lam[4] = {lv[k].x, lv[k].y, lv[k].z, lv[k].w};
+		double v[4], term[4];
+		const double q0 = x0 + sh.d[k][0], q1 = x1 + sh.d[k][1], q2 = x2 + sh.d[k][2];
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const int p = vs[i];
+			// SPACETIME: value i is slot s of the face's current (s < 3) or new (s >= 3) invariants
+			const int sl = (meta[k] >> (4 + 4 * i)) & 15;
+			const int r = sl < 3 ? sl : sl - 3;
+			const int ps = r == 0 ? vs[0] : (r == 1 ? vs[1] : vs[2]);
+			const double* src = (kind == GSX_FOOT_CELL) ? w + (size_t)p * kM + k
+			                    : (sl < 3)              ? w + (size_t)ps * kM + k
+			                                            : wn + (size_t)k * N + ps;
+			v[i] = *src;
+			// TetrahedronInterpolator::hybridInterpolate (hpp:93-104) terms
+			const double d0 = q0 - coords[3 * (size_t)p + 0];
+			const double d1 = q1 - coords[3 * (size_t)p + 1];
+			const double d2 = q2 - coords[3 * (size_t)p + 2];
+			const double* gp = grad + (size_t)p * 3 * kG;
+			double dot = gp[0 * kG + k] * d0;
+			dot += gp[1 * kG + k] * d1;
+			dot += gp[2 * kG + k] * d2;
+			term[i] = v[i] + dot / 2.0;
+		}
 		double ans;
-		if (k >= 6) {
-			ans = w[(size_t)n * kM + k];  // dx(k) == 0: exact hit (hpp:166-170)
+		if (kind == GSX_FOOT_CELL) {
+			const double quadratic =
+			    lam[0] * term[0] + lam[1] * term[1] + lam[2] * term[2] + lam[3] * term[3];
+			const double mn = std_min(std_min(std_min(v[0], v[1]), v[2]), v[3]);
+			const double mx = std_max(std_max(std_max(v[0], v[1]), v[2]), v[3]);
+			const double limited = std_min(std_max(quadratic, mn), mx);
+			ans = (quadratic == limited) ? quadratic
+			                             : lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
+		} else if (kind == GSX_FOOT_SPACETIME) {
+			// the face's border nodes: current invariants w, new invariants wn
+			ans = lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
 		} else {
-			const size_t e = (size_t)k * N + n;
-			const int meta = fmeta[e];
-			const int kind = meta & 15;
-			if (kind == GSX_FOOT_CELL) {
-				// TetrahedronInterpolator::hybridInterpolate (hpp:93-104)
-				const int4 fvv = fv[e];
-				const double4 l = flam[e];
-				const int vs[4] = {fvv.x, fvv.y, fvv.z, fvv.w};
-				const double lam[4] = {l.x, l.y, l.z, l.w};
-				const double q0 = x0 + sh.d[k][0], q1 = x1 + sh.d[k][1], q2 = x2 + sh.d[k][2];
-				double v[4], term[4];
-#pragma unroll
-				for (int i = 0; i < 4; i++) {
-					const int p = vs[i];
-					v[i] = w[(size_t)p * kM + k];
-					const double d0 = q0 - coords[3 * (size_t)p + 0];
-					const double d1 = q1 - coords[3 * (size_t)p + 1];
-					const double d2 = q2 - coords[3 * (size_t)p + 2];
-					const double* gp = grad + (size_t)p * 3 * kG;
-					double dot = gp[0 * kG + k] * d0;
-					dot += gp[1 * kG + k] * d1;
-					dot += gp[2 * kG + k] * d2;
-					term[i] = v[i] + dot / 2.0;
-				}
-				const double quadratic =
-				    lam[0] * term[0] + lam[1] * term[1] + lam[2] * term[2] + lam[3] * term[3];
-				const double mn = std_min(std_min(std_min(v[0], v[1]), v[2]), v[3]);
-				const double mx = std_max(std_max(std_max(v[0], v[1]), v[2]), v[3]);
-				const double limited = std_min(std_max(quadratic, mn), mx);
-				ans = (quadratic == limited)
-				          ? quadratic
-				          : lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
-			} else if (kind == GSX_FOOT_SPACETIME) {
-				// the face's border nodes: current invariants w, new invariants wn
-				const int4 fvv = fv[e];
-				const double4 l = flam[e];
-				const int vs[3] = {fvv.x, fvv.y, fvv.z};
-				const double lam[4] = {l.x, l.y, l.z, l.w};
-				double val[4];
-#pragma unroll
-				for (int i = 0; i < 4; i++) {
-					const int s = (meta >> (4 + 4 * i)) & 15;
-					val[i] = (s < 3) ? w[(size_t)vs[s] * kM + k] : wn[k * N + vs[s - 3]];
-				}
-				ans = lam[0] * val[0] + lam[1] * val[1] + lam[2] * val[2] + lam[3] * val[3];
-			} else {
-				ans = 0.0;  // outer invariant / walk ended on a vertex
-			}
+			ans = 0.0;  // outer invariant / walk ended on a vertex
 		}
 		out[k] = ans;
 	}
@@ -375,8 +404,9 @@ __device__ void plain_correction(double (&u)[kM], int type, const double* __rest
 
 // calculateOuterWaveCorrection (common.hpp:186-202) with Omega = the U1 columns
 // `cols` (getColumnsFromGcmMatrices, common.hpp:153-165).
+template <class BT>  // B: a pointer into the plan or the node's 27 values in registers
 __device__ bool outer_wave_correction(const double (&u)[kM], const double* __restrict__ U1,
-                                      const int (&cols)[3], const double* __restrict__ B,
+                                      const int (&cols)[3], const BT& B,
                                       const double (&b)[3], double minValid, double (&value)[kM]) {
 	double M[3][3];
 	for (int i = 0; i < 3; i++)
@@ -486,6 +516,23 @@ struct BorderDevArgs {  // the border plan's device arrays (null cond = no plan)
 // only read the node's own new invariants) and, for every node that is not in a
 // contact, afterStage + the next beforeStage.  wn keeps the corrected invariants
 // of these nodes: inner space-time feet and the contact correctors read them.
+// The corrector kernels read U / U1 / U_next entry by entry in long unrolled
+// sums; as uniform loads they land in SGPRs, which overflow into VGPR lanes (1 200+
+// v_readlane per launch, measured 10 us of a 19 us border launch at 16^3).  Staged
+// once per block in LDS, every entry is a broadcast ds_read instead.
+template <int NMAT>
+struct SharedMats {
+	double m[NMAT][81];
+};
+template <int NMAT>
+__device__ __forceinline__ void stage_mats(SharedMats<NMAT>& sm, const double* const (&src)[NMAT]) {
+	for (int i = threadIdx.x; i < 81; i += blockDim.x)
+#pragma unroll
+		for (int k = 0; k < NMAT; k++)
+			if (src[k]) sm.m[k][i] = src[k][i];
+	__syncthreads();
+}
+
 __global__ __launch_bounds__(64) void k_sx_border(
     const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
     const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
@@ -493,6 +540,8 @@ __global__ __launch_bounds__(64) void k_sx_border(
     double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, BorderArgs args,
     const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int stage, int N) {
+	__shared__ SharedMats<3> sm;
+	stage_mats<3>(sm, {U, U1, Unext});
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int n = nodes[t];
@@ -500,11 +549,12 @@ __global__ __launch_bounds__(64) void k_sx_border(
 	node_invariants(n, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
 	if (bp.cond) {
 		const int ci = bp.corrOf[n];
-		if (ci >= 0) border_correct(out, ci, bp.cond, bp.B, bp.S, bp.outer, bp.count, U, U1, stage, args);
+		if (ci >= 0)
+			border_correct(out, ci, bp.cond, bp.B, bp.S, bp.outer, bp.count, sm.m[0], sm.m[1], stage, args);
 	}
 #pragma unroll
 	for (int k = 0; k < kM; k++) wn[k * N + n] = out[k];
-	if (!deferred[n]) finalize(n, out, U1, Unext, un, wnext, N);
+	if (!deferred[n]) finalize(n, out, sm.m[1], Unext ? sm.m[2] : nullptr, un, wnext, N);
 }
 
 // innerStage (hpp:98-112) + afterStage + the next beforeStage for the inner nodes;
@@ -521,6 +571,288 @@ __global__ __launch_bounds__(256) void k_sx_inner(
 	double out[kM];
 	node_invariants(n, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
 	finalize(n, out, U1, Unext, un, wnext, N);
+}
+
+// ---- latency layout: eight lanes per node (gsx_set_node_lanes) ----------------
+// Small meshes (the reference's 16^3 cube: 4 913 nodes) leave most of the chip
+// idle with one thread per node, and a node's work is a chain of dependent
+// gathers.  Here lane c of a node's group of kL handles component / foot c: the
+// gradient lanes sum their own component's terms (in neighbour order, as the
+// node-per-thread kernel), the foot lanes interpolate their own invariant, and
+// the 9 results meet through cross-lane shuffles (__shfl within the group); the
+// U1 / U products are split by rows.  Every value is produced by the same
+// operations in the same order as in the node-per-thread kernels.
+constexpr int kL = 8;
+
+__global__ __launch_bounds__(256) void k_sx_gradient_l8(const double* __restrict__ w,
+                                                        double* __restrict__ grad,
+                                                        const int* __restrict__ off,
+                                                        const int* __restrict__ nbs,
+                                                        const double* __restrict__ coords,
+                                                        const double* __restrict__ wts,
+                                                        const double* __restrict__ Mm,
+                                                        const double* __restrict__ dets, int N) {
+	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const int n = gid / kL, c = gid % kL;
+	if (n >= N || c >= kG) return;  // no shuffles in this kernel
+	const int b0 = off[n], K = off[n + 1] - b0;
+	const double wc = w[(size_t)n * kM + c];
+	const double x0 = coords[3 * (size_t)n], x1 = coords[3 * (size_t)n + 1],
+	             x2 = coords[3 * (size_t)n + 2];
+	constexpr int kGB = 10;
+	int nbv[kMaxNb];
+#pragma unroll
+	for (int i = 0; i < kMaxNb; i++) nbv[i] = i < K ? nbs[b0 + i] : n;
+	double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll
+	for (int i0 = 0; i0 < kMaxNb; i0 += kGB) {
+		if (i0 >= K) break;
+		double wb_[kGB], a_[kGB][3], we_[kGB];
+#pragma unroll
+		for (int j = 0; j < kGB; j++) {
+			const int nb = nbv[i0 + j];
+			wb_[j] = w[(size_t)nb * kM + c];
+#pragma unroll
+			for (int r = 0; r < 3; r++) a_[j][r] = coords[3 * (size_t)nb + r];
+			we_[j] = i0 + j < K ? wts[b0 + i0 + j] : 0.0;
+		}
+#pragma unroll
+		for (int j = 0; j < kGB; j++) {
+			const int i = i0 + j;
+			if (i < K) {
+				const double a0 = a_[j][0] - x0, a1 = a_[j][1] - x1, a2 = a_[j][2] - x2;
+				const double bi = wb_[j] - wc;  // b(i) = pde(neighbor) - pde(it)
+				const double wb = we_[j] * bi;  // (W * b)(i)
+				const double t0 = a0 * wb, t1 = a1 * wb, t2 = a2 * wb;
+				if (i == 0) {
+					r0 = t0; r1 = t1; r2 = t2;
+				} else {
+					r0 += t0; r1 += t1; r2 += t2;
+				}
+			}
+		}
+	}
+	const double* M = Mm + 9 * (size_t)n;
+	const double det = dets[n];
+	double y0 = r0, y1 = r1, y2 = r2;
+	if (K < kMaxNb) {  // the zero rows: 0 * (0 * 0) = +0
+		y0 += 0.0; y1 += 0.0; y2 += 0.0;
+	}
+	const double d1 = det3(y0, M[1], M[2], y1, M[4], M[5], y2, M[7], M[8]);
+	const double d2 = det3(M[0], y0, M[2], M[3], y1, M[5], M[6], y2, M[8]);
+	const double d3 = det3(M[0], M[1], y0, M[3], M[4], y1, M[6], M[7], y2);
+	double* g = grad + (size_t)n * 3 * kG;
+	g[0 * kG + c] = d1 / det;
+	g[1 * kG + c] = d2 / det;
+	g[2 * kG + c] = d3 / det;
+}
+
+// interpolateValuesAround for one invariant k (0..5) of node n (node_invariants' body).
+__device__ __forceinline__ double foot_value(int n, int k, const int4* __restrict__ fv,
+                                             const double4* __restrict__ flam,
+                                             const int* __restrict__ fmeta, const StageShift& sh,
+                                             const double* __restrict__ coords,
+                                             const double* __restrict__ w,
+                                             const double* __restrict__ grad,
+                                             const double* __restrict__ wn, int N) {
+	double s0 = sh.d[0][0], s1 = sh.d[0][1], s2 = sh.d[0][2];  // shift of invariant k (selects)
+#pragma unroll
+	for (int kk = 1; kk < 6; kk++)
+		if (k == kk) {
+			s0 = sh.d[kk][0];
+			s1 = sh.d[kk][1];
+			s2 = sh.d[kk][2];
+		}
+	const size_t e = (size_t)k * N + n;
+	const int meta = fmeta[e];
+	const int4 f = fv[e];
+	const double4 l = flam[e];
+	const int kind = meta & 15;
+	const int vs[4] = {f.x, f.y, f.z, f.w};
+	const double lam[4] = {l.x, l.y, l.z, l.w};
+	const double q0 = coords[3 * (size_t)n + 0] + s0, q1 = coords[3 * (size_t)n + 1] + s1,
+	             q2 = coords[3 * (size_t)n + 2] + s2;
+	double v[4], term[4];
+#pragma unroll
+	for (int i = 0; i < 4; i++) {
+		const int p = vs[i];
+		const int sl = (meta >> (4 + 4 * i)) & 15;
+		const int r = sl < 3 ? sl : sl - 3;
+		const int ps = r == 0 ? vs[0] : (r == 1 ? vs[1] : vs[2]);
+		const double* src = (kind == GSX_FOOT_CELL) ? w + (size_t)p * kM + k
+		                    : (sl < 3)              ? w + (size_t)ps * kM + k
+		                                            : wn + (size_t)k * N + ps;
+		v[i] = *src;
+		const double d0 = q0 - coords[3 * (size_t)p + 0];
+		const double d1 = q1 - coords[3 * (size_t)p + 1];
+		const double d2 = q2 - coords[3 * (size_t)p + 2];
+		const double* gp = grad + (size_t)p * 3 * kG;
+		double dot = gp[0 * kG + k] * d0;
+		dot += gp[1 * kG + k] * d1;
+		dot += gp[2 * kG + k] * d2;
+		term[i] = v[i] + dot / 2.0;
+	}
+	if (kind == GSX_FOOT_CELL) {
+		const double quadratic = lam[0] * term[0] + lam[1] * term[1] + lam[2] * term[2] + lam[3] * term[3];
+		const double mn = std_min(std_min(std_min(v[0], v[1]), v[2]), v[3]);
+		const double mx = std_max(std_max(std_max(v[0], v[1]), v[2]), v[3]);
+		const double limited = std_min(std_max(quadratic, mn), mx);
+		return (quadratic == limited) ? quadratic
+		                              : lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
+	}
+	if (kind == GSX_FOOT_SPACETIME) return lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
+	return 0.0;
+}
+
+// All 9 new invariants of node n in every lane of its group (lane c < 6 interpolates
+// invariant c, lanes 6, 7 read the exact hits 6, 7; every lane reads 8).
+__device__ __forceinline__ void group_invariants(int n, int c, const int4* __restrict__ fv,
+                                                 const double4* __restrict__ flam,
+                                                 const int* __restrict__ fmeta, const StageShift& sh,
+                                                 const double* __restrict__ coords,
+                                                 const double* __restrict__ w,
+                                                 const double* __restrict__ grad,
+                                                 const double* __restrict__ wn, int N, double (&o)[kM]) {
+	const double mine = c < 6 ? foot_value(n, c, fv, flam, fmeta, sh, coords, w, grad, wn, N)
+	                          : w[(size_t)n * kM + c];
+	const double w8 = w[(size_t)n * kM + 8];
+#pragma unroll
+	for (int j = 0; j < kL; j++) o[j] = __shfl(mine, j, kL);
+	o[8] = w8;
+}
+
+__device__ __forceinline__ double pick9(const double (&o)[kM], int c) {
+	double r = o[0];
+#pragma unroll
+	for (int j = 1; j < kM; j++)
+		if (c == j) r = o[j];
+	return r;
+}
+
+// Row c (and row 8, in every lane) of Mx * in, in mat_vec's order.
+__device__ __forceinline__ void rows_mat_vec(const double* __restrict__ Mx, const double (&in)[kM], int c,
+                                             double& rc, double& r8) {
+	double s = Mx[c * kM + 0] * in[0];
+#pragma unroll
+	for (int j = 1; j < kM; j++) s += Mx[c * kM + j] * in[j];
+	rc = s;
+	double t = Mx[8 * kM + 0] * in[0];
+#pragma unroll
+	for (int j = 1; j < kM; j++) t += Mx[8 * kM + j] * in[j];
+	r8 = t;
+}
+
+// finalize() split over the group: lane c writes component c, lane 0 also 8.
+__device__ __forceinline__ void group_finalize(int n, int c, bool store, const double (&wv)[kM],
+                                               const double* __restrict__ U1,
+                                               const double* __restrict__ Unext, double* __restrict__ un,
+                                               double* __restrict__ wnext, int N) {
+	double uc, u8;
+	rows_mat_vec(U1, wv, c, uc, u8);
+	if (store) {
+		un[(size_t)c * N + n] = uc;
+		if (c == 0) un[(size_t)8 * N + n] = u8;
+	}
+	if (Unext) {
+		double u[kM];
+#pragma unroll
+		for (int j = 0; j < kL; j++) u[j] = __shfl(uc, j, kL);
+		u[8] = u8;
+		double wc, w8;
+		rows_mat_vec(Unext, u, c, wc, w8);
+		if (store) {
+			wnext[(size_t)n * kM + c] = wc;
+			if (c == 0) wnext[(size_t)n * kM + 8] = w8;
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void k_sx_inner_l8(
+    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
+    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
+    const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
+    double* __restrict__ un, double* __restrict__ wnext, int N) {
+	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const int t = gid / kL, c = gid % kL;
+	// whole groups stay active for the shuffles; a group past the list redoes the last node, unstored
+	const bool store = t < count;
+	const int n = nodes[store ? t : count - 1];
+	double o[kM];
+	group_invariants(n, c, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
+	group_finalize(n, c, store, o, U1, Unext, un, wnext, N);
+}
+
+// border_correct with the node's plan data already in registers (B, condition,
+// outer code) and both one-sided corrections always evaluated, so the lanes of a
+// wave do not serialise over the nodes' codes; the result of each path is the
+// one border_correct computes.
+__device__ void border_correct_pre(double (&w)[kM], int t, int c, int code, const double (&B)[27],
+                                   const double* __restrict__ Sm, const double* __restrict__ U,
+                                   const double* __restrict__ U1, int stage, const BorderArgs& args) {
+	const double b[3] = {args.b[3 * c], args.b[3 * c + 1], args.b[3 * c + 2]};
+	const double minValid = args.minDet[c][stage];
+	double u[kM];
+	mat_vec(U1, w, u);
+	const int R[3] = {1, 3, 5}, L[3] = {0, 2, 4};  // Model.cpp:81-82
+	double vr[kM], vl[kM];
+	const bool okR = outer_wave_correction(u, U1, R, B, b, minValid, vr);
+	const bool okL = outer_wave_correction(u, U1, L, B, b, minValid, vl);
+	if (code == 1 || code == 2) {
+		if (code == 1 ? okR : okL) {
+			for (int k = 0; k < kM; k++) u[k] += code == 1 ? vr[k] : vl[k];
+		} else {
+			plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+		}
+	} else {
+		if (okR && okL) {
+			for (int k = 0; k < kM; k++) u[k] += (vr[k] + vl[k]) / 2;
+		} else {
+			plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+		}
+	}
+	mat_vec(U, u, w);
+}
+
+__global__ __launch_bounds__(256) void k_sx_border_l8(
+    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
+    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
+    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, BorderArgs args,
+    const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
+    double* __restrict__ un, double* __restrict__ wnext, int stage, int N) {
+	__shared__ SharedMats<3> sm;
+	stage_mats<3>(sm, {U, U1, Unext});
+	const double* Us = sm.m[0];
+	const double* U1s = sm.m[1];
+	const double* Uns = Unext ? sm.m[2] : nullptr;
+	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const int t = gid / kL, c = gid % kL;
+	const bool store = t < count;
+	const int n = nodes[store ? t : count - 1];
+	// the node's corrector data first: its loads overlap the feet's gathers
+	const int ci = bp.cond ? bp.corrOf[n] : -1;
+	int cnd = 0, code = 0;
+	double Bv[27];
+	if (ci >= 0) {
+		cnd = bp.cond[ci];
+		code = bp.outer[(size_t)stage * bp.count + ci];
+#pragma unroll
+		for (int i = 0; i < 27; i++) Bv[i] = bp.B[27 * (size_t)ci + i];
+	}
+	double o[kM];
+	group_invariants(n, c, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
+	// every lane corrects its own copy (identical inputs, identical results)
+#ifndef GCMX_SX_DIAG_NOCORR  // tuning builds only: time the kernel without the correctors
+	if (ci >= 0) border_correct_pre(o, ci, cnd, code, Bv, bp.S, Us, U1s, stage, args);
+#endif
+	if (store) {
+		wn[(size_t)c * N + n] = pick9(o, c);
+		if (c == 0) wn[(size_t)8 * N + n] = o[8];
+	}
+#ifndef GCMX_SX_DIAG_NOFIN
+	group_finalize(n, c, store && !deferred[n], o, U1s, Uns, un, wnext, N);
+#endif
 }
 
 // The step's border values b(t) into device memory (gsx_set_border_values).
@@ -548,17 +880,51 @@ __global__ __launch_bounds__(64) void k_sx_plain(const int* __restrict__ nodes,
 	for (int k = 0; k < kM; k++) u_[k * N + n] = u[k];
 }
 
+// The plain border corrections (as k_sx_plain) of the plan's nodes fused with the
+// first stage's beforeStage (w = U_0 u, as k_sx_transform<true>) of every node:
+// both act on one node's own vector, so one pass does the step's start.
+__global__ __launch_bounds__(256) void k_sx_begin(double* u_, double* __restrict__ w,
+                                                  const double* __restrict__ U0,
+                                                  const int* __restrict__ corrOf,
+                                                  const int* __restrict__ cond,
+                                                  const double* __restrict__ Sm, int N, BorderArgs args) {
+	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	if (n >= N) return;
+	double u[kM];
+#pragma unroll
+	for (int k = 0; k < kM; k++) u[k] = u_[k * N + n];
+	const int t = corrOf ? corrOf[n] : -1;
+	if (t >= 0) {
+		const int c = cond[t];
+		const double b[3] = {args.b[3 * c], args.b[3 * c + 1], args.b[3 * c + 2]};
+		plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+		for (int k = 0; k < kM; k++) u_[k * N + n] = u[k];
+	}
+	double wv[kM];
+	mat_vec(U0, u, wv);
+#pragma unroll
+	for (int k = 0; k < kM; k++) w[(size_t)n * kM + k] = wv[k];
+}
+
 // ContactCorrectorInRiemannInvariants::applyInGlobalBasis (ContactCorrector.hpp:333-348):
 // matchInnersAndOuters (zeroing decided on the host), invariants -> PDE (U1),
 // ContactCorrectorInPdeVectors::applyInGlobalBasis (:150-247), PDE -> invariants (U).
 __global__ __launch_bounds__(64) void k_sx_contact(
     const int* __restrict__ na, const int* __restrict__ nb, const double* __restrict__ normal,
     const double* __restrict__ Sm, const signed char* __restrict__ codeA,
-    const signed char* __restrict__ codeB, const double* __restrict__ UA,
-    const double* __restrict__ U1A, const double* __restrict__ UB, const double* __restrict__ U1B,
+    const signed char* __restrict__ codeB, const double* __restrict__ UA_,
+    const double* __restrict__ U1A_, const double* __restrict__ UB_, const double* __restrict__ U1B_,
     double* wnA, double* wnB, int NA, int NB, int count, int stage, double min1, double min2,
-    const double* __restrict__ UnextA, const double* __restrict__ UnextB, double* unA, double* unB,
+    const double* __restrict__ UnextA_, const double* __restrict__ UnextB_, double* unA, double* unB,
     double* wnextA, double* wnextB) {
+	__shared__ SharedMats<6> sm;
+	stage_mats<6>(sm, {UA_, U1A_, UB_, U1B_, UnextA_, UnextB_});
+	const double* UA = sm.m[0];
+	const double* U1A = sm.m[1];
+	const double* UB = sm.m[2];
+	const double* U1B = sm.m[3];
+	const double* UnextA = UnextA_ ? sm.m[4] : nullptr;
+	const double* UnextB = UnextB_ ? sm.m[5] : nullptr;
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int a = na[t], b = nb[t];
@@ -765,6 +1131,7 @@ gcmx_status gsx_set_matrices(gsx_ctx* c, const double* U, const double* U1) {
 	s = upload(&c->mats, m.data(), m.size());
 	if (s) return s;
 	c->matsSet = true;
+	c->wStage = -1;
 	return GCMX_OK;
 }
 
@@ -860,7 +1227,7 @@ gcmx_status gsx_upload(gsx_ctx* c, const double* aos) {
 		for (int k = 0; k < kM; k++) soa[k * N + n] = aos[kM * n + k];
 	SX_TRY(hipStreamSynchronize(c->stream));
 	SX_TRY(hipMemcpy(c->u, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice));
-	c->chained = false;
+	c->wStage = -1;
 	return GCMX_OK;
 }
 
@@ -927,12 +1294,16 @@ gcmx_status gsx_set_border_values(gsx_ctx* c, const double* b) {
 	// written by a one-block kernel whose arguments carry the values: ordered on
 	// the context stream before the step that reads them, with no host buffer
 	// that must outlive the call
+	// (skipped when the values equal the ones already written: constant conditions)
 	if (c->bd.nCond) {
 		BorderValues v{};
 		for (int i = 0; i < 3 * c->bd.nCond; i++) v.b[i] = b[i];
-		hipLaunchKernelGGL(k_sx_set_border_values, dim3(1), dim3(64), 0, c->stream, c->bvals, v,
-		                   3 * c->bd.nCond);
-		SX_TRY(hipGetLastError());
+		if (!c->bd.valuesSet || std::memcmp(v.b, c->bd.lastValues, sizeof(v.b)) != 0) {
+			hipLaunchKernelGGL(k_sx_set_border_values, dim3(1), dim3(64), 0, c->stream, c->bvals, v,
+			                   3 * c->bd.nCond);
+			SX_TRY(hipGetLastError());
+			std::memcpy(c->bd.lastValues, v.b, sizeof(v.b));
+		}
 	}
 	c->bd.valuesSet = true;
 	return GCMX_OK;
@@ -943,14 +1314,22 @@ gcmx_status gsx_plain_correction(gsx_ctx* c) {
 	if (s) return s;
 	const BorderDev& bd = c->bd;
 	if (!bd.set || !bd.valuesSet) return fail(GCMX_ERR_STATE, "border plan / values not set");
-	if (bd.n)
+	if (c->matsSet) {  // fused with the first stage's beforeStage (the next call is stage 0)
+		hipLaunchKernelGGL(k_sx_begin, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->u, c->w,
+		                   c->mats, bd.n ? c->corrOf : nullptr, bd.cond, bd.S, c->N, bd.args);
+		c->wStage = 0;
+	} else if (bd.n) {
 		hipLaunchKernelGGL(k_sx_plain, dim3((bd.n + 63) / 64), dim3(64), 0, c->stream, bd.nodes,
 		                   bd.cond, bd.S, c->u, bd.n, c->N, bd.args);
+		c->wStage = -1;
+	}
 	SX_TRY(hipGetLastError());
 	return GCMX_OK;
 }
 
 namespace {
+// Node-kernel layout (gsx_set_node_lanes): eight lanes per node below 32 768 nodes.
+int node_lanes(const gsx_ctx* c) { return c->nodeLanes ? c->nodeLanes : (c->N < 32768 ? kL : 1); }
 // The next stage's U for the fused beforeStage, or null after the last stage of
 // the step (the next step starts with the plain corrections, which change u).
 const double* nextU(const gsx_ctx* c, int stage) {
@@ -969,22 +1348,36 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 	const int N = c->N;
 	const dim3 blk(256), grd((N + 255) / 256);
 	const StageDev& st = c->st[stage];
+	const bool l8 = node_lanes(c) == kL;
 	// beforeStage: the invariants come from the previous stage's final writers when
 	// chained, otherwise from a transform pass
-	if (!(c->chained && stage > 0))
+	if (c->wStage != stage)
 		hipLaunchKernelGGL(k_sx_transform<true>, grd, blk, 0, c->stream, c->u, c->w,
 		                   c->mats + stage * 81, N);
-	c->chained = false;
-	hipLaunchKernelGGL(k_sx_gradient, grd, blk, 0, c->stream, c->w, c->grad, c->gOff, c->gNb,
-	                   c->coords, c->gW, c->gM, c->gDet, N);
+	c->wStage = -1;
+	if (l8)
+		hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + 255) / 256), blk, 0, c->stream, c->w,
+		                   c->grad, c->gOff, c->gNb, c->coords, c->gW, c->gM, c->gDet, N);
+	else
+		hipLaunchKernelGGL(k_sx_gradient, grd, blk, 0, c->stream, c->w, c->grad, c->gOff, c->gNb,
+		                   c->coords, c->gW, c->gM, c->gDet, N);
 	if (st.nBorder) {
 		const BorderDevArgs bp = {c->corrOf, (bd.set && bd.n) ? bd.cond : nullptr, bd.B, bd.S,
 		                          bd.outer, bd.n};
-		// border lists are short (a surface): 64-thread blocks spread them over the CUs
-		hipLaunchKernelGGL(k_sx_border, dim3((st.nBorder + 63) / 64), dim3(64), 0, c->stream, st.border,
-		                   st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
-		                   c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
-		                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N);
+		if (l8) {
+#ifdef GCMX_SX_DIAG_TWICE  // tuning builds only: a second, warm-cache launch of the same kernel
+			for (int rep = 0; rep < 2; rep++)
+#endif
+			hipLaunchKernelGGL(k_sx_border_l8, dim3(((size_t)st.nBorder * kL + 255) / 256), blk, 0, c->stream,
+			                   st.border, st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w,
+			                   c->grad, c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
+			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N);
+		}
+		else  // border lists are short (a surface): 64-thread blocks spread them over the CUs
+			hipLaunchKernelGGL(k_sx_border, dim3((st.nBorder + 63) / 64), dim3(64), 0, c->stream, st.border,
+			                   st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
+			                   c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
+			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N);
 	}
 	SX_TRY(hipGetLastError());
 	return GCMX_OK;
@@ -999,7 +1392,11 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 	const int N = c->N;
 	const dim3 blk(256);
 	const StageDev& st = c->st[stage];
-	if (st.nInner)
+	if (st.nInner && node_lanes(c) == kL)
+		hipLaunchKernelGGL(k_sx_inner_l8, dim3(((size_t)st.nInner * kL + 255) / 256), blk, 0, c->stream,
+		                   st.inner, st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
+		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N);
+	else if (st.nInner)
 		hipLaunchKernelGGL(k_sx_inner, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
 		                   st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
 		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N);
@@ -1007,8 +1404,16 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 	std::swap(c->u, c->un);
 	if (stage < 2) {
 		std::swap(c->w, c->wnext);
-		c->chained = true;
+		c->wStage = stage + 1;
 	}
+	return GCMX_OK;
+}
+
+gcmx_status gsx_set_node_lanes(gsx_ctx* c, int lanes) {
+	gcmx_status s = check(c);
+	if (s) return s;
+	if (lanes != 0 && lanes != 1 && lanes != kL) return fail(GCMX_ERR_INVALID_ARG, "node lanes must be 0, 1 or 8");
+	c->nodeLanes = lanes;
 	return GCMX_OK;
 }
 
@@ -1088,6 +1493,7 @@ gcmx_status gsx_contact_plain(gsx_contact* c) {
 	gcmx_status s = check(c->a);
 	if (s) return s;
 	if (!c->n) return GCMX_OK;
+	c->a->wStage = c->b->wStage = -1;  // u changes under any prepared invariants
 	return onBothStreams(c, [&] {
 		hipLaunchKernelGGL(k_sx_contact_plain, dim3((c->n + 255) / 256), dim3(256), 0, c->a->stream,
 		                   c->na, c->nb, c->S, c->a->u, c->b->u, c->a->N, c->b->N, c->n);

@@ -502,6 +502,8 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    .def("sync", [](PySimplexEngine& p) { p.e->sync(); }, "wait for the bodies' streams")
 	    .def("set_replay_steps", [](PySimplexEngine& p, bool on) { p.e->setReplaySteps(on); },
 	         "gsx_step graph replay or the individual stage calls (default)", py::arg("on"))
+	    .def("set_node_lanes", [](PySimplexEngine& p, int lanes) { p.e->setNodeLanes(lanes); },
+	         "node-kernel layout: 0 automatic, 1 thread per node, 8 lanes per node", py::arg("lanes"))
 	    .def_property_readonly("steps", [](PySimplexEngine& p) { return p.e->stepsDone(); })
 	    .def_property_readonly("time_step", [](PySimplexEngine& p) { return p.e->timeStepValue(); })
 	    .def_property_readonly("required_time", [](PySimplexEngine& p) { return p.e->getRequiredTime(); });

@@ -1228,6 +1228,10 @@ void Engine::plainCorrections() {
 		if (b.hasBorderPlan) gcmxCheck(gsx_plain_correction(b.ctx), "gsx_plain_correction");
 }
 
+void Engine::setNodeLanes(int lanes) {
+	for (auto& b : bodies) gcmxCheck(gsx_set_node_lanes(b.ctx, lanes), "gsx_set_node_lanes");
+}
+
 Engine::~Engine() {
 	for (auto* c : contacts) gsx_contact_destroy(c);
 	for (auto& b : bodies) gsx_destroy(b.ctx);

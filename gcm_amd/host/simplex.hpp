@@ -252,6 +252,8 @@ public:
 	/// stage calls (default); identical results.  Measured equal speed on MI355X:
 	/// the step is bound by the kernels' own duration, not by launches.
 	void setReplaySteps(bool on) { replaySteps = on; }
+	/// Thread layout of every body's node kernels (gsx_set_node_lanes: 0 auto, 1, 8).
+	void setNodeLanes(int lanes);
 
 protected:
 	void nextTimeStep() override;

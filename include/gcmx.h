@@ -297,6 +297,12 @@ gcmx_status gsx_stage(gsx_ctx* ctx, int stage);
 gcmx_status gsx_stage_nodes(gsx_ctx* ctx, int stage);
 /* border correctors + innerStage + afterStage + swap. */
 gcmx_status gsx_stage_finish(gsx_ctx* ctx, int stage);
+/* Thread layout of the node kernels (gradient, border, inner): 1 = one thread per
+ * node (throughput layout for large meshes), 8 = eight lanes per node, one per
+ * component / characteristic foot (latency layout for the reference's mesh
+ * sizes: a node's dependent gathers run in parallel), 0 = automatic (8 below
+ * 32 768 nodes).  Results are identical. */
+gcmx_status gsx_set_node_lanes(gsx_ctx* ctx, int lanes);
 
 /* ---- simplex contact correctors ----------------------------------------------
  * ContactCorrectorInRiemannInvariants<Elastic, Elastic, AdhesionContactMatrixCreator>

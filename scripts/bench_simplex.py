@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="node-kernel layout (gsx_set_node_lanes): 0 automatic, 1, 8")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from a gsx_step HIP graph instead of the stage calls")
     a = ap.parse_args()
@@ -56,6 +58,7 @@ def main():
         task.number_of_snaps = 10 ** 6
         e = H.SimplexEngine(task)
         e.set_replay_steps(a.graph)
+        e.set_node_lanes(a.lanes)
         setup = time.perf_counter() - t0
         nv = sum(e.number_of_vertices(b) for b in range(e.number_of_bodies))
         e.run_steps(a.warmup)
@@ -70,7 +73,7 @@ def main():
             "ms_per_step": round(dt / a.steps * 1e3, 4), "vertices": nv,
             "bodies": e.number_of_bodies, "contact_pairs": e.number_of_contact_pairs,
             "steps": a.steps, "warmup": a.warmup, "setup_s": round(setup, 1), "dtype": "f64",
-            "graph": a.graph,
+            "graph": a.graph, "lanes": a.lanes,
         }), flush=True)
 
 

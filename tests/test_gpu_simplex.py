@@ -17,12 +17,25 @@ def H():
     return _gcm_host
 
 
+@pytest.fixture(params=[1, 8], ids=["lanes1", "lanes8"])
+def lanes(request):
+    """gsx_set_node_lanes: one thread per node, or eight lanes per node (the
+    automatic choice below 32 768 nodes, i.e. for every mesh here)."""
+    return request.param
+
+
+def engine(H, t, lanes):
+    e = H.SimplexEngine(t)
+    e.set_node_lanes(lanes)
+    return e
+
+
 @pytest.mark.parametrize("n,courant,jitter,seed,steps", [(4, 1.0, 0.1, 7, 3), (4, 2.0, 0.1, 7, 2),
                                                          (6, 1.3, 0.15, 9, 2)])
-def test_simplex_engine_matches_oracle(H, n, courant, jitter, seed, steps):
+def test_simplex_engine_matches_oracle(H, lanes, n, courant, jitter, seed, steps):
     t = host_task(n, courant, jitter, seed, vector=[0.1 * i for i in range(9)])
     p = H.simplex_plans(t)
-    e = H.SimplexEngine(t)
+    e = engine(H, t, lanes)
     assert e.time_step == p["tau"]
     o = oracle_engine(p, courant)
     e.run_steps(steps)
@@ -49,13 +62,13 @@ from tests.simplex_spec import FREE_BORDER, MIXED_BORDER  # noqa: E402
 @pytest.mark.parametrize("border,n,courant,steps", [(FREE_BORDER, 4, 1.0, 3), (MIXED_BORDER, 4, 1.3, 3),
                                                     (FREE_BORDER, 5, 2.0, 2)],
                          ids=["free-c1", "mixed-c1.3", "free-c2"])
-def test_simplex_border_correctors_match_oracle(H, border, n, courant, steps):
+def test_simplex_border_correctors_match_oracle(H, lanes, border, n, courant, steps):
     """BorderCorrectorInRiemannInvariants (GLOBAL_BASIS) + the plain correction at
     the start of every step: GPU == oracle bitwise (the cube task's free surface,
     main.cpp:209-220, and a time-dependent FIXED_VELOCITY patch)."""
     t = host_task(n, courant, 0.1, 7, border=border)
     p = H.simplex_plans(t)
-    e = H.SimplexEngine(t)
+    e = engine(H, t, lanes)
     o = oracle_engine(p, courant, border)
     assert len(o.corrected) == len(p["border_plan"]["nodes"]) > 0
     e.run_steps(steps)
@@ -73,13 +86,13 @@ from tests.simplex_spec import fracture_task  # noqa: E402
 
 
 @pytest.mark.parametrize("courant,steps", [(1.0, 3), (1.7, 2)])
-def test_fracture_layer_matches_oracle(H, courant, steps):
+def test_fracture_layer_matches_oracle(H, lanes, courant, steps):
     """BASELINE config 5 (meshes/layers_with_fracture.off): the layer with the
     fracture cavity, free surface on the box and on the fracture faces
     (border correctors), GPU == oracle bitwise."""
     t = fracture_task((16, 16, 8), courant)
     p = H.simplex_plans(t)
-    e = H.SimplexEngine(t)
+    e = engine(H, t, lanes)
     o = oracle_engine(p, courant, FREE_BORDER)
     e.run_steps(steps)
     for _ in range(steps):
@@ -95,14 +108,14 @@ from tests.simplex_spec import layered_task, oracle_multi  # noqa: E402
 @pytest.mark.parametrize("n,courant,steps,border", [(6, 1.0, 3, None), (6, 1.7, 2, None),
                                                     (5, 1.3, 2, MIXED_BORDER)],
                          ids=["c1", "c1.7", "mixed-c1.3"])
-def test_layered_adhesion_contact_matches_oracle(H, n, courant, steps, border):
+def test_layered_adhesion_contact_matches_oracle(H, lanes, n, courant, steps, border):
     """Two bodies of different materials glued by ADHESION: the contact correctors
     (the 3 + 3 system, the 6 x 6 GSL system of a one-sided node and the averaged
     pair) between the bodies' node and inner phases, the plain contact correction
     at every step, border correctors on the outer surface: GPU == oracle bitwise."""
     t = layered_task(n, courant, border=border)
     p = H.simplex_plans(t)
-    e = H.SimplexEngine(t)
+    e = engine(H, t, lanes)
     assert e.number_of_bodies == 2 and e.time_step == p["tau"]
     o = oracle_multi(p, courant, border=border if border is not None else FREE_BORDER)
     e.run_steps(steps)
@@ -138,7 +151,7 @@ def test_simplex_engine_writes_vtu_snapshots(H, tmp_path, monkeypatch):
         assert np.array_equal(arrays["Velocity"], e.pde(body)[:, :3].astype(np.float32))
 
 
-def test_inm_mesh_engine_matches_oracle(H, tmp_path):
+def test_inm_mesh_engine_matches_oracle(H, lanes, tmp_path):
     """INM_MESHER (InmMeshLoader.hpp): a two-material tetrahedral mesh read from an
     INM file, per-cell materials as body ids, ADHESION contact between them:
     GPU == oracle bitwise."""
@@ -148,7 +161,7 @@ def test_inm_mesh_engine_matches_oracle(H, tmp_path):
     write_inm(path, P, C, G)
     t = layered_task(5, 1.0, inm=path)
     p = H.simplex_plans(t)
-    e = H.SimplexEngine(t)
+    e = engine(H, t, lanes)
     o = oracle_multi(p, 1.0)
     e.run_steps(2)
     for _ in range(2):
@@ -159,7 +172,7 @@ def test_inm_mesh_engine_matches_oracle(H, tmp_path):
 
 
 @pytest.mark.parametrize("workload", ["cube", "layered"])
-def test_graph_replayed_steps_equal_individual_calls(H, workload):
+def test_graph_replayed_steps_equal_individual_calls(H, lanes, workload):
     """gsx_step (one step captured into a HIP graph per layer state and replayed)
     == the individual gsx_stage_nodes / gsx_contact_correct / gsx_stage_finish
     calls, bitwise, over enough steps to replay both layer parities, with
@@ -170,7 +183,7 @@ def test_graph_replayed_steps_equal_individual_calls(H, workload):
     mk = (lambda: host_task(6, 1.0, 0.1, 7, border=MIXED_BORDER)) if workload == "cube" else \
         (lambda: layered_task(5, 1.0))
     def run(replay):  # one engine at a time: Clock is process-global, as in the reference
-        e = H.SimplexEngine(mk())
+        e = engine(H, mk(), lanes)
         e.set_replay_steps(replay)
         out = []
         for chunk in (1, 2, 3):
