@@ -239,6 +239,11 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "kernel": dom_name, "kernel_avg_ms": round(avg_ms, 4),
+                # the library's "fused_xyz" bucket is the one-pass step; with bs 2 and
+                # Z <= 512 it launches k_step_tx2 (kernels_xyz.hip), else k_fused_xyz
+                "kernel_symbol": ("k_step_tx2<2, 512, KF0, UNI, !FACES>" if N <= 512
+                                  else "k_fused_xyz<2, 1024, KF0, UNI>")
+                if dom_name.startswith("fused_xyz") else dom_name,
                 "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
                 "kernels": {k: {"avg_ms": round(v["total_ms"] / max(1, v["launches"]), 4),
                                 "GBps": round(v["bytes_per_launch"] /

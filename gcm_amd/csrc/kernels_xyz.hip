@@ -237,17 +237,11 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #ifndef GCMX_TX2_ZS2  // split the ahead-loads around the two nodes' Z stage + stores (-1: unless NB)
 #define GCMX_TX2_ZS2 -1
 #endif
-#ifndef GCMX_TX2_LA  // tuning: where the ahead-loads of the next X stage are issued (0: after barrier 2)
-#define GCMX_TX2_LA 0
-#endif
 #ifndef GCMX_TX2_NB  // UNI launches: Z exchange without block barriers (per-wave regions + edge ring)
 #define GCMX_TX2_NB 1
 #endif
 #ifndef GCMX_TX2_SLEEP  // NB: s_sleep argument while a neighbour wave's edges are not there yet
 #define GCMX_TX2_SLEEP 1
-#endif
-#ifndef GCMX_TX2_XALL  // every X-stage load issued ahead (with the ahead pairs)
-#define GCMX_TX2_XALL 0
 #endif
 #ifndef GCMX_TX2_DIAG  // tuning builds only: per-wave phase cycle counters (s_memtime)
 #define GCMX_TX2_DIAG 0
@@ -470,8 +464,6 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// X-stage inputs issued ahead of the X stage: load pairs 0 and 1.
 	struct XPre {
 		PairWin a, b;
-		PairWin c;         // GCMX_TX2_XALL only
-		double cv[2][9];   // GCMX_TX2_XALL only (node-only components)
 	};
 	auto cv_load = [&](double (&cv)[2][9], unsigned o) {
 #pragma unroll
@@ -483,24 +475,16 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	auto x_load_ahead = [&](XPre& pre, int r) {
 		pair_load(P0{}, pre.a, base + (unsigned)r * sty);
 		pair_load(P1{}, pre.b, base + (unsigned)r * sty);
-		if constexpr (GCMX_TX2_XALL) {
-			pair_load(P2{}, pre.c, base + (unsigned)r * sty);
-			cv_load(pre.cv, base + (unsigned)r * sty);
-		}
 	};
 	// X stage of row r for both nodes: pair 2 and the node-only components are
 	// issued first, then the pairs are consumed in order.
 	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9]) {
 		const unsigned o = base + (unsigned)r * sty;
 		double rr[2][9], n0[2][9];
-		PairWin wc_;
-		double cv_[2][9];
-		if constexpr (!GCMX_TX2_XALL) {
-			pair_load(P2{}, wc_, o);
-			cv_load(cv_, o);
-		}
-		const PairWin& wc = GCMX_TX2_XALL ? pre.c : wc_;
-		const double(&cv)[2][9] = GCMX_TX2_XALL ? pre.cv : cv_;
+		PairWin wc;
+		double cv[2][9];
+		pair_load(P2{}, wc, o);
+		cv_load(cv, o);
 		sched_fence();
 		pair_rows(P0{}, pre.a, rr);
 		pair_rows(P1{}, pre.b, rr);
@@ -591,25 +575,12 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		const int ring = (y + BS) % (BS + 1);
 		XPre pre;
 		const int rn = clamp_row(y + BS + 1);
-		// GCMX_TX2_LA 1: pair 0 at the row start; 2: pair 0 at the row start and pair 1
-		// between the barriers; 3: both at the row start; 4: pair 0 after the Y stage
-		if constexpr (GCMX_TX2_LA == 1 || GCMX_TX2_LA == 2 || GCMX_TX2_LA == 3) {
-			sched_fence();
-			pair_load(P0{}, pre.a, base + (unsigned)rn * sty);
-			if constexpr (GCMX_TX2_LA == 3) pair_load(P1{}, pre.b, base + (unsigned)rn * sty);
-			sched_fence();
-		}
 #pragma unroll
 		for (int t = 0; t < 2; t++)
 			node_update<1, BS, KF0>(
 			    AY, [&](int j, int o) { return win[t][wslot(WMY, j)][BS + o]; },
 			    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cl[ring][t][wslot(CMY, j)][z]; },
 			    yv[t]);
-		if constexpr (GCMX_TX2_LA == 4) {
-			sched_fence();
-			pair_load(P0{}, pre.a, base + (unsigned)rn * sty);
-			sched_fence();
-		}
 		TX2_T(0);
 		const int es = y & 1;  // NB: edge ring slot of this row
 		if constexpr (NB) {
@@ -637,11 +608,6 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		} else {
 			__syncthreads();  // every wave has finished reading zl (previous row's Z stage)
 			TX2_T(1);
-			if constexpr (GCMX_TX2_LA == 2) {
-				sched_fence();
-				pair_load(P1{}, pre.b, base + (unsigned)rn * sty);
-				sched_fence();
-			}
 #pragma unroll
 			for (int t = 0; t < 2; t++)
 #pragma unroll
@@ -662,8 +628,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			TX2_T(2);
 		}
 		const unsigned offo = plane + (unsigned)y * sty + zo;
-		if constexpr (GCMX_TX2_LA != 0) {
-		} else if constexpr (ZS2) {
+		if constexpr (ZS2) {
 			sched_fence();
 			pair_load(P0{}, pre.a, base + (unsigned)rn * sty);
 			sched_fence();
@@ -701,7 +666,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		TX2_T(4);
 #pragma unroll
 		for (int t = 0; t < 2; t++) {  // each node's stores right after its Z stage
-			if constexpr (ZS2 && GCMX_TX2_LA != 2 && GCMX_TX2_LA != 3) {
+			if constexpr (ZS2) {
 				if (t == 1) {
 					sched_fence();
 					pair_load(P1{}, pre.b, base + (unsigned)rn * sty);

@@ -54,6 +54,8 @@ struct BorderDev {
 	int *nodes = nullptr, *cond = nullptr;
 	double *B = nullptr, *S = nullptr;
 	signed char* outer = nullptr;
+	double* md = nullptr;  // [entry][stage][side R, L][10]: B * Omega (3x3) and det, k_sx_border_prep
+	int2* nodeRec = nullptr;  // [node]: (plan entry, its condition) or (-1, 0)
 	BorderArgs args{};
 	bool set = false, valuesSet = false;
 	double lastValues[3 * GSX_MAX_BORDER_CONDITIONS] = {};  // what bvals holds once valuesSet
@@ -63,7 +65,8 @@ struct StageShift {  // crossingPoints' shift of every invariant: direction * (-
 	double d[6][3];
 };
 
-// Feet in a compact, coalesced layout ([k][n]): fv = the cell's (or face's)
+// Feet in a compact, coalesced layout ([k][pos], pos = position in the stage's
+// border list, then its inner list): fv = the cell's (or face's)
 // vertices, flam = barycentric weights, fmeta = kind | slot(i) << (4 + 4 i).  The
 // foot point of a CELL foot is recomputed as coords[n] + shift[k], the same IEEE
 // sum the host's plan made (gsx_set_stage_plan checks it).
@@ -76,6 +79,10 @@ struct StageDev {
 	int* inner = nullptr;
 	int nBorder = 0, nInner = 0;
 	bool set = false;
+	// border corrector records by position t in `border` (k_sx_border_rec): plan
+	// entry, condition, outer code, which sides are solvable; B; B * Omega and det
+	int4* rec = nullptr;
+	double *recB = nullptr, *recMd = nullptr;
 };
 
 }  // namespace
@@ -279,7 +286,7 @@ __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ?
 // gsx_set_stage_plan checks them; a foot that needs no gradient still reads one
 // it ignores), so one node costs three dependent memory round trips, not three
 // per foot.  The arithmetic of the selected kind is unchanged.
-__device__ __forceinline__ void node_invariants(int n, const int4* __restrict__ fv,
+__device__ __forceinline__ void node_invariants(int n, int pos, int P, const int4* __restrict__ fv,
                                                 const double4* __restrict__ flam,
                                                 const int* __restrict__ fmeta, const StageShift& sh,
                                                 const double* __restrict__ coords,
@@ -294,7 +301,7 @@ __device__ __forceinline__ void node_invariants(int n, const int4* __restrict__ 
 	double4 lv[6];
 #pragma unroll
 	for (int k = 0; k < 6; k++) {
-		const size_t e = (size_t)k * N + n;
+		const size_t e = (size_t)k * P + pos;
 		meta[k] = fmeta[e];
 		fvv[k] = fv[e];
 		lv[k] = flam[e];
@@ -404,19 +411,26 @@ __device__ void plain_correction(double (&u)[kM], int type, const double* __rest
 
 // calculateOuterWaveCorrection (common.hpp:186-202) with Omega = the U1 columns
 // `cols` (getColumnsFromGcmMatrices, common.hpp:153-165).
+// Its matrix part, B * Omega and det, depends only on the node's border matrix and
+// the stage's U1: owc_matrix is what k_sx_border_prep evaluates once per plan.
 template <class BT>  // B: a pointer into the plan or the node's 27 values in registers
-__device__ bool outer_wave_correction(const double (&u)[kM], const double* __restrict__ U1,
-                                      const int (&cols)[3], const BT& B,
-                                      const double (&b)[3], double minValid, double (&value)[kM]) {
-	double M[3][3];
+__device__ __forceinline__ double owc_matrix(const double* __restrict__ U1, const int (&cols)[3],
+                                             const BT& B, double (&M)[3][3]) {
 	for (int i = 0; i < 3; i++)
 		for (int j = 0; j < 3; j++) {
 			double x = B[i * kM + 0] * U1[0 * kM + cols[j]];
 			for (int n = 1; n < kM; n++) x += B[i * kM + n] * U1[n * kM + cols[j]];
 			M[i][j] = x;
 		}
-	const double det = det3(M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1],
-	                        M[2][2]);
+	return det3(M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1], M[2][2]);
+}
+
+template <class BT>  // B: a pointer into the plan or the node's 27 values in registers
+__device__ bool outer_wave_correction(const double (&u)[kM], const double* __restrict__ U1,
+                                      const int (&cols)[3], const BT& B,
+                                      const double (&b)[3], double minValid, double (&value)[kM]) {
+	double M[3][3];
+	const double det = owc_matrix(U1, cols, B, M);
 	if (!(fabs(det) > minValid)) return false;
 	double r[3];
 	for (int i = 0; i < 3; i++) {
@@ -509,6 +523,8 @@ struct BorderDevArgs {  // the border plan's device arrays (null cond = no plan)
 	const double *B, *S;
 	const signed char* outer;
 	int count;
+	const int4* rec;  // the stage's corrector records by list position (eight-lane kernel)
+	const double *recB, *recMd;
 };
 
 // contactAndBorderStage (hpp:57-95) for the contact and border nodes, the border
@@ -539,14 +555,14 @@ __global__ __launch_bounds__(64) void k_sx_border(
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
     double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, BorderArgs args,
     const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
-    double* __restrict__ un, double* __restrict__ wnext, int stage, int N) {
+    double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
 	__shared__ SharedMats<3> sm;
 	stage_mats<3>(sm, {U, U1, Unext});
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int n = nodes[t];
 	double out[kM];
-	node_invariants(n, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
+	node_invariants(n, pos0 + t, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
 	if (bp.cond) {
 		const int ci = bp.corrOf[n];
 		if (ci >= 0)
@@ -564,12 +580,12 @@ __global__ __launch_bounds__(256) void k_sx_inner(
     const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
     const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
-    double* __restrict__ un, double* __restrict__ wnext, int N) {
+    double* __restrict__ un, double* __restrict__ wnext, int N, int pos0, int P) {
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int n = nodes[t];
 	double out[kM];
-	node_invariants(n, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
+	node_invariants(n, pos0 + t, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, out);
 	finalize(n, out, U1, Unext, un, wnext, N);
 }
 
@@ -583,6 +599,13 @@ __global__ __launch_bounds__(256) void k_sx_inner(
 // U1 / U products are split by rows.  Every value is produced by the same
 // operations in the same order as in the node-per-thread kernels.
 constexpr int kL = 8;
+// Threads per block of the eight-lane kernels: their launches are a few thousand
+// groups of gather chains, so small blocks spread them over more CUs (each CU's
+// L1 / address units serve fewer gathering waves).
+#ifndef GCMX_SX_L8_BLOCK
+#define GCMX_SX_L8_BLOCK 256
+#endif
+constexpr int kL8Block = GCMX_SX_L8_BLOCK;
 
 __global__ __launch_bounds__(256) void k_sx_gradient_l8(const double* __restrict__ w,
                                                         double* __restrict__ grad,
@@ -648,7 +671,7 @@ __global__ __launch_bounds__(256) void k_sx_gradient_l8(const double* __restrict
 }
 
 // interpolateValuesAround for one invariant k (0..5) of node n (node_invariants' body).
-__device__ __forceinline__ double foot_value(int n, int k, const int4* __restrict__ fv,
+__device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const int4* __restrict__ fv,
                                              const double4* __restrict__ flam,
                                              const int* __restrict__ fmeta, const StageShift& sh,
                                              const double* __restrict__ coords,
@@ -663,7 +686,7 @@ __device__ __forceinline__ double foot_value(int n, int k, const int4* __restric
 			s1 = sh.d[kk][1];
 			s2 = sh.d[kk][2];
 		}
-	const size_t e = (size_t)k * N + n;
+	const size_t e = (size_t)k * P + pos;
 	const int meta = fmeta[e];
 	const int4 f = fv[e];
 	const double4 l = flam[e];
@@ -706,14 +729,14 @@ __device__ __forceinline__ double foot_value(int n, int k, const int4* __restric
 
 // All 9 new invariants of node n in every lane of its group (lane c < 6 interpolates
 // invariant c, lanes 6, 7 read the exact hits 6, 7; every lane reads 8).
-__device__ __forceinline__ void group_invariants(int n, int c, const int4* __restrict__ fv,
+__device__ __forceinline__ void group_invariants(int n, int c, int pos, int P, const int4* __restrict__ fv,
                                                  const double4* __restrict__ flam,
                                                  const int* __restrict__ fmeta, const StageShift& sh,
                                                  const double* __restrict__ coords,
                                                  const double* __restrict__ w,
                                                  const double* __restrict__ grad,
                                                  const double* __restrict__ wn, int N, double (&o)[kM]) {
-	const double mine = c < 6 ? foot_value(n, c, fv, flam, fmeta, sh, coords, w, grad, wn, N)
+	const double mine = c < 6 ? foot_value(n, c, pos, P, fv, flam, fmeta, sh, coords, w, grad, wn, N)
 	                          : w[(size_t)n * kM + c];
 	const double w8 = w[(size_t)n * kM + 8];
 #pragma unroll
@@ -772,46 +795,153 @@ __global__ __launch_bounds__(256) void k_sx_inner_l8(
     const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
     const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
-    double* __restrict__ un, double* __restrict__ wnext, int N) {
+    double* __restrict__ un, double* __restrict__ wnext, int N, int pos0, int P) {
 	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const int t = gid / kL, c = gid % kL;
 	// whole groups stay active for the shuffles; a group past the list redoes the last node, unstored
 	const bool store = t < count;
 	const int n = nodes[store ? t : count - 1];
 	double o[kM];
-	group_invariants(n, c, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
+	group_invariants(n, c, pos0 + (store ? t : count - 1), P, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
 	group_finalize(n, c, store, o, U1, Unext, un, wnext, N);
 }
 
-// border_correct with the node's plan data already in registers (B, condition,
-// outer code) and both one-sided corrections always evaluated, so the lanes of a
-// wave do not serialise over the nodes' codes; the result of each path is the
-// one border_correct computes.
-__device__ void border_correct_pre(double (&w)[kM], int t, int c, int code, const double (&B)[27],
-                                   const double* __restrict__ Sm, const double* __restrict__ U,
-                                   const double* __restrict__ U1, int stage, const BorderArgs& args) {
-	const double b[3] = {args.b[3 * c], args.b[3 * c + 1], args.b[3 * c + 2]};
-	const double minValid = args.minDet[c][stage];
-	double u[kM];
-	mat_vec(U1, w, u);
-	const int R[3] = {1, 3, 5}, L[3] = {0, 2, 4};  // Model.cpp:81-82
-	double vr[kM], vl[kM];
-	const bool okR = outer_wave_correction(u, U1, R, B, b, minValid, vr);
-	const bool okL = outer_wave_correction(u, U1, L, B, b, minValid, vl);
+// The matrix part of calculateOuterWaveCorrection for every border-plan entry t,
+// stage s and side (R: Omega = U1 columns 1, 3, 5; L: 0, 2, 4; Model.cpp:81-82):
+// B * Omega and its determinant (owc_matrix), md[((t * 3 + s) * 2 + side) * 10].
+// Static for a plan and its matrices, so it is evaluated once, not per step.
+__global__ __launch_bounds__(256) void k_sx_border_prep(const double* __restrict__ Bm,
+                                                        const double* __restrict__ mats, int count,
+                                                        double* __restrict__ md) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= count * 6) return;
+	const int t = i / 6, s = (i / 2) % 3, side = i & 1;
+	const double* U1 = mats + 3 * 81 + s * 81;
+	const int R[3] = {1, 3, 5}, L[3] = {0, 2, 4};
+	double M[3][3];
+	const double det = side ? owc_matrix(U1, L, Bm + 27 * (size_t)t, M) : owc_matrix(U1, R, Bm + 27 * (size_t)t, M);
+	double* o = md + (size_t)i * 10;
+	for (int a = 0; a < 3; a++)
+		for (int b = 0; b < 3; b++) o[3 * a + b] = M[a][b];
+	o[9] = det;
+}
+
+// The stage's corrector record of every border-list position t: the node's plan
+// entry ci (-1: not corrected), its condition and outer-wave code, whether each
+// side's system is solvable (|det| > minDet of the condition and stage, as
+// outer_wave_correction decides), B and the two sides' B * Omega, det -- so the
+// border kernel reads them by t, not through node -> entry -> condition.
+__global__ __launch_bounds__(256) void k_sx_border_rec(const int* __restrict__ border, int nb,
+                                                       const int* __restrict__ corrOf,
+                                                       const int* __restrict__ cond,
+                                                       const signed char* __restrict__ outer, int count,
+                                                       const double* __restrict__ Bm,
+                                                       const double* __restrict__ md, int stage,
+                                                       BorderArgs args, int4* __restrict__ rec,
+                                                       double* __restrict__ recB,
+                                                       double* __restrict__ recMd) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= nb) return;
+	const int ci = corrOf[border[t]];
+	if (ci < 0) {
+		rec[t] = make_int4(-1, 0, 0, 0);
+		return;
+	}
+	const int cnd = cond[ci];
+	const double* m = md + ((size_t)ci * 3 + stage) * 20;
+	const double minValid = args.minDet[cnd][stage];
+	const int okR = fabs(m[9]) > minValid, okL = fabs(m[19]) > minValid;
+	rec[t] = make_int4(ci, cnd, outer[(size_t)stage * count + ci], okR | (okL << 1));
+	for (int i = 0; i < 27; i++) recB[(size_t)t * 27 + i] = Bm[27 * (size_t)ci + i];
+	for (int i = 0; i < 20; i++) recMd[(size_t)t * 20 + i] = m[i];
+}
+
+__device__ __forceinline__ double pick3(const double (&v)[3], int i) {
+	return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]);
+}
+
+// border_correct (BorderCorrector.hpp:256-265, 118-165) split over the node's group of kL lanes (c = lane in the group,
+// h = c / 4, q = c % 4): the U1 and U products by rows; side R in lanes 0-3 and side L
+// in lanes 4-7, the matrix part precomputed (k_sx_border_prep, `Md` of this lane's
+// side), the residual's three rows over a half's lanes (Brow = row min(q, 2) of B),
+// the correction's components q, q + 4 and 8 per lane; the two sides meet through
+// one shuffle; both one-sided corrections are always evaluated, so the lanes of a
+// wave do not serialise over the nodes' codes.  Every value is produced by
+// border_correct's operations in its order.  Returns the node's corrected invariants in every lane of the group.
+__device__ __forceinline__ void border_correct_l8(double (&w)[kM], int t, int c, int cnd, int code,
+                                                  int okRL, const double (&Brow)[kM],
+                                                  const double (&Md)[10],
+                                                  const double* __restrict__ Sm,
+                                                  const double* __restrict__ U,
+                                                  const double* __restrict__ U1, int stage,
+                                                  const BorderArgs& args) {
+	const double b[3] = {args.b[3 * cnd], args.b[3 * cnd + 1], args.b[3 * cnd + 2]};
+	const int h = c >> 2, q = c & 3;
+	double u[kM], uc, u8;
+	rows_mat_vec(U1, w, c, uc, u8);  // u = U1 w (mat_vec), rows c and 8 here
+#pragma unroll
+	for (int j = 0; j < kL; j++) u[j] = __shfl(uc, j, kL);
+	u[8] = u8;
+	double r[3];
+	{  // r_i = b_i - B(i, :) u, row min(q, 2) here
+		double x = Brow[0] * u[0];
+#pragma unroll
+		for (int n = 1; n < kM; n++) x += Brow[n] * u[n];
+		const double ri = pick3(b, q < 3 ? q : 2) - x;
+#pragma unroll
+		for (int i = 0; i < 3; i++) r[i] = __shfl(ri, 4 * h + i, kL);
+	}
+	const double det = Md[9];
+	const double d1 = det3(r[0], Md[1], Md[2], r[1], Md[4], Md[5], r[2], Md[7], Md[8]);
+	const double d2 = det3(Md[0], r[0], Md[2], Md[3], r[1], Md[5], Md[6], r[2], Md[8]);
+	const double d3 = det3(Md[0], Md[1], r[0], Md[3], Md[4], r[1], Md[6], Md[7], r[2]);
+	const double alpha[3] = {d1 / det, d2 / det, d3 / det};
+	const int c0 = 1 - h;  // this side's columns c0, c0 + 2, c0 + 4
+	auto value = [&](int i) {
+		double x = U1[i * kM + c0] * alpha[0];
+		x += U1[i * kM + c0 + 2] * alpha[1];
+		x += U1[i * kM + c0 + 4] * alpha[2];
+		return x;
+	};
+	const double vq = value(q), vq4 = value(q + 4), v8 = value(8);
+	// this side's value of the own component c, the other side's from the partner c ^ 4
+	const double mine = h ? vq4 : vq;
+	const double other = __shfl_xor(h ? vq : vq4, 4, kL);
+	const double other8 = __shfl_xor(v8, 4, kL);
+	const double vrc = h ? other : mine, vlc = h ? mine : other;
+	const double vr8 = h ? other8 : v8, vl8 = h ? v8 : other8;
+	const bool okR = okRL & 1, okL = (okRL >> 1) & 1;
+	bool plain = false;
 	if (code == 1 || code == 2) {
 		if (code == 1 ? okR : okL) {
-			for (int k = 0; k < kM; k++) u[k] += code == 1 ? vr[k] : vl[k];
+			uc += code == 1 ? vrc : vlc;
+			u8 += code == 1 ? vr8 : vl8;
 		} else {
-			plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+			plain = true;
 		}
 	} else {
 		if (okR && okL) {
-			for (int k = 0; k < kM; k++) u[k] += (vr[k] + vl[k]) / 2;
+			uc += (vrc + vlc) / 2;
+			u8 += (vr8 + vl8) / 2;
 		} else {
-			plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
+			plain = true;
 		}
 	}
-	mat_vec(U, u, w);
+	double up[kM];  // the plain correction: per node, so the whole group takes it
+#pragma unroll
+	for (int j = 0; j < kM; j++) up[j] = u[j];
+	if (plain) plain_correction(up, args.type[cnd], Sm + 9 * (size_t)t, b);
+#pragma unroll
+	for (int j = 0; j < kL; j++) {
+		const double sj = __shfl(uc, j, kL);
+		u[j] = plain ? up[j] : sj;
+	}
+	u[8] = plain ? up[8] : u8;
+	double wc, w8;  // w = U u (mat_vec), rows c and 8 here
+	rows_mat_vec(U, u, c, wc, w8);
+#pragma unroll
+	for (int j = 0; j < kL; j++) w[j] = __shfl(wc, j, kL);
+	w[8] = w8;
 }
 
 __global__ __launch_bounds__(256) void k_sx_border_l8(
@@ -820,31 +950,45 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
     double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, BorderArgs args,
     const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
-    double* __restrict__ un, double* __restrict__ wnext, int stage, int N) {
+    double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
+#ifndef GCMX_SX_L8_STAGE  // tuning: stage U / U1 / U_next in LDS (1) or read them through the caches (0)
+#define GCMX_SX_L8_STAGE 0
+#endif
+#if GCMX_SX_L8_STAGE
 	__shared__ SharedMats<3> sm;
 	stage_mats<3>(sm, {U, U1, Unext});
 	const double* Us = sm.m[0];
 	const double* U1s = sm.m[1];
 	const double* Uns = Unext ? sm.m[2] : nullptr;
+#else
+	const double* Us = U;
+	const double* U1s = U1;
+	const double* Uns = Unext;
+#endif
 	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const int t = gid / kL, c = gid % kL;
 	const bool store = t < count;
 	const int n = nodes[store ? t : count - 1];
 	// the node's corrector data first: its loads overlap the feet's gathers
-	const int ci = bp.cond ? bp.corrOf[n] : -1;
-	int cnd = 0, code = 0;
-	double Bv[27];
+	// the node's corrector record first (by list position: no dependent loads), so
+	// its loads overlap the feet's gathers
+	const int tr = store ? t : count - 1;
+	const int4 rc = bp.cond ? bp.rec[tr] : make_int4(-1, 0, 0, 0);
+	const int ci = rc.x, cnd = rc.y, code = rc.z;
+	double Brow[kM], Md[10];
 	if (ci >= 0) {
-		cnd = bp.cond[ci];
-		code = bp.outer[(size_t)stage * bp.count + ci];
+		const int q = c & 3;
+		const double* Bi = bp.recB + 27 * (size_t)tr + kM * (q < 3 ? q : 2);
 #pragma unroll
-		for (int i = 0; i < 27; i++) Bv[i] = bp.B[27 * (size_t)ci + i];
+		for (int i = 0; i < kM; i++) Brow[i] = Bi[i];
+		const double* m = bp.recMd + (size_t)tr * 20 + (c >> 2) * 10;
+#pragma unroll
+		for (int i = 0; i < 10; i++) Md[i] = m[i];
 	}
 	double o[kM];
-	group_invariants(n, c, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
-	// every lane corrects its own copy (identical inputs, identical results)
+	group_invariants(n, c, pos0 + tr, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
 #ifndef GCMX_SX_DIAG_NOCORR  // tuning builds only: time the kernel without the correctors
-	if (ci >= 0) border_correct_pre(o, ci, cnd, code, Bv, bp.S, Us, U1s, stage, args);
+	if (ci >= 0) border_correct_l8(o, ci, c, cnd, code, rc.w, Brow, Md, bp.S, Us, U1s, stage, args);
 #endif
 	if (store) {
 		wn[(size_t)c * N + n] = pick9(o, c);
@@ -885,17 +1029,17 @@ __global__ __launch_bounds__(64) void k_sx_plain(const int* __restrict__ nodes,
 // both act on one node's own vector, so one pass does the step's start.
 __global__ __launch_bounds__(256) void k_sx_begin(double* u_, double* __restrict__ w,
                                                   const double* __restrict__ U0,
-                                                  const int* __restrict__ corrOf,
-                                                  const int* __restrict__ cond,
+                                                  const int2* __restrict__ nodeRec,
                                                   const double* __restrict__ Sm, int N, BorderArgs args) {
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
 	if (n >= N) return;
 	double u[kM];
 #pragma unroll
 	for (int k = 0; k < kM; k++) u[k] = u_[k * N + n];
-	const int t = corrOf ? corrOf[n] : -1;
+	const int2 rc = nodeRec ? nodeRec[n] : make_int2(-1, 0);  // (entry, condition)
+	const int t = rc.x;
 	if (t >= 0) {
-		const int c = cond[t];
+		const int c = rc.y;
 		const double b[3] = {args.b[3 * c], args.b[3 * c + 1], args.b[3 * c + 2]};
 		plain_correction(u, args.type[c], Sm + 9 * (size_t)t, b);
 		for (int k = 0; k < kM; k++) u_[k * N + n] = u[k];
@@ -1038,6 +1182,32 @@ gcmx_status upload(T** dst, const T* src, size_t n) {
 	return GCMX_OK;
 }
 
+// The corrector matrices of the current border plan and matrices (k_sx_border_prep)
+// and every set stage's records (k_sx_border_rec), enqueued on the context stream
+// whenever one of matrices, border plan or a stage plan is (re)set.
+gcmx_status prep_border(gsx_ctx* c) {
+	BorderDev& bd = c->bd;
+	if (!c->matsSet || !bd.set || bd.n == 0) return GCMX_OK;
+	if (!bd.md) SX_TRY(hipMalloc(&bd.md, (size_t)bd.n * 60 * sizeof(double)));
+	hipLaunchKernelGGL(k_sx_border_prep, dim3(((size_t)bd.n * 6 + 255) / 256), dim3(256), 0, c->stream,
+	                   bd.B, c->mats, bd.n, bd.md);
+	SX_TRY(hipGetLastError());
+	for (int s = 0; s < 3; s++) {
+		StageDev& st = c->st[s];
+		if (!st.set || st.nBorder == 0) continue;
+		if (!st.rec) {
+			SX_TRY(hipMalloc(&st.rec, (size_t)st.nBorder * sizeof(int4)));
+			SX_TRY(hipMalloc(&st.recB, (size_t)st.nBorder * 27 * sizeof(double)));
+			SX_TRY(hipMalloc(&st.recMd, (size_t)st.nBorder * 20 * sizeof(double)));
+		}
+		hipLaunchKernelGGL(k_sx_border_rec, dim3((st.nBorder + 255) / 256), dim3(256), 0, c->stream,
+		                   st.border, st.nBorder, c->corrOf, bd.cond, bd.outer, bd.n, bd.B, bd.md, s,
+		                   bd.args, st.rec, st.recB, st.recMd);
+		SX_TRY(hipGetLastError());
+	}
+	return GCMX_OK;
+}
+
 }  // namespace
 
 namespace {
@@ -1106,7 +1276,7 @@ void gsx_destroy(gsx_ctx* c) {
 	                c->gRows, c->gW, c->gM, c->gDet};
 	for (void* p : ptrs)
 		if (p) (void)hipFree(p);
-	void* bptrs[] = {c->bd.nodes, c->bd.cond, c->bd.B, c->bd.S, c->bd.outer};
+	void* bptrs[] = {c->bd.nodes, c->bd.cond, c->bd.B, c->bd.S, c->bd.outer, c->bd.md, c->bd.nodeRec};
 	for (void* p : bptrs)
 		if (p) (void)hipFree(p);
 	for (auto& st : c->st) {
@@ -1115,6 +1285,9 @@ void gsx_destroy(gsx_ctx* c) {
 		if (st.fmeta) (void)hipFree(st.fmeta);
 		if (st.border) (void)hipFree(st.border);
 		if (st.inner) (void)hipFree(st.inner);
+		if (st.rec) (void)hipFree(st.rec);
+		if (st.recB) (void)hipFree(st.recB);
+		if (st.recMd) (void)hipFree(st.recMd);
 	}
 	if (c->stream) (void)hipStreamDestroy(c->stream);
 	delete c;
@@ -1132,7 +1305,7 @@ gcmx_status gsx_set_matrices(gsx_ctx* c, const double* U, const double* U1) {
 	if (s) return s;
 	c->matsSet = true;
 	c->wStage = -1;
-	return GCMX_OK;
+	return prep_border(c);
 }
 
 gcmx_status gsx_set_gradient_plan(gsx_ctx* c, const int* off, const int* nbs, const double* rows,
@@ -1177,11 +1350,15 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 		if (border[i] < 0 || border[i] >= N) return fail(GCMX_ERR_INVALID_ARG, "node out of range");
 	for (int i = 0; i < ni; i++)
 		if (inner[i] < 0 || inner[i] >= N) return fail(GCMX_ERR_INVALID_ARG, "node out of range");
-	std::vector<int4> fv((size_t)N * 6);
-	std::vector<double4> flam((size_t)N * 6);
-	std::vector<int> fmeta((size_t)N * 6);
-	for (int n = 0; n < N; n++)
+	// feet stored by list position (border list, then inner list), [k][pos]: the
+	// node kernels read them by the thread's position, not through the node id
+	const int P = nb + ni;
+	std::vector<int4> fv((size_t)P * 6);
+	std::vector<double4> flam((size_t)P * 6);
+	std::vector<int> fmeta((size_t)P * 6);
+	for (int pos = 0; pos < P; pos++)
 		for (int k = 0; k < 6; k++) {
+			const int n = pos < nb ? border[pos] : inner[pos - nb];
 			const gsx_foot& f = feet[(size_t)n * 6 + k];
 			const int nv = f.kind == GSX_FOOT_CELL ? 4 : f.kind == GSX_FOOT_SPACETIME ? 3 : 0;
 			if (f.kind < 0 || f.kind > 3) return fail(GCMX_ERR_INVALID_ARG, "bad foot kind");
@@ -1197,7 +1374,7 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 				for (int r = 0; r < 3; r++)
 					if (!(c->hostCoords[3 * (size_t)n + r] + shift[k * 3 + r] == f.q[r]))
 						return fail(GCMX_ERR_INVALID_ARG, "foot point is not node + shift");
-			const size_t e = (size_t)k * N + n;
+			const size_t e = (size_t)k * P + pos;
 			fv[e] = make_int4(nv > 0 ? f.v[0] : 0, nv > 1 ? f.v[1] : 0, nv > 2 ? f.v[2] : 0,
 			                  nv > 3 ? f.v[3] : 0);
 			flam[e] = make_double4(f.lam[0], f.lam[1], f.lam[2], f.lam[3]);
@@ -1211,10 +1388,17 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 		return s;
 	for (int k = 0; k < 6; k++)
 		for (int r = 0; r < 3; r++) st.shift.d[k][r] = shift[k * 3 + r];
+	if (st.rec && st.nBorder != nb) {  // the records are sized by the border list
+		SX_TRY(hipFree(st.rec));
+		SX_TRY(hipFree(st.recB));
+		SX_TRY(hipFree(st.recMd));
+		st.rec = nullptr;
+		st.recB = st.recMd = nullptr;
+	}
 	st.nBorder = nb;
 	st.nInner = ni;
 	st.set = true;
-	return GCMX_OK;
+	return prep_border(c);
 }
 
 gcmx_status gsx_upload(gsx_ctx* c, const double* aos) {
@@ -1263,6 +1447,8 @@ gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const d
 		if (outer[i] < 0 || outer[i] > 3) return fail(GCMX_ERR_INVALID_ARG, "bad outer code");
 	SX_TRY(hipStreamSynchronize(c->stream));
 	BorderDev& bd = c->bd;
+	if (bd.md) SX_TRY(hipFree(bd.md));  // sized by the plan: prep_border reallocates it
+	bd.md = nullptr;
 	if ((s = upload(&bd.nodes, nodes, (size_t)n)) || (s = upload(&bd.cond, cond, (size_t)n)) ||
 	    (s = upload(&bd.B, B, 27 * (size_t)n)) || (s = upload(&bd.S, S, 9 * (size_t)n)) ||
 	    (s = upload(&bd.outer, outer, 3 * (size_t)n)))
@@ -1272,7 +1458,11 @@ gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const d
 		if (corrOf[(size_t)nodes[i]] >= 0) return fail(GCMX_ERR_INVALID_ARG, "node corrected twice");
 		corrOf[(size_t)nodes[i]] = i;
 	}
-	if ((s = upload(&c->corrOf, corrOf.data(), corrOf.size()))) return s;
+	std::vector<int2> nodeRec((size_t)c->N, make_int2(-1, 0));
+	for (int i = 0; i < n; i++) nodeRec[(size_t)nodes[i]] = make_int2(i, cond[i]);
+	if ((s = upload(&c->corrOf, corrOf.data(), corrOf.size())) ||
+	    (s = upload(&bd.nodeRec, nodeRec.data(), nodeRec.size())))
+		return s;
 	bd.n = n;
 	bd.nCond = n_cond;
 	bd.args = BorderArgs{};
@@ -1283,7 +1473,7 @@ gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const d
 	}
 	bd.set = true;
 	bd.valuesSet = (n_cond == 0);
-	return GCMX_OK;
+	return prep_border(c);
 }
 
 gcmx_status gsx_set_border_values(gsx_ctx* c, const double* b) {
@@ -1316,7 +1506,7 @@ gcmx_status gsx_plain_correction(gsx_ctx* c) {
 	if (!bd.set || !bd.valuesSet) return fail(GCMX_ERR_STATE, "border plan / values not set");
 	if (c->matsSet) {  // fused with the first stage's beforeStage (the next call is stage 0)
 		hipLaunchKernelGGL(k_sx_begin, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->u, c->w,
-		                   c->mats, bd.n ? c->corrOf : nullptr, bd.cond, bd.S, c->N, bd.args);
+		                   c->mats, bd.n ? bd.nodeRec : nullptr, bd.S, c->N, bd.args);
 		c->wStage = 0;
 	} else if (bd.n) {
 		hipLaunchKernelGGL(k_sx_plain, dim3((bd.n + 63) / 64), dim3(64), 0, c->stream, bd.nodes,
@@ -1356,28 +1546,32 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 		                   c->mats + stage * 81, N);
 	c->wStage = -1;
 	if (l8)
-		hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + 255) / 256), blk, 0, c->stream, c->w,
+		hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
+		                   c->stream, c->w,
 		                   c->grad, c->gOff, c->gNb, c->coords, c->gW, c->gM, c->gDet, N);
 	else
 		hipLaunchKernelGGL(k_sx_gradient, grd, blk, 0, c->stream, c->w, c->grad, c->gOff, c->gNb,
 		                   c->coords, c->gW, c->gM, c->gDet, N);
 	if (st.nBorder) {
 		const BorderDevArgs bp = {c->corrOf, (bd.set && bd.n) ? bd.cond : nullptr, bd.B, bd.S,
-		                          bd.outer, bd.n};
+		                          bd.outer, bd.n, st.rec, st.recB, st.recMd};
 		if (l8) {
 #ifdef GCMX_SX_DIAG_TWICE  // tuning builds only: a second, warm-cache launch of the same kernel
 			for (int rep = 0; rep < 2; rep++)
 #endif
-			hipLaunchKernelGGL(k_sx_border_l8, dim3(((size_t)st.nBorder * kL + 255) / 256), blk, 0, c->stream,
+			hipLaunchKernelGGL(k_sx_border_l8, dim3(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block),
+			                   dim3(kL8Block), 0, c->stream,
 			                   st.border, st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w,
 			                   c->grad, c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
-			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N);
+			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, 0,
+			                   st.nBorder + st.nInner);
 		}
 		else  // border lists are short (a surface): 64-thread blocks spread them over the CUs
 			hipLaunchKernelGGL(k_sx_border, dim3((st.nBorder + 63) / 64), dim3(64), 0, c->stream, st.border,
 			                   st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
 			                   c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
-			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N);
+			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, 0,
+			                   st.nBorder + st.nInner);
 	}
 	SX_TRY(hipGetLastError());
 	return GCMX_OK;
@@ -1393,13 +1587,16 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 	const dim3 blk(256);
 	const StageDev& st = c->st[stage];
 	if (st.nInner && node_lanes(c) == kL)
-		hipLaunchKernelGGL(k_sx_inner_l8, dim3(((size_t)st.nInner * kL + 255) / 256), blk, 0, c->stream,
+		hipLaunchKernelGGL(k_sx_inner_l8, dim3(((size_t)st.nInner * kL + kL8Block - 1) / kL8Block),
+		                   dim3(kL8Block), 0, c->stream,
 		                   st.inner, st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
-		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N);
+		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N,
+		                   st.nBorder, st.nBorder + st.nInner);
 	else if (st.nInner)
 		hipLaunchKernelGGL(k_sx_inner, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
 		                   st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
-		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N);
+		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N,
+		                   st.nBorder, st.nBorder + st.nInner);
 	SX_TRY(hipGetLastError());
 	std::swap(c->u, c->un);
 	if (stage < 2) {

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/sxv
 cp gcm_amd/lib/libgcmx.so gcm_amd/lib/sxtune/base.so
-for d in base gcm_amd/lib/sxtune/*/; do
+for d in base $(ls -d gcm_amd/lib/sxtune/*/ 2>/dev/null); do
   name=$(basename "$d")
   if [ "$name" = base ]; then cp gcm_amd/lib/sxtune/base.so gcm_amd/lib/libgcmx.so; else cp "$d/libgcmx.so" gcm_amd/lib/libgcmx.so; fi
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sxv/$name -o run -- \
