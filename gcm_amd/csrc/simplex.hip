@@ -57,6 +57,7 @@ struct BorderDev {
 	double* md = nullptr;  // [entry][stage][side R, L][10]: B * Omega (3x3) and det, k_sx_border_prep
 	int2* nodeRec = nullptr;  // [node]: (plan entry, its condition) or (-1, 0)
 	BorderArgs args{};
+	BorderArgs* argsDev = nullptr;  // device copy of args (what the kernels read)
 	bool set = false, valuesSet = false;
 	double lastValues[3 * GSX_MAX_BORDER_CONDITIONS] = {};  // what bvals holds once valuesSet
 };
@@ -93,6 +94,7 @@ struct gsx_ctx {
 	std::vector<double> hostCoords;  // [n][3]
 	double *coords = nullptr, *u = nullptr, *un = nullptr, *w = nullptr, *wn = nullptr,
 	       *grad = nullptr;
+	double* arena = nullptr;  // one allocation holding u, un, w, wn, grad, wnext
 	double* mats = nullptr;  // [2][3][81]: U then U1
 	bool matsSet = false;
 	int nodeLanes = 0;  // gsx_set_node_lanes: 0 auto, 1, 8
@@ -324,7 +326,7 @@ __device__ __forceinline__ void node_invariants(int n, int pos, int P, const int
 			const int ps = r == 0 ? vs[0] : (r == 1 ? vs[1] : vs[2]);
 			const double* src = (kind == GSX_FOOT_CELL) ? w + (size_t)p * kM + k
 			                    : (sl < 3)              ? w + (size_t)ps * kM + k
-			                                            : wn + (size_t)k * N + ps;
+			                                            : wn + (size_t)ps * kM + k;
 			v[i] = *src;
 			// TetrahedronInterpolator::hybridInterpolate (hpp:93-104) terms
 			const double d0 = q0 - coords[3 * (size_t)p + 0];
@@ -553,9 +555,10 @@ __global__ __launch_bounds__(64) void k_sx_border(
     const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
     const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
-    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, BorderArgs args,
+    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, const BorderArgs* __restrict__ argp,
     const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
+	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
 	__shared__ SharedMats<3> sm;
 	stage_mats<3>(sm, {U, U1, Unext});
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -569,7 +572,7 @@ __global__ __launch_bounds__(64) void k_sx_border(
 			border_correct(out, ci, bp.cond, bp.B, bp.S, bp.outer, bp.count, sm.m[0], sm.m[1], stage, args);
 	}
 #pragma unroll
-	for (int k = 0; k < kM; k++) wn[k * N + n] = out[k];
+	for (int k = 0; k < kM; k++) wn[(size_t)n * kM + k] = out[k];
 	if (!deferred[n]) finalize(n, out, sm.m[1], Unext ? sm.m[2] : nullptr, un, wnext, N);
 }
 
@@ -704,7 +707,7 @@ __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const
 		const int ps = r == 0 ? vs[0] : (r == 1 ? vs[1] : vs[2]);
 		const double* src = (kind == GSX_FOOT_CELL) ? w + (size_t)p * kM + k
 		                    : (sl < 3)              ? w + (size_t)ps * kM + k
-		                                            : wn + (size_t)k * N + ps;
+		                                            : wn + (size_t)ps * kM + k;
 		v[i] = *src;
 		const double d0 = q0 - coords[3 * (size_t)p + 0];
 		const double d1 = q1 - coords[3 * (size_t)p + 1];
@@ -766,24 +769,33 @@ __device__ __forceinline__ void rows_mat_vec(const double* __restrict__ Mx, cons
 }
 
 // finalize() split over the group: lane c writes component c, lane 0 also 8.
+// Every store comes after the node's last load: on gfx950 loads and stores share
+// vmcnt, so a load issued after a store waits for the store's completion (measured:
+// a border launch at 16^3 spent 7 of its 12 us that way).  `wrec`: the border
+// kernel's corrected invariants wv, stored node-major when `store_w`.
 __device__ __forceinline__ void group_finalize(int n, int c, bool store, const double (&wv)[kM],
                                                const double* __restrict__ U1,
                                                const double* __restrict__ Unext, double* __restrict__ un,
-                                               double* __restrict__ wnext, int N) {
+                                               double* __restrict__ wnext, int N,
+                                               double* __restrict__ wrec = nullptr, bool store_w = false) {
 	double uc, u8;
 	rows_mat_vec(U1, wv, c, uc, u8);
-	if (store) {
-		un[(size_t)c * N + n] = uc;
-		if (c == 0) un[(size_t)8 * N + n] = u8;
-	}
+	double wc = 0.0, w8 = 0.0;
 	if (Unext) {
 		double u[kM];
 #pragma unroll
 		for (int j = 0; j < kL; j++) u[j] = __shfl(uc, j, kL);
 		u[8] = u8;
-		double wc, w8;
 		rows_mat_vec(Unext, u, c, wc, w8);
-		if (store) {
+	}
+	if (store_w) {
+		wrec[(size_t)n * kM + c] = pick9(wv, c);
+		if (c == 0) wrec[(size_t)n * kM + 8] = wv[8];
+	}
+	if (store) {
+		un[(size_t)c * N + n] = uc;
+		if (c == 0) un[(size_t)8 * N + n] = u8;
+		if (Unext) {
 			wnext[(size_t)n * kM + c] = wc;
 			if (c == 0) wnext[(size_t)n * kM + 8] = w8;
 		}
@@ -837,9 +849,10 @@ __global__ __launch_bounds__(256) void k_sx_border_rec(const int* __restrict__ b
                                                        const signed char* __restrict__ outer, int count,
                                                        const double* __restrict__ Bm,
                                                        const double* __restrict__ md, int stage,
-                                                       BorderArgs args, int4* __restrict__ rec,
+                                                       const BorderArgs* __restrict__ argp, int4* __restrict__ rec,
                                                        double* __restrict__ recB,
                                                        double* __restrict__ recMd) {
+	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= nb) return;
 	const int ci = corrOf[border[t]];
@@ -948,9 +961,10 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
     const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
     const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
-    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, BorderArgs args,
+    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, const BorderArgs* __restrict__ argp,
     const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
+	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
 #ifndef GCMX_SX_L8_STAGE  // tuning: stage U / U1 / U_next in LDS (1) or read them through the caches (0)
 #define GCMX_SX_L8_STAGE 0
 #endif
@@ -990,13 +1004,8 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
 #ifndef GCMX_SX_DIAG_NOCORR  // tuning builds only: time the kernel without the correctors
 	if (ci >= 0) border_correct_l8(o, ci, c, cnd, code, rc.w, Brow, Md, bp.S, Us, U1s, stage, args);
 #endif
-	if (store) {
-		wn[(size_t)c * N + n] = pick9(o, c);
-		if (c == 0) wn[(size_t)8 * N + n] = o[8];
-	}
-#ifndef GCMX_SX_DIAG_NOFIN
-	group_finalize(n, c, store && !deferred[n], o, U1s, Uns, un, wnext, N);
-#endif
+	// wn (node-major, like wnext) is stored with the finalisation's stores, after every load
+	group_finalize(n, c, store && !deferred[n], o, U1s, Uns, un, wnext, N, wn, store);
 }
 
 // The step's border values b(t) into device memory (gsx_set_border_values).
@@ -1013,7 +1022,8 @@ __global__ __launch_bounds__(64) void k_sx_set_border_values(double* __restrict_
 __global__ __launch_bounds__(64) void k_sx_plain(const int* __restrict__ nodes,
                                                   const int* __restrict__ cond,
                                                   const double* __restrict__ Sm, double* u_,
-                                                  int count, int N, BorderArgs args) {
+                                                  int count, int N, const BorderArgs* __restrict__ argp) {
+	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
 	const int t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= count) return;
 	const int n = nodes[t], c = cond[t];
@@ -1030,7 +1040,8 @@ __global__ __launch_bounds__(64) void k_sx_plain(const int* __restrict__ nodes,
 __global__ __launch_bounds__(256) void k_sx_begin(double* u_, double* __restrict__ w,
                                                   const double* __restrict__ U0,
                                                   const int2* __restrict__ nodeRec,
-                                                  const double* __restrict__ Sm, int N, BorderArgs args) {
+                                                  const double* __restrict__ Sm, int N, const BorderArgs* __restrict__ argp) {
+	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
 	if (n >= N) return;
 	double u[kM];
@@ -1076,8 +1087,8 @@ __global__ __launch_bounds__(64) void k_sx_contact(
 	const int R[3] = {1, 3, 5}, L[3] = {0, 2, 4};  // Model.cpp:81-82
 	double wA[kM], wB[kM], uA[kM], uB[kM];
 	for (int k = 0; k < kM; k++) {
-		wA[k] = wnA[k * NA + a];
-		wB[k] = wnB[k * NB + b];
+		wA[k] = wnA[(size_t)a * kM + k];
+		wB[k] = wnB[(size_t)b * kM + k];
 	}
 	auto zero = [&](double (&w)[kM], int code) {
 		if (!(code & 4)) return;
@@ -1136,8 +1147,8 @@ __global__ __launch_bounds__(64) void k_sx_contact(
 	mat_vec(UA, uA, wA);
 	mat_vec(UB, uB, wB);
 	for (int k = 0; k < kM; k++) {
-		wnA[k * NA + a] = wA[k];
-		wnB[k * NB + b] = wB[k];
+		wnA[(size_t)a * kM + k] = wA[k];
+		wnB[(size_t)b * kM + k] = wB[k];
 	}
 	finalize(a, wA, U1A, UnextA, unA, wnextA, NA);
 	finalize(b, wB, U1B, UnextB, unB, wnextB, NB);
@@ -1202,7 +1213,7 @@ gcmx_status prep_border(gsx_ctx* c) {
 		}
 		hipLaunchKernelGGL(k_sx_border_rec, dim3((st.nBorder + 255) / 256), dim3(256), 0, c->stream,
 		                   st.border, st.nBorder, c->corrOf, bd.cond, bd.outer, bd.n, bd.B, bd.md, s,
-		                   bd.args, st.rec, st.recB, st.recMd);
+		                   bd.argsDev, st.rec, st.recB, st.recMd);
 		SX_TRY(hipGetLastError());
 	}
 	return GCMX_OK;
@@ -1242,15 +1253,19 @@ gcmx_status gsx_create(int device, int n_nodes, const double* coords, gsx_ctx** 
 	c->hostCoords.assign(coords, coords + 3 * N);
 	gcmx_status s = upload(&c->coords, coords, 3 * N);  // node-major [n][3]
 	if (s) { gsx_destroy(c); return s; }
+	// The per-step node arrays live in one allocation (2 MiB-aligned pieces of one
+	// range): the node kernels of a small mesh touch all of them every stage, and
+	// a few large pages keep their address translations resident.
 	double** bufs[6] = {&c->u, &c->un, &c->w, &c->wn, &c->grad, &c->wnext};
 	const size_t sizes[6] = {kM * N, kM * N, kM * N, kM * N, 3 * 6 * N, kM * N};
-	for (int i = 0; i < 6; i++) {
-		if (hipMalloc(bufs[i], sizes[i] * sizeof(double)) != hipSuccess ||
-		    hipMemset(*bufs[i], 0, sizes[i] * sizeof(double)) != hipSuccess) {
-			gsx_destroy(c);
-			return fail(GCMX_ERR_OOM, "simplex layer allocation failed");
-		}
+	size_t total = 0;
+	for (int i = 0; i < 6; i++) total += (sizes[i] + 31) / 32 * 32;  // 256-byte aligned pieces
+	if (hipMalloc(&c->arena, total * sizeof(double)) != hipSuccess ||
+	    hipMemset(c->arena, 0, total * sizeof(double)) != hipSuccess) {
+		gsx_destroy(c);
+		return fail(GCMX_ERR_OOM, "simplex layer allocation failed");
 	}
+	for (size_t i = 0, o = 0; i < 6; o += (sizes[i] + 31) / 32 * 32, i++) *bufs[i] = c->arena + o;
 	c->hostDeferred.assign(N, 0);
 	if ((s = upload(&c->deferred, c->hostDeferred.data(), N))) {
 		gsx_destroy(c);
@@ -1271,12 +1286,13 @@ void gsx_destroy(gsx_ctx* c) {
 	if (c->stream) (void)hipStreamSynchronize(c->stream);
 	c->graphs.reset();
 	if (c->bvals) (void)hipFree(c->bvals);
-	void* ptrs[] = {c->coords, c->u, c->un, c->w, c->wn, c->grad, c->wnext, c->corrOf, c->deferred,
+	void* ptrs[] = {c->coords, c->arena, c->corrOf, c->deferred,
 	                c->mats, c->gOff, c->gNb,
 	                c->gRows, c->gW, c->gM, c->gDet};
 	for (void* p : ptrs)
 		if (p) (void)hipFree(p);
-	void* bptrs[] = {c->bd.nodes, c->bd.cond, c->bd.B, c->bd.S, c->bd.outer, c->bd.md, c->bd.nodeRec};
+	void* bptrs[] = {c->bd.nodes, c->bd.cond, c->bd.B, c->bd.S, c->bd.outer, c->bd.md, c->bd.nodeRec,
+	                 c->bd.argsDev};
 	for (void* p : bptrs)
 		if (p) (void)hipFree(p);
 	for (auto& st : c->st) {
@@ -1471,6 +1487,7 @@ gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const d
 		bd.args.type[i] = type[i];
 		for (int st = 0; st < 3; st++) bd.args.minDet[i][st] = min_det[i * 3 + st];
 	}
+	if ((s = upload(&bd.argsDev, &bd.args, 1))) return s;
 	bd.set = true;
 	bd.valuesSet = (n_cond == 0);
 	return prep_border(c);
@@ -1506,11 +1523,11 @@ gcmx_status gsx_plain_correction(gsx_ctx* c) {
 	if (!bd.set || !bd.valuesSet) return fail(GCMX_ERR_STATE, "border plan / values not set");
 	if (c->matsSet) {  // fused with the first stage's beforeStage (the next call is stage 0)
 		hipLaunchKernelGGL(k_sx_begin, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->u, c->w,
-		                   c->mats, bd.n ? bd.nodeRec : nullptr, bd.S, c->N, bd.args);
+		                   c->mats, bd.n ? bd.nodeRec : nullptr, bd.S, c->N, bd.argsDev);
 		c->wStage = 0;
 	} else if (bd.n) {
 		hipLaunchKernelGGL(k_sx_plain, dim3((bd.n + 63) / 64), dim3(64), 0, c->stream, bd.nodes,
-		                   bd.cond, bd.S, c->u, bd.n, c->N, bd.args);
+		                   bd.cond, bd.S, c->u, bd.n, c->N, bd.argsDev);
 		c->wStage = -1;
 	}
 	SX_TRY(hipGetLastError());
@@ -1559,17 +1576,25 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 #ifdef GCMX_SX_DIAG_TWICE  // tuning builds only: a second, warm-cache launch of the same kernel
 			for (int rep = 0; rep < 2; rep++)
 #endif
+#ifdef GCMX_SX_DIAG_ASINNER  // tuning builds only: time the inner kernel over the border list
+			if (true)
+				hipLaunchKernelGGL(k_sx_inner_l8, dim3(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block),
+			                   dim3(kL8Block), 0, c->stream, st.border, st.nBorder, st.fv, st.flam, st.fmeta,
+			                   st.shift, c->coords, c->w, c->grad, c->wn, c->mats + 3 * 81 + stage * 81,
+			                   nextU(c, stage), c->un, c->wnext, N, 0, st.nBorder + st.nInner);
+			else
+#endif
 			hipLaunchKernelGGL(k_sx_border_l8, dim3(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block),
 			                   dim3(kL8Block), 0, c->stream,
 			                   st.border, st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w,
-			                   c->grad, c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
+			                   c->grad, c->wn, c->deferred, bp, bd.argsDev, c->mats + stage * 81,
 			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, 0,
 			                   st.nBorder + st.nInner);
 		}
 		else  // border lists are short (a surface): 64-thread blocks spread them over the CUs
 			hipLaunchKernelGGL(k_sx_border, dim3((st.nBorder + 63) / 64), dim3(64), 0, c->stream, st.border,
 			                   st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
-			                   c->wn, c->deferred, bp, bd.args, c->mats + stage * 81,
+			                   c->wn, c->deferred, bp, bd.argsDev, c->mats + stage * 81,
 			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, 0,
 			                   st.nBorder + st.nInner);
 	}
