@@ -524,7 +524,7 @@ struct BorderDevArgs {  // the border plan's device arrays (null cond = no plan)
 	const int *corrOf, *cond;
 	const double *B, *S;
 	const signed char* outer;
-	int count;
+	int count, ncond;
 	const int4* rec;  // the stage's corrector records by list position (eight-lane kernel)
 	const double *recB, *recMd;
 };
@@ -768,25 +768,51 @@ __device__ __forceinline__ void rows_mat_vec(const double* __restrict__ Mx, cons
 	r8 = t;
 }
 
+// Rows c and 8 of a 9 x 9 matrix in registers, loaded at the kernel start: a
+// matrix entry read where it is used costs one more memory round trip on the
+// node's dependent chain (the eight-lane kernels run a few waves per CU, so
+// nothing hides it).  rows_mv is rows_mat_vec's arithmetic.
+struct Rows2 {
+	double rc[kM], r8[kM];
+};
+__device__ __forceinline__ void load_rows(Rows2& R, const double* __restrict__ Mx, int c) {
+#pragma unroll
+	for (int j = 0; j < kM; j++) {
+		R.rc[j] = Mx[c * kM + j];
+		R.r8[j] = Mx[8 * kM + j];
+	}
+}
+__device__ __forceinline__ void rows_mv(const Rows2& R, const double (&in)[kM], double& rc, double& r8) {
+	double s = R.rc[0] * in[0];
+#pragma unroll
+	for (int j = 1; j < kM; j++) s += R.rc[j] * in[j];
+	rc = s;
+	double t = R.r8[0] * in[0];
+#pragma unroll
+	for (int j = 1; j < kM; j++) t += R.r8[j] * in[j];
+	r8 = t;
+}
+
 // finalize() split over the group: lane c writes component c, lane 0 also 8.
 // Every store comes after the node's last load: on gfx950 loads and stores share
 // vmcnt, so a load issued after a store waits for the store's completion (measured:
 // a border launch at 16^3 spent 7 of its 12 us that way).  `wrec`: the border
 // kernel's corrected invariants wv, stored node-major when `store_w`.
+// R1, Rn: rows c and 8 of U1_s and U_{s+1} (has_next: there is a next stage).
 __device__ __forceinline__ void group_finalize(int n, int c, bool store, const double (&wv)[kM],
-                                               const double* __restrict__ U1,
-                                               const double* __restrict__ Unext, double* __restrict__ un,
-                                               double* __restrict__ wnext, int N,
+                                               const Rows2& R1, const Rows2& Rn, bool has_next,
+                                               double* __restrict__ un, double* __restrict__ wnext, int N,
                                                double* __restrict__ wrec = nullptr, bool store_w = false) {
 	double uc, u8;
-	rows_mat_vec(U1, wv, c, uc, u8);
+	rows_mv(R1, wv, uc, u8);
 	double wc = 0.0, w8 = 0.0;
+	const bool Unext = has_next;
 	if (Unext) {
 		double u[kM];
 #pragma unroll
 		for (int j = 0; j < kL; j++) u[j] = __shfl(uc, j, kL);
 		u[8] = u8;
-		rows_mat_vec(Unext, u, c, wc, w8);
+		rows_mv(Rn, u, wc, w8);
 	}
 	if (store_w) {
 		wrec[(size_t)n * kM + c] = pick9(wv, c);
@@ -813,9 +839,12 @@ __global__ __launch_bounds__(256) void k_sx_inner_l8(
 	// whole groups stay active for the shuffles; a group past the list redoes the last node, unstored
 	const bool store = t < count;
 	const int n = nodes[store ? t : count - 1];
+	Rows2 R1, Rn;
+	load_rows(R1, U1, c);
+	if (Unext) load_rows(Rn, Unext, c);
 	double o[kM];
 	group_invariants(n, c, pos0 + (store ? t : count - 1), P, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
-	group_finalize(n, c, store, o, U1, Unext, un, wnext, N);
+	group_finalize(n, c, store, o, R1, Rn, Unext != nullptr, un, wnext, N);
 }
 
 // The matrix part of calculateOuterWaveCorrection for every border-plan entry t,
@@ -864,7 +893,7 @@ __global__ __launch_bounds__(256) void k_sx_border_rec(const int* __restrict__ b
 	const double* m = md + ((size_t)ci * 3 + stage) * 20;
 	const double minValid = args.minDet[cnd][stage];
 	const int okR = fabs(m[9]) > minValid, okL = fabs(m[19]) > minValid;
-	rec[t] = make_int4(ci, cnd, outer[(size_t)stage * count + ci], okR | (okL << 1));
+	rec[t] = make_int4(ci, cnd, outer[(size_t)stage * count + ci], okR | (okL << 1) | (args.type[cnd] << 8));
 	for (int i = 0; i < 27; i++) recB[(size_t)t * 27 + i] = Bm[27 * (size_t)ci + i];
 	for (int i = 0; i < 20; i++) recMd[(size_t)t * 20 + i] = m[i];
 }
@@ -883,15 +912,12 @@ __device__ __forceinline__ double pick3(const double (&v)[3], int i) {
 // border_correct's operations in its order.  Returns the node's corrected invariants in every lane of the group.
 __device__ __forceinline__ void border_correct_l8(double (&w)[kM], int t, int c, int cnd, int code,
                                                   int okRL, const double (&Brow)[kM],
-                                                  const double (&Md)[10],
-                                                  const double* __restrict__ Sm,
-                                                  const double* __restrict__ U,
-                                                  const double* __restrict__ U1, int stage,
-                                                  const BorderArgs& args) {
-	const double b[3] = {args.b[3 * cnd], args.b[3 * cnd + 1], args.b[3 * cnd + 2]};
+                                                  const double (&Md)[10], const double (&Sv)[9],
+                                                  const Rows2& RU, const Rows2& RU1,
+                                                  const double (&cv)[3][3], const double (&b)[3]) {
 	const int h = c >> 2, q = c & 3;
 	double u[kM], uc, u8;
-	rows_mat_vec(U1, w, c, uc, u8);  // u = U1 w (mat_vec), rows c and 8 here
+	rows_mv(RU1, w, uc, u8);  // u = U1 w (mat_vec), rows c and 8 here
 #pragma unroll
 	for (int j = 0; j < kL; j++) u[j] = __shfl(uc, j, kL);
 	u[8] = u8;
@@ -909,14 +935,15 @@ __device__ __forceinline__ void border_correct_l8(double (&w)[kM], int t, int c,
 	const double d2 = det3(Md[0], r[0], Md[2], Md[3], r[1], Md[5], Md[6], r[2], Md[8]);
 	const double d3 = det3(Md[0], Md[1], r[0], Md[3], Md[4], r[1], Md[6], Md[7], r[2]);
 	const double alpha[3] = {d1 / det, d2 / det, d3 / det};
-	const int c0 = 1 - h;  // this side's columns c0, c0 + 2, c0 + 4
-	auto value = [&](int i) {
-		double x = U1[i * kM + c0] * alpha[0];
-		x += U1[i * kM + c0 + 2] * alpha[1];
-		x += U1[i * kM + c0 + 4] * alpha[2];
+	// cv[r][j] = U1(row, c0 + 2 j) for rows q, q + 4, 8, with c0 = 1 - h: this
+	// side's columns (R: 1, 3, 5; L: 0, 2, 4)
+	auto value = [&](int r) {
+		double x = cv[r][0] * alpha[0];
+		x += cv[r][1] * alpha[1];
+		x += cv[r][2] * alpha[2];
 		return x;
 	};
-	const double vq = value(q), vq4 = value(q + 4), v8 = value(8);
+	const double vq = value(0), vq4 = value(1), v8 = value(2);
 	// this side's value of the own component c, the other side's from the partner c ^ 4
 	const double mine = h ? vq4 : vq;
 	const double other = __shfl_xor(h ? vq : vq4, 4, kL);
@@ -943,7 +970,7 @@ __device__ __forceinline__ void border_correct_l8(double (&w)[kM], int t, int c,
 	double up[kM];  // the plain correction: per node, so the whole group takes it
 #pragma unroll
 	for (int j = 0; j < kM; j++) up[j] = u[j];
-	if (plain) plain_correction(up, args.type[cnd], Sm + 9 * (size_t)t, b);
+	if (plain) plain_correction(up, okRL >> 8, Sv, b);
 #pragma unroll
 	for (int j = 0; j < kL; j++) {
 		const double sj = __shfl(uc, j, kL);
@@ -951,7 +978,7 @@ __device__ __forceinline__ void border_correct_l8(double (&w)[kM], int t, int c,
 	}
 	u[8] = plain ? up[8] : u8;
 	double wc, w8;  // w = U u (mat_vec), rows c and 8 here
-	rows_mat_vec(U, u, c, wc, w8);
+	rows_mv(RU, u, wc, w8);
 #pragma unroll
 	for (int j = 0; j < kL; j++) w[j] = __shfl(wc, j, kL);
 	w[8] = w8;
@@ -989,23 +1016,38 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
 	const int tr = store ? t : count - 1;
 	const int4 rc = bp.cond ? bp.rec[tr] : make_int4(-1, 0, 0, 0);
 	const int ci = rc.x, cnd = rc.y, code = rc.z;
-	double Brow[kM], Md[10];
+	double Brow[kM], Md[10], cv[3][3], Sv[9], bv[3] = {0.0, 0.0, 0.0};
+	Rows2 RU, RU1, Rn;  // every matrix entry the node needs, loaded up front
+	load_rows(RU1, U1s, c);
+	if (Uns) load_rows(Rn, Uns, c);
+	const bool fin = store && !deferred[n];
 	if (ci >= 0) {
-		const int q = c & 3;
+		const int q = c & 3, h = c >> 2;
 		const double* Bi = bp.recB + 27 * (size_t)tr + kM * (q < 3 ? q : 2);
 #pragma unroll
 		for (int i = 0; i < kM; i++) Brow[i] = Bi[i];
-		const double* m = bp.recMd + (size_t)tr * 20 + (c >> 2) * 10;
+		const double* m = bp.recMd + (size_t)tr * 20 + h * 10;
 #pragma unroll
 		for (int i = 0; i < 10; i++) Md[i] = m[i];
+		load_rows(RU, Us, c);
+		const double* Si = bp.S + 9 * (size_t)ci;
+#pragma unroll
+		for (int i = 0; i < 9; i++) Sv[i] = Si[i];
+#pragma unroll
+		for (int i = 0; i < 3; i++) bv[i] = args.b[3 * cnd + i];  // the step's b(t) of the condition
+		const int rows[3] = {q, q + 4, 8};
+#pragma unroll
+		for (int r = 0; r < 3; r++)
+#pragma unroll
+			for (int j = 0; j < 3; j++) cv[r][j] = U1s[rows[r] * kM + (1 - h) + 2 * j];
 	}
 	double o[kM];
 	group_invariants(n, c, pos0 + tr, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
 #ifndef GCMX_SX_DIAG_NOCORR  // tuning builds only: time the kernel without the correctors
-	if (ci >= 0) border_correct_l8(o, ci, c, cnd, code, rc.w, Brow, Md, bp.S, Us, U1s, stage, args);
+	if (ci >= 0) border_correct_l8(o, ci, c, cnd, code, rc.w, Brow, Md, Sv, RU, RU1, cv, bv);
 #endif
 	// wn (node-major, like wnext) is stored with the finalisation's stores, after every load
-	group_finalize(n, c, store && !deferred[n], o, U1s, Uns, un, wnext, N, wn, store);
+	group_finalize(n, c, fin, o, RU1, Rn, Uns != nullptr, un, wnext, N, wn, store);
 }
 
 // The step's border values b(t) into device memory (gsx_set_border_values).
@@ -1571,7 +1613,7 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 		                   c->coords, c->gW, c->gM, c->gDet, N);
 	if (st.nBorder) {
 		const BorderDevArgs bp = {c->corrOf, (bd.set && bd.n) ? bd.cond : nullptr, bd.B, bd.S,
-		                          bd.outer, bd.n, st.rec, st.recB, st.recMd};
+		                          bd.outer, bd.n, bd.nCond, st.rec, st.recB, st.recMd};
 		if (l8) {
 #ifdef GCMX_SX_DIAG_TWICE  // tuning builds only: a second, warm-cache launch of the same kernel
 			for (int rep = 0; rep < 2; rep++)

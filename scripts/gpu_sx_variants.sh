@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/sxv
-cp gcm_amd/lib/libgcmx.so gcm_amd/lib/sxtune/base.so
+mkdir -p gcm_amd/lib/sxtune && cp gcm_amd/lib/libgcmx.so gcm_amd/lib/sxtune/base.so
 for d in base $(ls -d gcm_amd/lib/sxtune/*/ 2>/dev/null); do
   name=$(basename "$d")
   if [ "$name" = base ]; then cp gcm_amd/lib/sxtune/base.so gcm_amd/lib/libgcmx.so; else cp "$d/libgcmx.so" gcm_amd/lib/libgcmx.so; fi
