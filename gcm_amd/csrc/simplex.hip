@@ -110,6 +110,7 @@ struct gsx_ctx {
 	std::vector<char> hostDeferred;
 	double* bvals = nullptr;             // [GSX_MAX_BORDER_CONDITIONS][3] border values b(t)
 	std::unique_ptr<struct StepGraphs> graphs;  // gsx_step's replayed steps (this ctx leads)
+	unsigned planGen = 0;  // bumped by every call that (re)sets device plan data graphs point into
 };
 
 // The host-side state a simplex step changes (pointer swaps, chaining flag).
@@ -133,6 +134,7 @@ static void set_body_state(gsx_ctx* c, const BodyState& b) {
 struct StepGraphs {
 	std::vector<gsx_ctx*> bodies;
 	std::vector<gsx_contact*> contacts;
+	std::vector<unsigned> gens;  // the bodies' planGen at capture
 	struct Entry {
 		std::vector<BodyState> before, after;
 		hipGraph_t graph = nullptr;
@@ -1354,6 +1356,7 @@ void gsx_destroy(gsx_ctx* c) {
 gcmx_status gsx_set_matrices(gsx_ctx* c, const double* U, const double* U1) {
 	gcmx_status s = check(c);
 	if (s) return s;
+	c->planGen++;  // captured step graphs point into what this call replaces
 	if (!U || !U1) return fail(GCMX_ERR_INVALID_ARG, "null matrices");
 	std::vector<double> m(2 * 3 * 81);
 	std::memcpy(m.data(), U, 3 * 81 * sizeof(double));
@@ -1370,6 +1373,7 @@ gcmx_status gsx_set_gradient_plan(gsx_ctx* c, const int* off, const int* nbs, co
                                   const double* wts, const double* M, const double* det) {
 	gcmx_status s = check(c);
 	if (s) return s;
+	c->planGen++;  // captured step graphs point into what this call replaces
 	if (!off || !nbs || !rows || !wts || !M || !det)
 		return fail(GCMX_ERR_INVALID_ARG, "null gradient plan");
 	const int N = c->N, E = off[N];
@@ -1400,6 +1404,7 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
                                int nb, const int* border, int ni, const int* inner) {
 	gcmx_status s = check(c);
 	if (s) return s;
+	c->planGen++;  // captured step graphs point into what this call replaces
 	if (stage < 0 || stage > 2 || !feet || !shift || nb < 0 || ni < 0 || (nb && !border) ||
 	    (ni && !inner))
 		return fail(GCMX_ERR_INVALID_ARG, "bad stage plan");
@@ -1491,6 +1496,7 @@ gcmx_status gsx_set_border_plan(gsx_ctx* c, int n_cond, const int* type, const d
                                 const double* S, const signed char* outer) {
 	gcmx_status s = check(c);
 	if (s) return s;
+	c->planGen++;  // captured step graphs point into what this call replaces
 	if (n_cond < 0 || n_cond > GSX_MAX_BORDER_CONDITIONS || n < 0 || (n_cond && (!type || !min_det)) ||
 	    (n && (!nodes || !cond || !B || !S || !outer)))
 		return fail(GCMX_ERR_INVALID_ARG, "bad border plan");
@@ -1676,6 +1682,7 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 gcmx_status gsx_set_node_lanes(gsx_ctx* c, int lanes) {
 	gcmx_status s = check(c);
 	if (s) return s;
+	c->planGen++;  // captured step graphs point into what this call replaces
 	if (lanes != 0 && lanes != 1 && lanes != kL) return fail(GCMX_ERR_INVALID_ARG, "node lanes must be 0, 1 or 8");
 	c->nodeLanes = lanes;
 	return GCMX_OK;
@@ -1726,6 +1733,8 @@ gcmx_status gsx_contact_create(gsx_ctx* a, gsx_ctx* b, int n, const int* nodes_a
 		a->hostDeferred[(size_t)nodes_a[i]] = 1;
 		b->hostDeferred[(size_t)nodes_b[i]] = 1;
 	}
+	a->planGen++;  // the deferred flags are reallocated below
+	b->planGen++;
 	if ((s = upload(&a->deferred, a->hostDeferred.data(), a->hostDeferred.size())) ||
 	    (s = upload(&b->deferred, b->hostDeferred.data(), b->hostDeferred.size()))) {
 		gsx_contact_destroy(c);
@@ -1824,11 +1833,15 @@ gcmx_status gsx_step(gsx_ctx* const* bodies_, int n_bodies, gsx_contact* const* 
 		if (!k || !in) return fail(GCMX_ERR_INVALID_ARG, "contact of a body outside the group");
 	}
 	SX_TRY(hipSetDevice(lead->device));
-	if (!lead->graphs || lead->graphs->bodies != bodies || lead->graphs->contacts != contacts) {
+	std::vector<unsigned> gens;
+	for (gsx_ctx* b : bodies) gens.push_back(b->planGen);
+	if (!lead->graphs || lead->graphs->bodies != bodies || lead->graphs->contacts != contacts ||
+	    lead->graphs->gens != gens) {
 		lead->graphs.reset(new StepGraphs());
 		StepGraphs& g = *lead->graphs;
 		g.bodies = bodies;
 		g.contacts = contacts;
+		g.gens = gens;
 		g.evBody.assign(bodies.size(), nullptr);
 		SX_TRY(hipEventCreateWithFlags(&g.evFork, hipEventDisableTiming));
 		SX_TRY(hipEventCreateWithFlags(&g.evJoin, hipEventDisableTiming));
