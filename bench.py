@@ -42,6 +42,8 @@ def parse():
                    help="bound on each of the two CPU baseline samples")
     p.add_argument("--rows-per-block", type=int, default=0,
                    help="fused-step y rows per block (0 = the library's automatic choice)")
+    p.add_argument("--no-copy-ceiling", action="store_true",
+                   help="skip the flat-copy measurement reported beside the roofline")
     p.add_argument("--no-profile", action="store_true",
                    help="no hipEvent bracketing of the launches in the timed repetitions")
     return p.parse_args()
@@ -93,6 +95,37 @@ def cpu_baseline(seconds: float):
                       f"per step: {sn} steps in {en:.1f} s on {all_threads} OpenMP threads "
                       f"(the job's CPU share; os.cpu_count() = {os.cpu_count()}, affinity "
                       f"{host_threads()}); {s1} steps in {e1:.1f} s on 1 thread"}
+
+
+def copy_ceiling(torch, device, step_bytes, achieved_gbps):
+    """What this box's HBM gives a plain copy of the same bytes the step must
+    move (half read, half written): a flat device-to-device copy of
+    step_bytes / 2, timed after the step's repetitions (outside them), median of
+    5.  The step's `achieved` over this rate says how close the kernel is to the
+    memory system's practical limit on this box (MI355X_MICROARCH.md: ~79 % of
+    the 8 TB/s spec for a float4 copy; tools/copy_probe.hip measures the
+    product layout's own copy beside a flat one)."""
+    n = int(step_bytes // 2 // 8)
+    src = torch.empty(n, dtype=torch.float64, device=f"cuda:{device}")
+    dst = torch.empty_like(src)
+    src.fill_(1.0)
+    dst.copy_(src)
+    ms = []
+    for _ in range(5):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src)
+        e1.record()
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    del src, dst
+    torch.cuda.empty_cache()
+    t = sorted(ms)[len(ms) // 2]
+    gbps = step_bytes / (t * 1e-3) / 1e9
+    return {"GBps": round(gbps, 1), "frac_of_copy": round(achieved_gbps / gbps, 4),
+            "how": f"torch copy_ of {n * 8 / 1e9:.2f} GB fp64 (flat, device to device), "
+                   f"median of 5, bytes counted read + write"}
 
 
 def multi_gpu_parity(dist, world, rank, device, U, U1, L):
@@ -251,6 +284,13 @@ def main():
                                               (v["total_ms"] / max(1, v["launches"]) * 1e-3) /
                                               1e9, 1)}
                             for k, v in kernels.items()}}
+
+    if roof is not None and not a.no_copy_ceiling:
+        try:
+            roof["copy_ceiling"] = copy_ceiling(torch, device, dom["bytes_per_launch"],
+                                                roof["achieved"])
+        except Exception as e:  # reported context, never required
+            log(f"copy ceiling failed: {e}")
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

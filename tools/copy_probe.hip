@@ -1,0 +1,93 @@
+// copy_probe.hip -- tuning tool (not product code): is the product layout's
+// copy rate (9 component planes per layer, 516 x 516 planes of 544-double rows,
+// gcmx.hip) below a flat copy of the same bytes, and does the component plane
+// stride matter (HBM channel mapping of the 9 + 9 concurrent streams)?
+//   flat      : 9*512^3 doubles, contiguous, double2 per lane
+//   layout P  : 9 loads + 9 stores per node, one z row per 512-thread block,
+//               marching y, component plane stride = CS + P doubles
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/copy_probe tools/copy_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                           \
+	do {                                                                                \
+		hipError_t e = (x);                                                             \
+		if (e != hipSuccess) {                                                          \
+			std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                 \
+			std::exit(1);                                                               \
+		}                                                                               \
+	} while (0)
+
+constexpr int N = 512, BS = 2, ROW = 544, LEAD = 14;
+constexpr long long STY = ROW, STX = (long long)ROW * (N + 2 * BS);
+constexpr long long CS = ((STX * (N + 2 * BS)) + 63) / 64 * 64;
+constexpr long long ORIGIN = LEAD + BS + BS * STY + BS * STX;
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256) void k_flat(const d2* __restrict__ in, d2* __restrict__ out, long long n2) {
+	const long long stride = (long long)gridDim.x * blockDim.x;
+	for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride)
+		__builtin_nontemporal_store(in[i], out + i);
+}
+
+__global__ __launch_bounds__(512) void k_layout(const double* __restrict__ in, double* __restrict__ out,
+                                                long long cs, int chunk) {
+	const int z = threadIdx.x;
+	const int T_ = gridDim.x, b = blockIdx.x;
+	const int p = (T_ % 8 == 0) ? (b % 8) * (T_ / 8) + b / 8 : b;
+	const int x = p % N, yb = (p / N) * chunk;
+	const long long base = ORIGIN + x * STX + z;
+	for (int y = yb; y < yb + chunk; y++) {
+		const long long o = base + (long long)y * STY;
+		double v[9];
+#pragma unroll
+		for (int c = 0; c < 9; c++) v[c] = in[c * cs + o];
+#pragma unroll
+		for (int c = 0; c < 9; c++) __builtin_nontemporal_store(v[c], out + c * cs + o);
+	}
+}
+
+template <class F>
+float timeit(F launch) {
+	hipEvent_t a, b;
+	CK(hipEventCreate(&a));
+	CK(hipEventCreate(&b));
+	launch();
+	CK(hipDeviceSynchronize());
+	CK(hipEventRecord(a));
+	for (int r = 0; r < 10; r++) launch();
+	CK(hipEventRecord(b));
+	CK(hipEventSynchronize(b));
+	float ms = 0;
+	CK(hipEventElapsedTime(&ms, a, b));
+	return ms / 10;
+}
+
+int main() {
+	const double nodes = (double)N * N * N;
+	const long long maxcs = CS + 8192;
+	const size_t bytes = (size_t)9 * maxcs * sizeof(double);
+	double *in, *out;
+	CK(hipMalloc(&in, bytes));
+	CK(hipMalloc(&out, bytes));
+	CK(hipMemset(in, 0, bytes));
+	CK(hipMemset(out, 0, bytes));
+	const long long n2 = (long long)9 * N * N * N / 2;
+	for (int g : {2048, 8192, 32768}) {
+		float ms = timeit([&] { hipLaunchKernelGGL(k_flat, dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		std::printf("flat copy grid %6d: %.3f ms (%.0f GB/s)\n", g, ms, 144.0 * nodes / (ms * 1e6));
+	}
+	for (int chunk : {128, 32}) {
+		for (long long pad : {0LL, 16LL, 32LL, 48LL, 64LL, 96LL, 160LL, 256LL, 544LL, 1024LL, 2048LL, 4096LL}) {
+			const long long cs = CS + pad;
+			float ms = timeit([&] {
+				hipLaunchKernelGGL(k_layout, dim3((N / chunk) * N), dim3(512), 0, 0, in, out, cs, chunk);
+			});
+			std::printf("layout copy chunk %3d plane stride CS+%5lld (CS %% 4096 = %4lld doubles): %.3f ms (%.0f GB/s)\n",
+			            chunk, pad, cs % 4096, ms, 144.0 * nodes / (ms * 1e6));
+		}
+	}
+	return 0;
+}
