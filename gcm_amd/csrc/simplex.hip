@@ -17,6 +17,7 @@
 //                         (u_new = U1_s w_new, hpp:115-126) + next beforeStage; swap.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -80,6 +81,10 @@ struct StageDev {
 	int* inner = nullptr;
 	int nBorder = 0, nInner = 0;
 	bool set = false;
+	// every new-invariant (wn) read of an inner foot names a node of this stage's
+	// border list, and no border foot reads wn: the stage may run as one launch
+	// (k_sx_stage_l8) whose inner groups wait for exactly those border nodes
+	bool fusable = false;
 	// border corrector records by position t in `border` (k_sx_border_rec): plan
 	// entry, condition, outer code, which sides are solvable; B; B * Omega and det
 	int4* rec = nullptr;
@@ -111,6 +116,14 @@ struct gsx_ctx {
 	double* bvals = nullptr;             // [GSX_MAX_BORDER_CONDITIONS][3] border values b(t)
 	std::unique_ptr<struct StepGraphs> graphs;  // gsx_step's replayed steps (this ctx leads)
 	unsigned planGen = 0;  // bumped by every call that (re)sets device plan data graphs point into
+	// one-launch stages (gsx_stage, eight-lane layout): per-node "wn written in
+	// launch #epoch" flags [N], the finished-gradient-block counter, then one error
+	// word (a wait that timed out)
+	int* ready = nullptr;
+	int epoch = 0;
+	unsigned gTarget = 0;
+	int fuseMode = 1;  // gsx_set_stage_fusion: 0 never, 1 border + inner, 2 gradient + border + inner
+	bool lastFused = false;  // the last gsx_stage ran as one launch
 };
 
 // The host-side state a simplex step changes (pointer swaps, chaining flag).
@@ -611,16 +624,15 @@ constexpr int kL = 8;
 #define GCMX_SX_L8_BLOCK 256
 #endif
 constexpr int kL8Block = GCMX_SX_L8_BLOCK;
+// Largest one-launch stage (k_sx_stage_l8), in blocks: about two per CU.
+constexpr size_t kFuseMaxBlocks = 512;
 
-__global__ __launch_bounds__(256) void k_sx_gradient_l8(const double* __restrict__ w,
-                                                        double* __restrict__ grad,
-                                                        const int* __restrict__ off,
-                                                        const int* __restrict__ nbs,
-                                                        const double* __restrict__ coords,
-                                                        const double* __restrict__ wts,
-                                                        const double* __restrict__ Mm,
-                                                        const double* __restrict__ dets, int N) {
-	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+template <bool SC1>
+__device__ __forceinline__ void gradient_node_l8(int gid, const double* __restrict__ w, double* __restrict__ grad,
+                                                 const int* __restrict__ off, const int* __restrict__ nbs,
+                                                 const double* __restrict__ coords, const double* __restrict__ wts,
+                                                 const double* __restrict__ Mm, const double* __restrict__ dets,
+                                                 int N) {
 	const int n = gid / kL, c = gid % kL;
 	if (n >= N || c >= kG) return;  // no shuffles in this kernel
 	const int b0 = off[n], K = off[n + 1] - b0;
@@ -670,19 +682,116 @@ __global__ __launch_bounds__(256) void k_sx_gradient_l8(const double* __restrict
 	const double d2 = det3(M[0], y0, M[2], M[3], y1, M[5], M[6], y2, M[8]);
 	const double d3 = det3(M[0], M[1], y0, M[3], M[4], y1, M[6], M[7], y2);
 	double* g = grad + (size_t)n * 3 * kG;
-	g[0 * kG + c] = d1 / det;
-	g[1 * kG + c] = d2 / det;
-	g[2 * kG + c] = d3 / det;
+	if constexpr (SC1) {  // handed off inside the launch: write-through
+		__hip_atomic_store(g + 0 * kG + c, d1 / det, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		__hip_atomic_store(g + 1 * kG + c, d2 / det, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		__hip_atomic_store(g + 2 * kG + c, d3 / det, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	} else {
+		g[0 * kG + c] = d1 / det;
+		g[1 * kG + c] = d2 / det;
+		g[2 * kG + c] = d3 / det;
+	}
+}
+
+// SIGNAL: count the block once all its gradients are stored (k_sx_stage_l8).
+template <bool SIGNAL>
+__device__ __forceinline__ void gradient_l8(int gid, const double* __restrict__ w, double* __restrict__ grad,
+                                            const int* __restrict__ off, const int* __restrict__ nbs,
+                                            const double* __restrict__ coords, const double* __restrict__ wts,
+                                            const double* __restrict__ Mm, const double* __restrict__ dets, int N,
+                                            unsigned* __restrict__ gcount) {
+	gradient_node_l8<SIGNAL>(gid, w, grad, off, nbs, coords, wts, Mm, dets, N);
+	if constexpr (SIGNAL) {  // every storing wave drains its sc1 stores, then one lane counts the block
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		if (threadIdx.x == 0) __hip_atomic_fetch_add(gcount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+
+__global__ __launch_bounds__(256) void k_sx_gradient_l8(const double* __restrict__ w,
+                                                        double* __restrict__ grad,
+                                                        const int* __restrict__ off,
+                                                        const int* __restrict__ nbs,
+                                                        const double* __restrict__ coords,
+                                                        const double* __restrict__ wts,
+                                                        const double* __restrict__ Mm,
+                                                        const double* __restrict__ dets, int N) {
+	gradient_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, w, grad, off, nbs, coords, wts, Mm, dets, N, nullptr);
+}
+
+// A border node's new invariants (wn) are complete once its flag holds this
+// launch's epoch (k_sx_stage_l8).  Bounded: a wait that cannot end (a plan the
+// host check missed) sets the error word instead of hanging the device.
+struct StageWait {
+	int* ready;         // [N] border nodes' wn stored (== epoch)
+	unsigned* gcount;   // gradient blocks finished, monotonic
+	unsigned gtarget;   // gcount once this launch's gradient blocks are done
+	int epoch;
+	int* err;
+};
+// Hand-offs inside k_sx_stage_l8 (cdna_hip_programming.md Guideline 16, the
+// write-through form): every handed-off byte (gradients, wn) is stored sc1 by its
+// producer wave, which drains its stores (vmcnt(0)) before the flag / counter is
+// written by an atomic; every load of those bytes is an sc1 load (read_ready), so
+// the consumer needs no agent acquire (whose L1 invalidate costs ~1.7 us per wave),
+// only a wavefront-scope fence that keeps the compiler from moving the loads above
+// the poll.
+__device__ __forceinline__ void wait_flag(const StageWait& sw, const int* flags, int node) {
+	int polls = 0;
+	while (__hip_atomic_load(flags + node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sw.epoch) {
+		if (++polls > (1 << 20)) {
+			atomicOr(sw.err, 1);
+			break;
+		}
+		__builtin_amdgcn_s_sleep(2);
+	}
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// Every gradient of the launch is stored (one poll address for all).
+__device__ __forceinline__ void wait_gradients(const StageWait& sw) {
+	int polls = 0;
+	while ((int)(__hip_atomic_load(sw.gcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - sw.gtarget) < 0) {
+		if (++polls > (1 << 20)) {
+			atomicOr(sw.err, 2);
+			break;
+		}
+		__builtin_amdgcn_s_sleep(2);
+	}
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// A value another group of the same launch stored: a device-scope atomic (sc1)
+// load, never served by this CU's L1 and never hoisted above the wait (the
+// kernels' pointers are __restrict__ const, which lets plain loads be treated as
+// invariant).
+__device__ __forceinline__ double read_ready(const double* p) {
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// TetrahedronInterpolator::hybridInterpolate's (hpp:93-104) gradient term of vertex p
+// SHARED: the gradients were stored by other groups of this launch (read_ready).
+template <bool SHARED = false>
+__device__ __forceinline__ double grad_dot(const double* __restrict__ grad, int p, int k, const double (&d)[3]) {
+	const double* gp = grad + (size_t)p * 3 * kG;
+	double g[3];
+#pragma unroll
+	for (int r = 0; r < 3; r++) g[r] = SHARED ? read_ready(gp + r * kG + k) : gp[r * kG + k];
+	double dot = g[0] * d[0];
+	dot += g[1] * d[1];
+	dot += g[2] * d[2];
+	return dot;
 }
 
 // interpolateValuesAround for one invariant k (0..5) of node n (node_invariants' body).
+// WAIT: the foot's new-invariant reads wait for the border nodes' flags first.
+template <bool WAIT = false>
 __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const int4* __restrict__ fv,
                                              const double4* __restrict__ flam,
                                              const int* __restrict__ fmeta, const StageShift& sh,
                                              const double* __restrict__ coords,
                                              const double* __restrict__ w,
                                              const double* __restrict__ grad,
-                                             const double* __restrict__ wn, int N) {
+                                             const double* __restrict__ wn, int N,
+                                             const StageWait& sw = StageWait{nullptr, nullptr, 0u, 0, nullptr}) {
 	double s0 = sh.d[0][0], s1 = sh.d[0][1], s2 = sh.d[0][2];  // shift of invariant k (selects)
 #pragma unroll
 	for (int kk = 1; kk < 6; kk++)
@@ -700,7 +809,10 @@ __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const
 	const double lam[4] = {l.x, l.y, l.z, l.w};
 	const double q0 = coords[3 * (size_t)n + 0] + s0, q1 = coords[3 * (size_t)n + 1] + s1,
 	             q2 = coords[3 * (size_t)n + 2] + s2;
-	double v[4], term[4];
+	double v[4], term[4], dots[4], dd[4][3];
+	bool waits[4];
+	const double* wsrc[4];
+	int wnode[4];
 #pragma unroll
 	for (int i = 0; i < 4; i++) {
 		const int p = vs[i];
@@ -710,16 +822,33 @@ __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const
 		const double* src = (kind == GSX_FOOT_CELL) ? w + (size_t)p * kM + k
 		                    : (sl < 3)              ? w + (size_t)ps * kM + k
 		                                            : wn + (size_t)ps * kM + k;
-		v[i] = *src;
-		const double d0 = q0 - coords[3 * (size_t)p + 0];
-		const double d1 = q1 - coords[3 * (size_t)p + 1];
-		const double d2 = q2 - coords[3 * (size_t)p + 2];
-		const double* gp = grad + (size_t)p * 3 * kG;
-		double dot = gp[0 * kG + k] * d0;
-		dot += gp[1 * kG + k] * d1;
-		dot += gp[2 * kG + k] * d2;
-		term[i] = v[i] + dot / 2.0;
+		// WAIT: a new-invariant value is read after every other load of the foot
+		// has been issued (an acquiring poll orders the loads that follow it)
+		waits[i] = WAIT && kind == GSX_FOOT_SPACETIME && sl >= 3;
+		wsrc[i] = src;
+		wnode[i] = ps;
+		if (!waits[i]) v[i] = *src;
+		dd[i][0] = q0 - coords[3 * (size_t)p + 0];
+		dd[i][1] = q1 - coords[3 * (size_t)p + 1];
+		dd[i][2] = q2 - coords[3 * (size_t)p + 2];
+		if constexpr (!WAIT) dots[i] = grad_dot(grad, p, k, dd[i]);
 	}
+	if constexpr (WAIT) {
+		// only a CELL foot uses the gradients (a SPACETIME foot's terms are unused,
+		// hybridInterpolate is not called for it); they come from this launch's
+		// gradient groups, so every value above was requested first
+		if (kind == GSX_FOOT_CELL && sw.gcount) wait_gradients(sw);
+#pragma unroll
+		for (int i = 0; i < 4; i++) dots[i] = kind == GSX_FOOT_CELL ? grad_dot<true>(grad, vs[i], k, dd[i]) : 0.0;
+#pragma unroll
+		for (int i = 0; i < 4; i++)
+			if (waits[i]) {
+				wait_flag(sw, sw.ready, wnode[i]);
+				v[i] = read_ready(wsrc[i]);
+			}
+	}
+#pragma unroll
+	for (int i = 0; i < 4; i++) term[i] = v[i] + dots[i] / 2.0;
 	if (kind == GSX_FOOT_CELL) {
 		const double quadratic = lam[0] * term[0] + lam[1] * term[1] + lam[2] * term[2] + lam[3] * term[3];
 		const double mn = std_min(std_min(std_min(v[0], v[1]), v[2]), v[3]);
@@ -734,14 +863,16 @@ __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const
 
 // All 9 new invariants of node n in every lane of its group (lane c < 6 interpolates
 // invariant c, lanes 6, 7 read the exact hits 6, 7; every lane reads 8).
+template <bool WAIT = false>
 __device__ __forceinline__ void group_invariants(int n, int c, int pos, int P, const int4* __restrict__ fv,
                                                  const double4* __restrict__ flam,
                                                  const int* __restrict__ fmeta, const StageShift& sh,
                                                  const double* __restrict__ coords,
                                                  const double* __restrict__ w,
                                                  const double* __restrict__ grad,
-                                                 const double* __restrict__ wn, int N, double (&o)[kM]) {
-	const double mine = c < 6 ? foot_value(n, c, pos, P, fv, flam, fmeta, sh, coords, w, grad, wn, N)
+                                                 const double* __restrict__ wn, int N, double (&o)[kM],
+                                                 const StageWait& sw = StageWait{nullptr, nullptr, 0u, 0, nullptr}) {
+	const double mine = c < 6 ? foot_value<WAIT>(n, c, pos, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, sw)
 	                          : w[(size_t)n * kM + c];
 	const double w8 = w[(size_t)n * kM + 8];
 #pragma unroll
@@ -801,6 +932,7 @@ __device__ __forceinline__ void rows_mv(const Rows2& R, const double (&in)[kM], 
 // a border launch at 16^3 spent 7 of its 12 us that way).  `wrec`: the border
 // kernel's corrected invariants wv, stored node-major when `store_w`.
 // R1, Rn: rows c and 8 of U1_s and U_{s+1} (has_next: there is a next stage).
+template <bool SC1_W = false>  // wrec is handed off inside the launch: write-through stores
 __device__ __forceinline__ void group_finalize(int n, int c, bool store, const double (&wv)[kM],
                                                const Rows2& R1, const Rows2& Rn, bool has_next,
                                                double* __restrict__ un, double* __restrict__ wnext, int N,
@@ -816,7 +948,10 @@ __device__ __forceinline__ void group_finalize(int n, int c, bool store, const d
 		u[8] = u8;
 		rows_mv(Rn, u, wc, w8);
 	}
-	if (store_w) {
+	if (store_w && SC1_W) {
+		__hip_atomic_store(wrec + (size_t)n * kM + c, pick9(wv, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (c == 0) __hip_atomic_store(wrec + (size_t)n * kM + 8, wv[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	} else if (store_w) {
 		wrec[(size_t)n * kM + c] = pick9(wv, c);
 		if (c == 0) wrec[(size_t)n * kM + 8] = wv[8];
 	}
@@ -830,13 +965,15 @@ __device__ __forceinline__ void group_finalize(int n, int c, bool store, const d
 	}
 }
 
-__global__ __launch_bounds__(256) void k_sx_inner_l8(
-    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
-    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
-    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
-    const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
-    double* __restrict__ un, double* __restrict__ wnext, int N, int pos0, int P) {
-	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+template <bool WAIT>
+__device__ __forceinline__ void inner_l8(int gid, const int* __restrict__ nodes, int count,
+                                         const int4* __restrict__ fv, const double4* __restrict__ flam,
+                                         const int* __restrict__ fmeta, const StageShift& sh,
+                                         const double* __restrict__ coords, const double* __restrict__ w,
+                                         const double* __restrict__ grad, const double* __restrict__ wn,
+                                         const double* __restrict__ U1, const double* __restrict__ Unext,
+                                         double* __restrict__ un, double* __restrict__ wnext, int N, int pos0,
+                                         int P, const StageWait& sw) {
 	const int t = gid / kL, c = gid % kL;
 	// whole groups stay active for the shuffles; a group past the list redoes the last node, unstored
 	const bool store = t < count;
@@ -845,8 +982,19 @@ __global__ __launch_bounds__(256) void k_sx_inner_l8(
 	load_rows(R1, U1, c);
 	if (Unext) load_rows(Rn, Unext, c);
 	double o[kM];
-	group_invariants(n, c, pos0 + (store ? t : count - 1), P, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
+	group_invariants<WAIT>(n, c, pos0 + (store ? t : count - 1), P, fv, flam, fmeta, sh, coords, w, grad, wn,
+	                       N, o, sw);
 	group_finalize(n, c, store, o, R1, Rn, Unext != nullptr, un, wnext, N);
+}
+
+__global__ __launch_bounds__(256) void k_sx_inner_l8(
+    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
+    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
+    const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
+    double* __restrict__ un, double* __restrict__ wnext, int N, int pos0, int P) {
+	inner_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
+	                U1, Unext, un, wnext, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr});
 }
 
 // The matrix part of calculateOuterWaveCorrection for every border-plan entry t,
@@ -986,13 +1134,16 @@ __device__ __forceinline__ void border_correct_l8(double (&w)[kM], int t, int c,
 	w[8] = w8;
 }
 
-__global__ __launch_bounds__(256) void k_sx_border_l8(
-    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
-    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+// SIGNAL: publish each node's flag once its wn is stored (k_sx_stage_l8).
+template <bool SIGNAL>
+__device__ __forceinline__ void border_l8(
+    int gid, const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
+    const double4* __restrict__ flam, const int* __restrict__ fmeta, const StageShift& sh,
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
-    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, const BorderArgs* __restrict__ argp,
-    const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
-    double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
+    double* __restrict__ wn, const char* __restrict__ deferred, const BorderDevArgs& bp,
+    const BorderArgs* __restrict__ argp, const double* __restrict__ U, const double* __restrict__ U1,
+    const double* __restrict__ Unext, double* __restrict__ un, double* __restrict__ wnext, int stage, int N,
+    int pos0, int P, const StageWait& sw) {
 	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
 #ifndef GCMX_SX_L8_STAGE  // tuning: stage U / U1 / U_next in LDS (1) or read them through the caches (0)
 #define GCMX_SX_L8_STAGE 0
@@ -1008,7 +1159,6 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
 	const double* U1s = U1;
 	const double* Uns = Unext;
 #endif
-	const int gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const int t = gid / kL, c = gid % kL;
 	const bool store = t < count;
 	const int n = nodes[store ? t : count - 1];
@@ -1044,12 +1194,62 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
 			for (int j = 0; j < 3; j++) cv[r][j] = U1s[rows[r] * kM + (1 - h) + 2 * j];
 	}
 	double o[kM];
-	group_invariants(n, c, pos0 + tr, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, o);
+	// in the one-launch stage the feet wait for their cells' gradients (never for wn:
+	// the plan check keeps new-invariant reads out of border feet)
+	group_invariants<SIGNAL>(n, c, pos0 + tr, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, o, sw);
 #ifndef GCMX_SX_DIAG_NOCORR  // tuning builds only: time the kernel without the correctors
 	if (ci >= 0) border_correct_l8(o, ci, c, cnd, code, rc.w, Brow, Md, Sv, RU, RU1, cv, bv);
 #endif
 	// wn (node-major, like wnext) is stored with the finalisation's stores, after every load
-	group_finalize(n, c, fin, o, RU1, Rn, Uns != nullptr, un, wnext, N, wn, store);
+	group_finalize<SIGNAL>(n, c, fin, o, RU1, Rn, Uns != nullptr, un, wnext, N, wn, store);
+	if constexpr (SIGNAL) {
+		// the group's eight lanes are one wave's: drain their sc1 wn stores, then the flag
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		if (c == 0 && store)
+			__hip_atomic_store(sw.ready + n, sw.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+
+__global__ __launch_bounds__(256) void k_sx_border_l8(
+    const int* __restrict__ nodes, int count, const int4* __restrict__ fv,
+    const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
+    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, const BorderArgs* __restrict__ argp,
+    const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
+    double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
+	border_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
+	                 deferred, bp, argp, U, U1, Unext, un, wnext, stage, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr});
+}
+
+// One launch for a whole stage of one body (gsx_stage, nothing between its
+// border and inner halves): blocks [0, ngBlk) run k_sx_gradient_l8's groups,
+// [ngBlk, ngBlk + nbBlk) k_sx_border_l8's over the border list, the rest
+// k_sx_inner_l8's over the inner list, side by side.  A CELL foot waits until
+// every gradient block has finished.
+// An inner foot interpolating in space-time with border nodes' NEW invariants
+// (interpolateInOwner; engine/simplex/Engine.cpp:119-135 orders the border
+// stage first) waits for exactly those nodes' flags.  Border blocks never wait
+// and have the lower block ids, and workgroups are dispatched in id order, so
+// every block an inner group waits for is resident or finished.
+__global__ __launch_bounds__(256) void k_sx_stage_l8(
+    const int* __restrict__ border, int nBorder, const int* __restrict__ inner, int nInner, int nbBlk,
+    const int4* __restrict__ fv, const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
+    const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
+    double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, const BorderArgs* __restrict__ argp,
+    const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
+    double* __restrict__ un, double* __restrict__ wnext, int stage, int N, StageWait sw, int ngBlk,
+    double* __restrict__ gradw, const int* __restrict__ gOff, const int* __restrict__ gNb,
+    const double* __restrict__ gW, const double* __restrict__ gM, const double* __restrict__ gDet) {
+	const int P = nBorder + nInner;
+	const int b = blockIdx.x;
+	if (b < ngBlk)
+		gradient_l8<true>(b * blockDim.x + threadIdx.x, w, gradw, gOff, gNb, coords, gW, gM, gDet, N, sw.gcount);
+	else if (b < ngBlk + nbBlk)
+		border_l8<true>((b - ngBlk) * blockDim.x + threadIdx.x, border, nBorder, fv, flam, fmeta, sh, coords, w, grad,
+		                wn, deferred, bp, argp, U, U1, Unext, un, wnext, stage, N, 0, P, sw);
+	else
+		inner_l8<true>((b - ngBlk - nbBlk) * blockDim.x + threadIdx.x, inner, nInner, fv, flam, fmeta, sh, coords,
+		               w, grad, wn, U1, Unext, un, wnext, N, nBorder, P, sw);
 }
 
 // The step's border values b(t) into device memory (gsx_set_border_values).
@@ -1320,6 +1520,11 @@ gcmx_status gsx_create(int device, int n_nodes, const double* coords, gsx_ctx** 
 		gsx_destroy(c);
 		return fail(GCMX_ERR_OOM, "simplex border-value allocation failed");
 	}
+	if (hipMalloc(&c->ready, (N + 2) * sizeof(int)) != hipSuccess ||
+	    hipMemset(c->ready, 0, (N + 2) * sizeof(int)) != hipSuccess) {
+		gsx_destroy(c);
+		return fail(GCMX_ERR_OOM, "simplex flag allocation failed");
+	}
 	*out = c;
 	return GCMX_OK;
 }
@@ -1330,6 +1535,7 @@ void gsx_destroy(gsx_ctx* c) {
 	if (c->stream) (void)hipStreamSynchronize(c->stream);
 	c->graphs.reset();
 	if (c->bvals) (void)hipFree(c->bvals);
+	if (c->ready) (void)hipFree(c->ready);
 	void* ptrs[] = {c->coords, c->arena, c->corrOf, c->deferred,
 	                c->mats, c->gOff, c->gNb,
 	                c->gRows, c->gW, c->gM, c->gDet};
@@ -1443,6 +1649,24 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 			flam[e] = make_double4(f.lam[0], f.lam[1], f.lam[2], f.lam[3]);
 			fmeta[e] = meta;
 		}
+	// one-launch stage (k_sx_stage_l8): every wn read of an inner foot must name a
+	// node of the border list (its flag is set in the same launch), and no border
+	// foot may read wn (border groups never wait)
+	bool fusable = true;
+	{
+		std::vector<char> inBorder(N, 0);
+		for (int i = 0; i < nb; i++) inBorder[border[i]] = 1;
+		for (int pos = 0; pos < P && fusable; pos++)
+			for (int k = 0; k < 6 && fusable; k++) {
+				const size_t e = (size_t)k * P + pos;
+				if ((fmeta[e] & 15) != GSX_FOOT_SPACETIME) continue;
+				const int vs[4] = {fv[e].x, fv[e].y, fv[e].z, fv[e].w};
+				for (int i = 0; i < 4; i++) {
+					const int sl = (fmeta[e] >> (4 + 4 * i)) & 15;
+					if (sl >= 3 && (pos < nb || !inBorder[vs[sl - 3]])) fusable = false;
+				}
+			}
+	}
 	SX_TRY(hipStreamSynchronize(c->stream));
 	StageDev& st = c->st[stage];
 	if ((s = upload(&st.fv, fv.data(), fv.size())) || (s = upload(&st.flam, flam.data(), flam.size())) ||
@@ -1460,6 +1684,7 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 	}
 	st.nBorder = nb;
 	st.nInner = ni;
+	st.fusable = fusable;
 	st.set = true;
 	return prep_border(c);
 }
@@ -1592,7 +1817,14 @@ const double* nextU(const gsx_ctx* c, int stage) {
 }
 }  // namespace
 
-gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
+}  // extern "C"
+
+namespace {
+// gsx_stage_nodes' launches; with `fuse` (gsx_stage: nothing runs between the
+// border and inner halves) an eligible stage runs both halves as one launch
+// (k_sx_stage_l8) and *fused says so, so the finish skips the inner launch.
+gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
+	*fused = false;
 	gcmx_status s = check(c);
 	if (s) return s;
 	if (stage < 0 || stage > 2) return fail(GCMX_ERR_INVALID_ARG, "stage out of range");
@@ -1610,6 +1842,43 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 		hipLaunchKernelGGL(k_sx_transform<true>, grd, blk, 0, c->stream, c->u, c->w,
 		                   c->mats + stage * 81, N);
 	c->wStage = -1;
+	// one-launch stage (k_sx_stage_l8: gradient, border and inner groups side by side)
+	// a few hundred blocks at most: every block is resident beside the ones it
+	// waits for (at 64^3 with eight lanes, 8 600 blocks of waiting groups measured
+	// 1.45x slower than separate launches)
+	const size_t nblk = ((size_t)(N + st.nBorder + st.nInner) * kL + kL8Block - 1) / kL8Block;
+	bool one = fuse && l8 && c->fuseMode && st.fusable && st.nBorder > 0 && st.nInner > 0 && nblk <= kFuseMaxBlocks;
+	const bool withGrad = c->fuseMode == 2;  // the gradient groups in the same launch
+	if (one) {  // a graph being captured would replay a stale epoch
+		hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+		SX_TRY(hipStreamIsCapturing(c->stream, &cs));
+		one = cs == hipStreamCaptureStatusNone;
+	}
+	if (one) {
+		if (c->epoch == INT_MAX) {  // flags restart from zero
+			SX_TRY(hipMemsetAsync(c->ready, 0, (size_t)N * sizeof(int), c->stream));
+			c->epoch = 0;
+		}
+		const BorderDevArgs bp = {c->corrOf, (bd.set && bd.n) ? bd.cond : nullptr, bd.B, bd.S,
+		                          bd.outer, bd.n, bd.nCond, st.rec, st.recB, st.recMd};
+		const int ngBlk = withGrad ? (int)(((size_t)N * kL + kL8Block - 1) / kL8Block) : 0;
+		c->gTarget += (unsigned)ngBlk;  // the counter wraps like the target
+		const StageWait sw{c->ready, withGrad ? reinterpret_cast<unsigned*>(c->ready + N) : nullptr, c->gTarget,
+		                   ++c->epoch, c->ready + N + 1};
+		if (!withGrad)
+			hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
+			                   c->stream, c->w, c->grad, c->gOff, c->gNb, c->coords, c->gW, c->gM, c->gDet, N);
+		const int nbBlk = (int)(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block);
+		const int niBlk = (int)(((size_t)st.nInner * kL + kL8Block - 1) / kL8Block);
+		hipLaunchKernelGGL(k_sx_stage_l8, dim3(ngBlk + nbBlk + niBlk), dim3(kL8Block), 0, c->stream, st.border,
+		                   st.nBorder, st.inner, st.nInner, nbBlk, st.fv, st.flam, st.fmeta, st.shift, c->coords,
+		                   c->w, c->grad, c->wn, c->deferred, bp, bd.argsDev, c->mats + stage * 81,
+		                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, sw, ngBlk,
+		                   c->grad, c->gOff, c->gNb, c->gW, c->gM, c->gDet);
+		SX_TRY(hipGetLastError());
+		*fused = true;
+		return GCMX_OK;
+	}
 	if (l8)
 		hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
 		                   c->stream, c->w,
@@ -1650,7 +1919,7 @@ gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
 	return GCMX_OK;
 }
 
-gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
+gcmx_status stage_finish(gsx_ctx* c, int stage, bool inner_done) {
 	gcmx_status s = check(c);
 	if (s) return s;
 	if (stage < 0 || stage > 2) return fail(GCMX_ERR_INVALID_ARG, "stage out of range");
@@ -1659,7 +1928,8 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 	const int N = c->N;
 	const dim3 blk(256);
 	const StageDev& st = c->st[stage];
-	if (st.nInner && node_lanes(c) == kL)
+	if (inner_done) {
+	} else if (st.nInner && node_lanes(c) == kL)
 		hipLaunchKernelGGL(k_sx_inner_l8, dim3(((size_t)st.nInner * kL + kL8Block - 1) / kL8Block),
 		                   dim3(kL8Block), 0, c->stream,
 		                   st.inner, st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
@@ -1679,6 +1949,31 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) {
 	return GCMX_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+gcmx_status gsx_stage_nodes(gsx_ctx* c, int stage) {
+	bool fused;
+	return stage_nodes(c, stage, false, &fused);
+}
+
+gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) { return stage_finish(c, stage, false); }
+
+gcmx_status gsx_set_stage_fusion(gsx_ctx* c, int on) {
+	gcmx_status s = check(c);
+	if (s) return s;
+	if (on < 0 || on > 2) return fail(GCMX_ERR_INVALID_ARG, "stage fusion must be 0, 1 or 2");
+	c->fuseMode = on;
+	return GCMX_OK;
+}
+
+gcmx_status gsx_last_stage_fused(const gsx_ctx* c, int* fused) {
+	if (!c || !fused) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	*fused = c->lastFused ? 1 : 0;
+	return GCMX_OK;
+}
+
 gcmx_status gsx_set_node_lanes(gsx_ctx* c, int lanes) {
 	gcmx_status s = check(c);
 	if (s) return s;
@@ -1689,9 +1984,11 @@ gcmx_status gsx_set_node_lanes(gsx_ctx* c, int lanes) {
 }
 
 gcmx_status gsx_stage(gsx_ctx* c, int stage) {
-	gcmx_status s = gsx_stage_nodes(c, stage);
+	bool fused = false;
+	gcmx_status s = stage_nodes(c, stage, true, &fused);
 	if (s) return s;
-	return gsx_stage_finish(c, stage);
+	c->lastFused = fused;
+	return stage_finish(c, stage, fused);
 }
 
 gcmx_status gsx_contact_create(gsx_ctx* a, gsx_ctx* b, int n, const int* nodes_a,
@@ -1902,6 +2199,9 @@ gcmx_status gsx_sync(gsx_ctx* c) {
 	gcmx_status s = check(c);
 	if (s) return s;
 	SX_TRY(hipStreamSynchronize(c->stream));
+	int err = 0;  // a one-launch stage's wait that timed out (k_sx_stage_l8)
+	SX_TRY(hipMemcpy(&err, c->ready + (size_t)c->N + 1, sizeof(int), hipMemcpyDeviceToHost));
+	if (err) return fail(GCMX_ERR_STATE, "one-launch simplex stage: a border-node wait timed out");
 	return GCMX_OK;
 }
 

@@ -50,6 +50,7 @@ SYMBOLS = [
     "gsx_plain_correction", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
     "gsx_stage_nodes", "gsx_stage_finish", "gsx_contact_create", "gsx_contact_destroy",
     "gsx_contact_plain", "gsx_contact_correct", "gsx_step", "gsx_set_node_lanes",
+    "gsx_set_stage_fusion", "gsx_last_stage_fused",
 ]
 
 

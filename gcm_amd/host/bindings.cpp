@@ -504,6 +504,10 @@ PYBIND11_MODULE(_gcm_host, m) {
 	         "gsx_step graph replay or the individual stage calls (default)", py::arg("on"))
 	    .def("set_node_lanes", [](PySimplexEngine& p, int lanes) { p.e->setNodeLanes(lanes); },
 	         "node-kernel layout: 0 automatic, 1 thread per node, 8 lanes per node", py::arg("lanes"))
+	    .def("set_stage_fusion", [](PySimplexEngine& p, int mode) { p.e->setStageFusion(mode); },
+	         "one launch per stage for a body without contacts: 0 off, 1 border + inner (default), "
+	         "2 with the gradient", py::arg("mode"))
+	    .def_property_readonly("fused_stages", [](PySimplexEngine& p) { return p.e->fusedStages(); })
 	    .def_property_readonly("steps", [](PySimplexEngine& p) { return p.e->stepsDone(); })
 	    .def_property_readonly("time_step", [](PySimplexEngine& p) { return p.e->timeStepValue(); })
 	    .def_property_readonly("required_time", [](PySimplexEngine& p) { return p.e->getRequiredTime(); });

@@ -1232,6 +1232,10 @@ void Engine::setNodeLanes(int lanes) {
 	for (auto& b : bodies) gcmxCheck(gsx_set_node_lanes(b.ctx, lanes), "gsx_set_node_lanes");
 }
 
+void Engine::setStageFusion(int mode) {
+	for (auto& b : bodies) gcmxCheck(gsx_set_stage_fusion(b.ctx, mode), "gsx_set_stage_fusion");
+}
+
 Engine::~Engine() {
 	for (auto* c : contacts) gsx_contact_destroy(c);
 	for (auto& b : bodies) gsx_destroy(b.ctx);
@@ -1254,6 +1258,15 @@ void Engine::nextTimeStep() {
 	}
 	plainCorrections();
 	for (int stage = 0; stage < 3; stage++) {
+		if (contacts.empty()) {  // nothing between a body's halves: gsx_stage may run them as one launch
+			for (auto& b : bodies) {
+				gcmxCheck(gsx_stage(b.ctx, stage), "gsx_stage");
+				int fused = 0;
+				gcmxCheck(gsx_last_stage_fused(b.ctx, &fused), "gsx_last_stage_fused");
+				fusedStages_ += fused;
+			}
+			continue;
+		}
 		for (auto& b : bodies) gcmxCheck(gsx_stage_nodes(b.ctx, stage), "gsx_stage_nodes");
 		for (auto* c : contacts) gcmxCheck(gsx_contact_correct(c, stage), "gsx_contact_correct");
 		for (auto& b : bodies) gcmxCheck(gsx_stage_finish(b.ctx, stage), "gsx_stage_finish");

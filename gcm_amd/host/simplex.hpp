@@ -254,6 +254,11 @@ public:
 	void setReplaySteps(bool on) { replaySteps = on; }
 	/// Thread layout of every body's node kernels (gsx_set_node_lanes: 0 auto, 1, 8).
 	void setNodeLanes(int lanes);
+	/// One launch per stage for the border and inner halves of a body without
+	/// contacts (gsx_set_stage_fusion: 0 off, 1 default, 2 with the gradient).
+	void setStageFusion(int mode);
+	/// stages run as one launch since construction
+	long long fusedStages() const { return fusedStages_; }
 
 protected:
 	void nextTimeStep() override;
@@ -276,6 +281,7 @@ private:
 	std::unique_ptr<VtkSnapshotter> vtk;
 	int stepsPerSnap = 1;
 	bool replaySteps = false;
+	long long fusedStages_ = 0;
 	void setBorderValues(real time);
 	void plainCorrections();
 };

@@ -303,6 +303,14 @@ gcmx_status gsx_stage_finish(gsx_ctx* ctx, int stage);
  * sizes: a node's dependent gathers run in parallel), 0 = automatic (8 below
  * 32 768 nodes).  Results are identical. */
 gcmx_status gsx_set_node_lanes(gsx_ctx* ctx, int lanes);
+/* gsx_stage in the eight-lane layout runs the border and inner halves of a stage
+ * as ONE launch where the plan allows it (every inner foot that interpolates in
+ * space-time with border nodes' new invariants waits, on the device, for exactly
+ * those nodes): on = 1 (default) border + inner, 2 also the gradient groups in
+ * the same launch, 0 separate launches.  Results are identical.
+ * gsx_last_stage_fused reports whether the last gsx_stage ran as one launch. */
+gcmx_status gsx_set_stage_fusion(gsx_ctx* ctx, int on);
+gcmx_status gsx_last_stage_fused(const gsx_ctx* ctx, int* fused);
 
 /* ---- simplex contact correctors ----------------------------------------------
  * ContactCorrectorInRiemannInvariants<Elastic, Elastic, AdhesionContactMatrixCreator>

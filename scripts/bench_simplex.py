@@ -50,6 +50,8 @@ def main():
                     help="node-kernel layout (gsx_set_node_lanes): 0 automatic, 1, 8")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from a gsx_step HIP graph instead of the stage calls")
+    ap.add_argument("--fusion", type=int, default=1,
+                    help="gsx_set_stage_fusion: 0 separate launches, 1 border + inner in one, 2 with the gradient")
     a = ap.parse_args()
     from gcm_amd import _gcm_host as H
     for name in a.workloads.split(","):
@@ -59,6 +61,7 @@ def main():
         e = H.SimplexEngine(task)
         e.set_replay_steps(a.graph)
         e.set_node_lanes(a.lanes)
+        e.set_stage_fusion(a.fusion)
         setup = time.perf_counter() - t0
         nv = sum(e.number_of_vertices(b) for b in range(e.number_of_bodies))
         e.run_steps(a.warmup)
@@ -73,7 +76,8 @@ def main():
             "ms_per_step": round(dt / a.steps * 1e3, 4), "vertices": nv,
             "bodies": e.number_of_bodies, "contact_pairs": e.number_of_contact_pairs,
             "steps": a.steps, "warmup": a.warmup, "setup_s": round(setup, 1), "dtype": "f64",
-            "graph": a.graph, "lanes": a.lanes,
+            "graph": a.graph, "lanes": a.lanes, "fusion": a.fusion,
+            "fused_stages": e.fused_stages,
         }), flush=True)
 
 

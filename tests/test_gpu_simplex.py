@@ -194,3 +194,32 @@ def test_graph_replayed_steps_equal_individual_calls(H, lanes, workload):
     for k, (xa, xb) in enumerate(zip(a, b)):
         for body, (pa, pb) in enumerate(zip(xa, xb)):
             assert np.array_equal(pa, pb), f"{workload} body {body} after chunk {k}"
+
+
+@pytest.mark.parametrize("mode", [1, 2], ids=["border+inner", "gradient+border+inner"])
+@pytest.mark.parametrize("case", ["free-c2", "mixed-c1.3", "fracture-c1.7", "plain-c1"])
+def test_one_launch_stage_equals_two_launches(H, case, mode):
+    """gsx_stage's one-launch stage (k_sx_stage_l8: border and inner groups side by
+    side, inner feet that interpolate in space-time with border nodes' new
+    invariants wait for exactly those nodes) == the border launch followed by
+    the inner launch, bitwise, with space-time feet present (Courant > 1)."""
+    if case == "free-c2":
+        mk = lambda: host_task(5, 2.0, 0.1, 7, border=FREE_BORDER)  # noqa: E731
+    elif case == "mixed-c1.3":
+        mk = lambda: host_task(4, 1.3, 0.1, 7, border=MIXED_BORDER)  # noqa: E731
+    elif case == "fracture-c1.7":
+        mk = lambda: fracture_task((16, 16, 8), 1.7)  # noqa: E731
+    else:
+        mk = lambda: host_task(6, 1.0, 0.15, 9, vector=[0.1 * i for i in range(9)])  # noqa: E731
+    out = []
+    for fuse in (mode, 0):
+        e = H.SimplexEngine(mk())
+        e.set_node_lanes(8)
+        e.set_stage_fusion(fuse)
+        e.run_steps(3)
+        e.sync()
+        out.append((e.pde(), e.fused_stages))
+    (fused, n_fused), (split, n_split) = out
+    assert n_fused == 9 and n_split == 0
+    assert np.array_equal(fused, split), f"{int((fused != split).sum())} values differ"
+    assert np.abs(fused).max() > 0
