@@ -97,35 +97,20 @@ def cpu_baseline(seconds: float):
                       f"{host_threads()}); {s1} steps in {e1:.1f} s on 1 thread"}
 
 
-def copy_ceiling(torch, device, step_bytes, achieved_gbps):
+def copy_ceiling(ctx, step_bytes, achieved_gbps):
     """What this box's HBM gives a plain copy of the same bytes the step must
-    move (half read, half written): a flat device-to-device copy of
-    step_bytes / 2, timed after the step's repetitions (outside them), median of
-    5.  The step's `achieved` over this rate says how close the kernel is to the
-    memory system's practical limit on this box (MI355X_MICROARCH.md: ~79 % of
-    the 8 TB/s spec for a float4 copy; tools/copy_probe.hip measures the
-    product layout's own copy beside a flat one)."""
-    n = int(step_bytes // 2 // 8)
-    src = torch.empty(n, dtype=torch.float64, device=f"cuda:{device}")
-    dst = torch.empty_like(src)
-    src.fill_(1.0)
-    dst.copy_(src)
-    ms = []
-    for _ in range(5):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        dst.copy_(src)
-        e1.record()
-        e1.synchronize()
-        ms.append(e0.elapsed_time(e1))
-    del src, dst
-    torch.cuda.empty_cache()
-    t = sorted(ms)[len(ms) // 2]
+    move (half read, half written): gcmx_copy_ceiling's flat copy (double2 per
+    lane, non-temporal stores; torch's copy_ measured 13 % slower), timed after
+    the step's repetitions (outside them), median of 5.  The step's `achieved`
+    over this rate says how close the kernel is to the memory system's practical
+    limit on this box (MI355X_MICROARCH.md: ~79 % of the 8 TB/s spec for a float4
+    copy; tools/copy_probe.hip measures the product layout's own copy beside a
+    flat one)."""
+    t = ctx.copy_ceiling_ms(int(step_bytes), 5)
     gbps = step_bytes / (t * 1e-3) / 1e9
     return {"GBps": round(gbps, 1), "frac_of_copy": round(achieved_gbps / gbps, 4),
-            "how": f"torch copy_ of {n * 8 / 1e9:.2f} GB fp64 (flat, device to device), "
-                   f"median of 5, bytes counted read + write"}
+            "how": f"gcmx_copy_ceiling: flat copy of {step_bytes / 2e9:.2f} GB (double2 loads, "
+                   f"non-temporal stores, 32768x256 threads), median of 5, bytes counted read + write"}
 
 
 def multi_gpu_parity(dist, world, rank, device, U, U1, L):
@@ -287,8 +272,7 @@ def main():
 
     if roof is not None and not a.no_copy_ceiling:
         try:
-            roof["copy_ceiling"] = copy_ceiling(torch, device, dom["bytes_per_launch"],
-                                                roof["achieved"])
+            roof["copy_ceiling"] = copy_ceiling(ctx, dom["bytes_per_launch"], roof["achieved"])
         except Exception as e:  # reported context, never required
             log(f"copy ceiling failed: {e}")
 

@@ -3,6 +3,7 @@
 // per-kernel event timing.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1180,5 +1181,59 @@ int gcmx_profile_read(gcmx_ctx* c, int index, const char** name, double* total_m
 long long gcmx_inner_nodes(gcmx_ctx* c) { return c ? c->geo.n_inner : 0; }
 long long gcmx_all_nodes(gcmx_ctx* c) { return c ? c->n_all : 0; }
 size_t gcmx_device_bytes(gcmx_ctx* c) { return c ? 2 * c->layer_elems * sizeof(double) : 0; }
+
+}  // extern "C"
+
+namespace {
+typedef double copy_d2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_copy_ceiling(const copy_d2* __restrict__ in, copy_d2* __restrict__ out,
+                                                      long long n2) {
+	const long long stride = (long long)gridDim.x * blockDim.x;
+	for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride)
+		__builtin_nontemporal_store(in[i], out + i);
+}
+}  // namespace
+
+extern "C" {
+
+gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!ms_out || reps < 1 || bytes < 64) return fail(GCMX_ERR_INVALID_ARG, "bad copy-ceiling arguments");
+	const size_t half = bytes / 2 / 16 * 16;
+	void *a = nullptr, *b = nullptr;
+	if (hipMalloc(&a, half) != hipSuccess || hipMalloc(&b, half) != hipSuccess) {
+		if (a) (void)hipFree(a);
+		return fail(GCMX_ERR_OOM, "copy-ceiling buffers");
+	}
+	hipEvent_t e0 = nullptr, e1 = nullptr;
+	std::vector<float> ms;
+	gcmx_status st = GCMX_OK;
+	const long long n2 = (long long)(half / 16);
+	if (hipMemsetAsync(a, 0, half, c->stream) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+	    hipEventCreate(&e1) != hipSuccess) {
+		st = fail(GCMX_ERR_HIP, "copy-ceiling set-up");
+	} else {
+		for (int r = 0; r <= reps && st == GCMX_OK; r++) {
+			hipEventRecord(e0, c->stream);
+			hipLaunchKernelGGL(k_copy_ceiling, dim3(32768), dim3(256), 0, c->stream,
+			                   static_cast<const copy_d2*>(a), static_cast<copy_d2*>(b), n2);
+			hipEventRecord(e1, c->stream);
+			float t = 0.0f;
+			if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&t, e0, e1) != hipSuccess)
+				st = fail(GCMX_ERR_HIP, "copy-ceiling timing");
+			else if (r > 0)  // the first copy warms the buffers' translations
+				ms.push_back(t);
+		}
+	}
+	if (e0) (void)hipEventDestroy(e0);
+	if (e1) (void)hipEventDestroy(e1);
+	(void)hipFree(a);
+	(void)hipFree(b);
+	if (st) return st;
+	std::sort(ms.begin(), ms.end());
+	*ms_out = ms[ms.size() / 2] * (float)((double)bytes / (double)(2 * half));  // per `bytes`
+	return GCMX_OK;
+}
 
 }  // extern "C"

@@ -44,7 +44,7 @@ SYMBOLS = [
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_sync", "gcmx_stream",
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_inner_nodes",
-    "gcmx_all_nodes", "gcmx_device_bytes",
+    "gcmx_all_nodes", "gcmx_device_bytes", "gcmx_copy_ceiling",
     "gsx_create", "gsx_destroy", "gsx_set_matrices", "gsx_set_gradient_plan",
     "gsx_set_stage_plan", "gsx_set_border_plan", "gsx_set_border_values",
     "gsx_plain_correction", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
@@ -138,6 +138,8 @@ def lib() -> ctypes.CDLL:
     L.gcmx_all_nodes.restype = ctypes.c_longlong
     L.gcmx_device_bytes.argtypes = [vp]
     L.gcmx_device_bytes.restype = ctypes.c_size_t
+    L.gcmx_copy_ceiling.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+    L.gcmx_copy_ceiling.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -302,6 +304,13 @@ class Context:
 
     def halo_exchange(self):
         _check(lib().gcmx_halo_exchange(self._ptr))
+
+    def copy_ceiling_ms(self, nbytes: int, reps: int = 5) -> float:
+        """Median duration (ms) of a flat device copy moving `nbytes` (half read,
+        half written) on this context's device (gcmx_copy_ceiling)."""
+        ms = ctypes.c_float(0.0)
+        _check(lib().gcmx_copy_ceiling(self._ptr, int(nbytes), int(reps), ctypes.byref(ms)))
+        return float(ms.value)
 
     def sync(self):
         _check(lib().gcmx_sync(self._ptr))

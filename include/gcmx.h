@@ -366,6 +366,13 @@ int         gcmx_profile_read(gcmx_ctx* ctx, int index, const char** name,
 long long   gcmx_inner_nodes(gcmx_ctx* ctx);
 long long   gcmx_all_nodes(gcmx_ctx* ctx);
 size_t      gcmx_device_bytes(gcmx_ctx* ctx);
+/* Measurement only (bench.py's roofline.copy_ceiling): the practical HBM rate
+ * of this device for a flat copy of `bytes` bytes (half read, half written;
+ * double2 per lane, non-temporal stores, 32 768 blocks of 256 threads, the
+ * fastest of tools/copy_probe.hip's grids).  Median of `reps` timed copies
+ * after one warm copy; *ms_out = that copy's duration (HIP events on the
+ * ctx stream).  Allocates and frees 2 x bytes / 2 on the context's device. */
+gcmx_status gcmx_copy_ceiling(gcmx_ctx* ctx, size_t bytes, int reps, float* ms_out);
 
 #ifdef __cplusplus
 }
