@@ -122,7 +122,8 @@ struct gsx_ctx {
 	int* ready = nullptr;
 	int epoch = 0;
 	unsigned gTarget = 0;
-	int fuseMode = 1;  // gsx_set_stage_fusion: 0 never, 1 border + inner, 2 gradient + border + inner
+	int fuseMode = 1;  // gsx_set_stage_fusion: 0 never, 1 border + inner, 2 gradient + border + inner,
+	                   // 3 border + inner without the grid-size cap (tuning)
 	bool lastFused = false;  // the last gsx_stage ran as one launch
 };
 
@@ -624,8 +625,12 @@ constexpr int kL = 8;
 #define GCMX_SX_L8_BLOCK 256
 #endif
 constexpr int kL8Block = GCMX_SX_L8_BLOCK;
-// Largest one-launch stage (k_sx_stage_l8), in blocks: about two per CU.
-constexpr size_t kFuseMaxBlocks = 512;
+// Automatic node-kernel layout: eight lanes per node below this many vertices.
+constexpr int kL8MaxNodes = 131072;
+// Largest one-launch stage (k_sx_stage_l8), in blocks.  Measured (one box,
+// profiles/r2/simplex_fused/f64.txt): 32^3 meshes (1 120 blocks) gain 14-8 %
+// against two launches, 64^3 (8 600 blocks) lose 11 % on the cube.
+constexpr size_t kFuseMaxBlocks = 4096;
 
 template <bool SC1>
 __device__ __forceinline__ void gradient_node_l8(int gid, const double* __restrict__ w, double* __restrict__ grad,
@@ -1808,8 +1813,10 @@ gcmx_status gsx_plain_correction(gsx_ctx* c) {
 }
 
 namespace {
-// Node-kernel layout (gsx_set_node_lanes): eight lanes per node below 32 768 nodes.
-int node_lanes(const gsx_ctx* c) { return c->nodeLanes ? c->nodeLanes : (c->N < 32768 ? kL : 1); }
+// Node-kernel layout (gsx_set_node_lanes): eight lanes per node below kL8MaxNodes vertices.
+// Measured: 32^3 meshes (35 937 vertices) run 7-35 % faster with eight lanes,
+// 64^3 (274 625) 6-12 % slower.
+int node_lanes(const gsx_ctx* c) { return c->nodeLanes ? c->nodeLanes : (c->N < kL8MaxNodes ? kL : 1); }
 // The next stage's U for the fused beforeStage, or null after the last stage of
 // the step (the next step starts with the plain corrections, which change u).
 const double* nextU(const gsx_ctx* c, int stage) {
@@ -1846,8 +1853,10 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 	// a few hundred blocks at most: every block is resident beside the ones it
 	// waits for (at 64^3 with eight lanes, 8 600 blocks of waiting groups measured
 	// 1.45x slower than separate launches)
-	const size_t nblk = ((size_t)(N + st.nBorder + st.nInner) * kL + kL8Block - 1) / kL8Block;
-	bool one = fuse && l8 && c->fuseMode && st.fusable && st.nBorder > 0 && st.nInner > 0 && nblk <= kFuseMaxBlocks;
+	const size_t nblk =
+	    ((size_t)((c->fuseMode == 2 ? N : 0) + st.nBorder + st.nInner) * kL + kL8Block - 1) / kL8Block;
+	bool one = fuse && l8 && c->fuseMode && st.fusable && st.nBorder > 0 && st.nInner > 0 &&
+	           (nblk <= kFuseMaxBlocks || c->fuseMode == 3);
 	const bool withGrad = c->fuseMode == 2;  // the gradient groups in the same launch
 	if (one) {  // a graph being captured would replay a stale epoch
 		hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1963,7 +1972,7 @@ gcmx_status gsx_stage_finish(gsx_ctx* c, int stage) { return stage_finish(c, sta
 gcmx_status gsx_set_stage_fusion(gsx_ctx* c, int on) {
 	gcmx_status s = check(c);
 	if (s) return s;
-	if (on < 0 || on > 2) return fail(GCMX_ERR_INVALID_ARG, "stage fusion must be 0, 1 or 2");
+	if (on < 0 || on > 3) return fail(GCMX_ERR_INVALID_ARG, "stage fusion must be 0..3");
 	c->fuseMode = on;
 	return GCMX_OK;
 }

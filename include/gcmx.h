@@ -301,7 +301,7 @@ gcmx_status gsx_stage_finish(gsx_ctx* ctx, int stage);
  * node (throughput layout for large meshes), 8 = eight lanes per node, one per
  * component / characteristic foot (latency layout for the reference's mesh
  * sizes: a node's dependent gathers run in parallel), 0 = automatic (8 below
- * 32 768 nodes).  Results are identical. */
+ * 131 072 nodes).  Results are identical. */
 gcmx_status gsx_set_node_lanes(gsx_ctx* ctx, int lanes);
 /* gsx_stage in the eight-lane layout runs the border and inner halves of a stage
  * as ONE launch where the plan allows it (every inner foot that interpolates in

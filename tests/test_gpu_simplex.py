@@ -20,7 +20,7 @@ def H():
 @pytest.fixture(params=[1, 8], ids=["lanes1", "lanes8"])
 def lanes(request):
     """gsx_set_node_lanes: one thread per node, or eight lanes per node (the
-    automatic choice below 32 768 nodes, i.e. for every mesh here)."""
+    automatic choice below 131 072 nodes, i.e. for every mesh here)."""
     return request.param
 
 
