@@ -752,7 +752,11 @@ __device__ __forceinline__ void wait_flag(const StageWait& sw, const int* flags,
 	}
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// Every gradient of the launch is stored (one poll address for all).
+// Every gradient of the launch is stored (one poll address for all; the sleep
+// between polls keeps the polling waves from crowding the counter's updates).
+#ifndef GCMX_SX_GPOLL_SLEEP
+#define GCMX_SX_GPOLL_SLEEP 2
+#endif
 __device__ __forceinline__ void wait_gradients(const StageWait& sw) {
 	int polls = 0;
 	while ((int)(__hip_atomic_load(sw.gcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - sw.gtarget) < 0) {
@@ -760,7 +764,7 @@ __device__ __forceinline__ void wait_gradients(const StageWait& sw) {
 			atomicOr(sw.err, 2);
 			break;
 		}
-		__builtin_amdgcn_s_sleep(2);
+		__builtin_amdgcn_s_sleep(GCMX_SX_GPOLL_SLEEP);
 	}
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
