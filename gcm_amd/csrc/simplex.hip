@@ -1658,6 +1658,44 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 			flam[e] = make_double4(f.lam[0], f.lam[1], f.lam[2], f.lam[3]);
 			fmeta[e] = meta;
 		}
+	// Inner nodes whose feet read border nodes' new invariants (wn) go to the END
+	// of the inner list (stable): in the one-launch stage they are the only
+	// groups that wait, so the independent ones fill the low block ids, finish
+	// and retire while the border groups run.  Every node is computed on its own,
+	// so the order changes no result.
+	std::vector<int> innerOrd(inner, inner + ni);
+	{
+		auto readsWn = [&](int pos) {
+			for (int k = 0; k < 6; k++) {
+				const size_t e = (size_t)k * P + pos;
+				if ((fmeta[e] & 15) != GSX_FOOT_SPACETIME) continue;
+				for (int i = 0; i < 4; i++)
+					if (((fmeta[e] >> (4 + 4 * i)) & 15) >= 3) return true;
+			}
+			return false;
+		};
+		std::vector<int> perm;  // new inner position -> old inner position
+		perm.reserve(ni);
+		for (int i = 0; i < ni; i++)
+			if (!readsWn(nb + i)) perm.push_back(i);
+		for (int i = 0; i < ni; i++)
+			if (readsWn(nb + i)) perm.push_back(i);
+		std::vector<int4> fv2(fv);
+		std::vector<double4> flam2(flam);
+		std::vector<int> fmeta2(fmeta);
+		for (int j = 0; j < ni; j++) {
+			innerOrd[j] = inner[perm[j]];
+			for (int k = 0; k < 6; k++) {
+				const size_t dst = (size_t)k * P + nb + j, src = (size_t)k * P + nb + perm[j];
+				fv2[dst] = fv[src];
+				flam2[dst] = flam[src];
+				fmeta2[dst] = fmeta[src];
+			}
+		}
+		fv.swap(fv2);
+		flam.swap(flam2);
+		fmeta.swap(fmeta2);
+	}
 	// one-launch stage (k_sx_stage_l8): every wn read of an inner foot must name a
 	// node of the border list (its flag is set in the same launch), and no border
 	// foot may read wn (border groups never wait)
@@ -1680,7 +1718,7 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 	StageDev& st = c->st[stage];
 	if ((s = upload(&st.fv, fv.data(), fv.size())) || (s = upload(&st.flam, flam.data(), flam.size())) ||
 	    (s = upload(&st.fmeta, fmeta.data(), fmeta.size())) ||
-	    (s = upload(&st.border, border, (size_t)nb)) || (s = upload(&st.inner, inner, (size_t)ni)))
+	    (s = upload(&st.border, border, (size_t)nb)) || (s = upload(&st.inner, innerOrd.data(), (size_t)ni)))
 		return s;
 	for (int k = 0; k < 6; k++)
 		for (int r = 0; r < 3; r++) st.shift.d[k][r] = shift[k * 3 + r];
