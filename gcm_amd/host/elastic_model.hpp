@@ -5,7 +5,7 @@
 // identity calculation basis the cubic engine uses.  Built once per material on
 // the host; the device only ever sees the finished U / U1 / L tables.  Every
 // expression keeps the reference's evaluation order so the tables are bitwise
-// the reference's (checked against the oracle in tests/test_host.py).
+// the reference's (checked against the oracle in tests/test_abi.py::test_host_matrices_match_oracle_bitwise).
 #pragma once
 
 #include <array>
