@@ -2252,7 +2252,11 @@ gcmx_status gsx_sync(gsx_ctx* c) {
 	SX_TRY(hipStreamSynchronize(c->stream));
 	int err = 0;  // a one-launch stage's wait that timed out (k_sx_stage_l8)
 	SX_TRY(hipMemcpy(&err, c->ready + (size_t)c->N + 1, sizeof(int), hipMemcpyDeviceToHost));
-	if (err) return fail(GCMX_ERR_STATE, "one-launch simplex stage: a border-node wait timed out");
+	if (err) {  // reported once: the word is cleared for the calls that follow
+		SX_TRY(hipMemset(c->ready + (size_t)c->N + 1, 0, sizeof(int)));
+		return fail(GCMX_ERR_STATE, err & 2 ? "one-launch simplex stage: a gradient wait timed out"
+		                                    : "one-launch simplex stage: a border-node wait timed out");
+	}
 	return GCMX_OK;
 }
 
