@@ -4,9 +4,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -58,6 +62,39 @@ struct Bucket {
 
 }  // namespace
 
+// In-process slab group (gcmx_comm_init_local): the RCCL exchange's semantics
+// with device copies.  Rank r posts generation g of its current layer (event
+// `ready` recorded after the work that produced it); the second rank of each
+// adjacent pair to post g issues that pair's two copies on its own comm stream,
+// after both ranks' `ready` events, and records `done`; a rank's wait for g
+// (host: until both its pairs were issued, then stream waits on their `done`)
+// covers the copies INTO its ghost planes and OUT OF its inner planes, as an
+// RCCL group's completion does.  Two event slots (g & 1) suffice: a rank's
+// wait(g) precedes its post(g + 1), and pair g + 2 needs both posts of g + 2.
+struct LocalComm {
+	int n = 0;
+	std::vector<gcmx_ctx*> ctx;
+	std::mutex mu;
+	std::condition_variable cv;
+	std::vector<long long> posted;         // [rank]: posts made
+	std::vector<long long> issued;         // [pair]: generations issued (pair i = ranks i, i+1)
+	std::vector<int> issuer[2];            // [slot][pair]: 0 = rank i issued, 1 = rank i+1
+	std::vector<double*> layer[2];         // [slot][rank]: the layer posted
+	std::vector<hipEvent_t> ready[2];      // [slot][rank] (rank's device)
+	std::vector<hipEvent_t> done[2][2];    // [slot][side][pair] (the issuing rank's device)
+	bool aborted = false;
+	std::string why;
+	~LocalComm() {
+		for (int t = 0; t < 2; t++) {
+			for (hipEvent_t e : ready[t])
+				if (e) (void)hipEventDestroy(e);
+			for (int sd = 0; sd < 2; sd++)
+				for (hipEvent_t e : done[t][sd])
+					if (e) (void)hipEventDestroy(e);
+		}
+	}
+};
+
 struct gcmx_ctx {
 	int device = 0;
 	hipStream_t stream = nullptr;
@@ -92,7 +129,12 @@ struct gcmx_ctx {
 	ncclComm_t comm = nullptr;
 	int nranks = 1, rank = 0, left = -1, right = -1;
 	bool halo_pending = false;     // an exchange is in flight on comm_stream (ev_halo)
+	bool halo_fresh = false;       // the current layer's ghost planes hold its neighbours' planes
+	double* halo_layer = nullptr;  // the layer the pending exchange fills
 	std::vector<int> halo_comps;
+	std::shared_ptr<LocalComm> lc;  // in-process slab group (gcmx_comm_init_local)
+	int lrank = -1;
+	long long halo_gen = 0;        // posts made (in-process group)
 	// profiling
 	bool prof = false;
 	std::vector<Bucket> buckets;
@@ -259,23 +301,121 @@ void compute_halo_comps(gcmx_ctx* c) {
 	}
 }
 
+bool has_halo(const gcmx_ctx* c) { return (c->comm || c->lc) && (c->left >= 0 || c->right >= 0); }
+
+// The current layer changed: its ghost planes no longer hold the neighbours' planes.
+void touch_layer(gcmx_ctx* c) { c->halo_fresh = false; }
+
+// x-plane x (all y/z rows including ghosts and row padding) of component `comp`
+// of `layer`: for D >= 2 the contiguous range [(x + bs) * stride0, (x + bs + 1) * stride0).
+double* plane_ptr(const gcmx_ctx* c, double* layer, int comp, int x) {
+	return layer + (size_t)comp * c->geo.cs + (size_t)((long long)(x + c->bs) * c->geo.stride[0]);
+}
+
+// How long a rank waits for a neighbour's post: GCMX_LOCAL_WAIT_SECONDS, default 60.
+double local_wait_seconds() {
+	const char* e = std::getenv("GCMX_LOCAL_WAIT_SECONDS");
+	const double d = e ? std::atof(e) : 0.0;
+	return d > 0 ? d : 60.0;
+}
+
+// In-process group: post generation halo_gen of the current layer.
+gcmx_status local_post(gcmx_ctx* c) {
+	LocalComm& L = *c->lc;
+	const int r = c->lrank;
+	const long long g = c->halo_gen;
+	const int slot = (int)(g & 1);
+	HIP_TRY(hipEventRecord(L.ready[slot][r], c->stream));
+	std::unique_lock<std::mutex> lk(L.mu);
+	if (L.aborted) return fail(GCMX_ERR_COMM, "in-process slab group aborted: " + L.why);
+	L.layer[slot][r] = c->cur;
+	L.posted[r] = g + 1;
+	for (int pr = r - 1; pr <= r; pr++) {  // pairs (r-1, r) and (r, r+1)
+		if (pr < 0 || pr + 1 >= L.n) continue;
+		const int other = (pr == r) ? r + 1 : r - 1;
+		if (L.posted[other] != g + 1) continue;  // the other rank issues this pair
+		gcmx_ctx* a = L.ctx[pr];
+		gcmx_ctx* b = L.ctx[pr + 1];
+		HIP_TRY(hipStreamWaitEvent(c->comm_stream, L.ready[slot][r], 0));
+		HIP_TRY(hipStreamWaitEvent(c->comm_stream, L.ready[slot][other], 0));
+		double* la = L.layer[slot][pr];
+		double* lb = L.layer[slot][pr + 1];
+		const size_t bytes = (size_t)(c->bs * c->geo.stride[0]) * sizeof(double);
+		const int Xa = a->geo.sizes[0];
+		for (int comp : c->halo_comps) {
+			// a's right ghosts [Xa, Xa+bs) <- b's inner [0, bs); b's left ghosts [-bs, 0) <- a's inner [Xa-bs, Xa)
+			HIP_TRY(hipMemcpyPeerAsync(plane_ptr(a, la, comp, Xa), a->device, plane_ptr(b, lb, comp, 0), b->device,
+			                           bytes, c->comm_stream));
+			HIP_TRY(hipMemcpyPeerAsync(plane_ptr(b, lb, comp, -b->bs), b->device, plane_ptr(a, la, comp, Xa - a->bs),
+			                           a->device, bytes, c->comm_stream));
+		}
+		const int side = (r == pr) ? 0 : 1;
+		HIP_TRY(hipEventRecord(L.done[slot][side][pr], c->comm_stream));
+		L.issuer[slot][pr] = side;
+		L.issued[pr] = g + 1;
+	}
+	lk.unlock();
+	L.cv.notify_all();
+	c->halo_gen = g + 1;
+	return GCMX_OK;
+}
+
+// In-process group: wait for the last posted generation (both pairs issued).
+gcmx_status local_wait(gcmx_ctx* c) {
+	LocalComm& L = *c->lc;
+	const int r = c->lrank;
+	const long long g = c->halo_gen - 1;
+	const int slot = (int)(g & 1);
+	std::unique_lock<std::mutex> lk(L.mu);
+	auto issued = [&] {
+		for (int pr = r - 1; pr <= r; pr++)
+			if (pr >= 0 && pr + 1 < L.n && L.issued[pr] < g + 1) return false;
+		return true;
+	};
+	const double wait_s = local_wait_seconds();
+	const bool ok = L.cv.wait_for(lk, std::chrono::duration<double>(wait_s),
+	                              [&] { return L.aborted || issued(); });
+	if (L.aborted) return fail(GCMX_ERR_COMM, "in-process slab group aborted: " + L.why);
+	if (!ok)
+		return fail(GCMX_ERR_COMM,
+		            "in-process slab group: a neighbour did not post its halo within " +
+		                std::to_string(wait_s) +
+		                " s (the contexts must be stepped concurrently, one host thread each)");
+	for (int pr = r - 1; pr <= r; pr++) {
+		if (pr < 0 || pr + 1 >= L.n) continue;
+		HIP_TRY(hipStreamWaitEvent(c->stream, L.done[slot][L.issuer[slot][pr]][pr], 0));
+	}
+	return GCMX_OK;
+}
+
+void local_abort(gcmx_ctx* c, const std::string& why) {
+	if (!c || !c->lc) return;
+	{
+		std::lock_guard<std::mutex> lk(c->lc->mu);
+		if (!c->lc->aborted) c->lc->why = why;
+		c->lc->aborted = true;
+	}
+	c->lc->cv.notify_all();
+}
+
 // Post the X-ghost exchange of the current layer on the comm stream (ordered
 // after all work issued so far on the compute stream).  Completion is marked
-// by ev_halo; consumers call halo_wait.
+// by ev_halo (RCCL) or the group's events (in-process); consumers call halo_wait.
 gcmx_status halo_post(gcmx_ctx* c) {
-	if (!c->comm || (c->left < 0 && c->right < 0)) return GCMX_OK;
+	if (!has_halo(c)) return GCMX_OK;
 	if (c->D < 2) return fail(GCMX_ERR_UNSUPPORTED, "X-slab halo needs dim >= 2");
 	if (c->halo_comps.empty()) return fail(GCMX_ERR_STATE, "materials not set");
+	if (c->lc) {
+		gcmx_status s = local_post(c);
+		if (s) return s;
+		c->halo_pending = true;
+		c->halo_layer = c->cur;
+		return GCMX_OK;
+	}
 	const Geo& g = c->geo;
-	const long long plane = g.stride[0];
-	const size_t n = (size_t)(c->bs * plane);
+	const size_t n = (size_t)(c->bs * g.stride[0]);
 	const int X = g.sizes[0];
 	// ghost planes [-bs, 0) and [X, X+bs); inner planes [0, bs) and [X-bs, X).
-	// For D >= 2 the x-plane x (all y/z rows including ghosts and row padding)
-	// is the contiguous range [(x + bs) * stride0, (x + bs + 1) * stride0).
-	auto plane_ptr = [&](int comp, int x) {
-		return c->cur + (size_t)comp * g.cs + (size_t)((long long)(x + c->bs) * plane);
-	};
 	HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
 	HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
 	ncclResult_t r = ncclGroupStart();
@@ -286,15 +426,15 @@ gcmx_status halo_post(gcmx_ctx* c) {
 	for (int comp : c->halo_comps) {
 		if (r == ncclSuccess && c->left >= 0) {
 			what = "ncclSend/Recv left";
-			r = ncclSend(plane_ptr(comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream);
+			r = ncclSend(plane_ptr(c, c->cur, comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream);
 			if (r == ncclSuccess)
-				r = ncclRecv(plane_ptr(comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream);
+				r = ncclRecv(plane_ptr(c, c->cur, comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream);
 		}
 		if (r == ncclSuccess && c->right >= 0) {
 			what = "ncclSend/Recv right";
-			r = ncclSend(plane_ptr(comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream);
+			r = ncclSend(plane_ptr(c, c->cur, comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream);
 			if (r == ncclSuccess)
-				r = ncclRecv(plane_ptr(comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream);
+				r = ncclRecv(plane_ptr(c, c->cur, comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream);
 		}
 	}
 	const ncclResult_t re = ncclGroupEnd();
@@ -302,19 +442,36 @@ gcmx_status halo_post(gcmx_ctx* c) {
 	if (re != ncclSuccess) return fail(GCMX_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
 	HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
 	c->halo_pending = true;
+	c->halo_layer = c->cur;
 	return GCMX_OK;
 }
 
 gcmx_status halo_wait(gcmx_ctx* c) {
 	if (!c->halo_pending) return GCMX_OK;
-	HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+	if (c->lc) {
+		gcmx_status s = local_wait(c);
+		if (s) return s;
+	} else {
+		HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+	}
 	c->halo_pending = false;
+	c->halo_fresh = c->halo_layer == c->cur;
 	return GCMX_OK;
 }
 
 gcmx_status halo_exchange_impl(gcmx_ctx* c) {
 	gcmx_status s = halo_wait(c);  // an earlier exchange of this layer is still in flight
 	if (s) return s;
+	s = halo_post(c);
+	if (s) return s;
+	return halo_wait(c);
+}
+
+// Ghost planes of the current layer valid before an X stage reads them: the
+// pending exchange, or a new one unless the layer's ghosts are already fresh.
+gcmx_status halo_ensure(gcmx_ctx* c) {
+	gcmx_status s = halo_wait(c);
+	if (s || c->halo_fresh) return s;
 	s = halo_post(c);
 	if (s) return s;
 	return halo_wait(c);
@@ -372,8 +529,8 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	if (s != GCMX_OK) return s;
 	s = halo_wait(c);
 	if (s != GCMX_OK) return s;
-	if (axis == 0 && c->comm) {
-		s = halo_exchange_impl(c);
+	if (axis == 0 && has_halo(c)) {
+		s = halo_ensure(c);
 		if (s != GCMX_OK) return s;
 	}
 	const Geo& g = c->geo;
@@ -393,6 +550,7 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "no kernel variant for this configuration");
 	HIP_TRY(hipGetLastError());
 	std::swap(c->cur, c->nxt);
+	touch_layer(c);
 	c->last_path = p == GCMX_PATH_GENERIC ? GCMX_PATH_GENERIC : GCMX_PATH_SPLIT;
 	return GCMX_OK;
 }
@@ -520,6 +678,11 @@ void gcmx_destroy(gcmx_ctx* c) {
 	drain_timings(c);
 	for (hipEvent_t ev : c->event_pool) hipEventDestroy(ev);
 	if (c->comm) ncclCommDestroy(c->comm);
+	if (c->lc) {  // the group cannot exchange without this rank any more
+		local_abort(c, "a context of the group was destroyed");
+		std::lock_guard<std::mutex> lk(c->lc->mu);
+		c->lc->ctx[c->lrank] = nullptr;
+	}
 	hipFree(c->cur);
 	hipFree(c->nxt);
 	hipFree(c->tabs_d);
@@ -667,6 +830,7 @@ gcmx_status gcmx_upload(gcmx_ctx* c, const double* aos) {
 	}
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	HIP_TRY(hipMemcpy(c->cur, soa.data(), c->layer_elems * sizeof(double), hipMemcpyHostToDevice));
+	touch_layer(c);
 	return GCMX_OK;
 }
 
@@ -698,6 +862,7 @@ gcmx_status gcmx_fill_random(gcmx_ctx* c, const int gs[3], uint64_t seed) {
 	}
 	launch_fill_random(c->cur, c->geo, st, D > 1 ? gs[1] : 1, D > 2 ? gs[2] : 1, seed, c->stream);
 	HIP_TRY(hipGetLastError());
+	touch_layer(c);
 	return GCMX_OK;
 }
 
@@ -738,7 +903,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 	const Geo& g = c->geo;
 	const int X = g.sizes[0], bs = c->bs;
 	const double plane_bytes = node_stage_bytes(c) * (double)g.sizes[1] * g.sizes[2];
-	const bool halo = c->comm && (c->left >= 0 || c->right >= 0);
+	const bool halo = has_halo(c);
 	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows) {
 		Timed t(c, name, plane_bytes * (x1 - x0), st);
 		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb);
@@ -760,7 +925,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 		HIP_TRY(hipStreamWaitEvent(c->inner_stream, c->ev_fork, 0));
 		join.inner = true;
 		ok = xyz("fused_xyz", bs, X - bs, c->inner_stream, c->rows_per_block);
-		if (ok && halo && !c->halo_pending) {
+		if (ok && halo && !c->halo_pending && !c->halo_fresh) {
 			s = halo_post(c);
 			if (s) return s;
 		}
@@ -782,7 +947,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 		}
 	} else {
 		if (halo) {
-			s = halo_exchange_impl(c);
+			s = halo_ensure(c);
 			if (s) return s;
 		}
 		ok = xyz("fused_xyz", 0, X, c->stream, c->rows_per_block);
@@ -790,6 +955,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
 	HIP_TRY(hipGetLastError());
 	std::swap(c->cur, c->nxt);
+	touch_layer(c);
 	c->last_path = GCMX_PATH_FUSED;
 	return GCMX_OK;
 }
@@ -1012,6 +1178,7 @@ gcmx_status gcmx_ode_maxwell(gcmx_ctx* c, double tau, const double* tau0, int n_
 		launch_scale_stress(c->cur, c->geo, c->mat_d, c->ode_d, 0.0, c->stream);
 	}
 	HIP_TRY(hipGetLastError());
+	touch_layer(c);
 	return GCMX_OK;
 }
 
@@ -1040,6 +1207,7 @@ gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dmin[3], const int dmax[3], g
 	HIP_TRY(hipStreamWaitEvent(dst->stream, src->ev_ready, 0));
 	launch_copy_box(dst->cur, dst->geo, src->cur, src->geo, dm, sm, ext, dst->stream);
 	HIP_TRY(hipGetLastError());
+	touch_layer(dst);
 	HIP_TRY(hipEventRecord(dst->ev_ready, dst->stream));
 	HIP_TRY(hipStreamWaitEvent(src->stream, dst->ev_ready, 0));
 	return GCMX_OK;
@@ -1062,7 +1230,7 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 	if (!id || nranks < 1 || rank < 0 || rank >= nranks || left >= nranks || right >= nranks ||
 	    left == rank || right == rank)
 		return fail(GCMX_ERR_INVALID_ARG, "bad communicator arguments");
-	if (c->comm) return fail(GCMX_ERR_STATE, "communicator already initialised");
+	if (c->comm || c->lc) return fail(GCMX_ERR_STATE, "communicator already initialised");
 	ncclUniqueId u;
 	std::memcpy(&u, id, sizeof(u));
 	ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
@@ -1088,6 +1256,7 @@ gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n) {
 	for (int i = 0; i < n; i++) {
 		gcmx_ctx* c = slabs[i];
 		if (!c || c->D < 2 || c->n_mat <= 0) return fail(GCMX_ERR_INVALID_ARG, "bad slab");
+		if (c->lc) return fail(GCMX_ERR_STATE, "slab belongs to an in-process group (gcmx_comm_init_local)");
 		if (i > 0) {
 			const gcmx_ctx* p = slabs[i - 1];
 			bool ok = p->D == c->D && p->bs == c->bs && p->desc.start[0] + p->geo.sizes[0] == c->desc.start[0];
@@ -1136,14 +1305,100 @@ gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n) {
 	return GCMX_OK;
 }
 
+gcmx_status gcmx_comm_init_local(gcmx_ctx* const* ctxs, int n) {
+	if (!ctxs || n < 1) return fail(GCMX_ERR_INVALID_ARG, "bad slab list");
+	for (int i = 0; i < n; i++) {
+		gcmx_ctx* c = ctxs[i];
+		if (!c || c->D < 2) return fail(GCMX_ERR_INVALID_ARG, "bad slab (null or dim < 2)");
+		if (c->comm || c->lc) return fail(GCMX_ERR_STATE, "communicator already initialised");
+		for (int j = 0; j < i; j++)
+			if (ctxs[j] == c) return fail(GCMX_ERR_INVALID_ARG, "a context appears twice");
+		if (i > 0) {
+			const gcmx_ctx* p = ctxs[i - 1];
+			bool ok = p->D == c->D && p->bs == c->bs && p->desc.start[0] + p->geo.sizes[0] == c->desc.start[0] &&
+			          p->geo.stride[0] == c->geo.stride[0];
+			for (int d = 1; d < c->D; d++)
+				ok = ok && p->geo.sizes[d] == c->geo.sizes[d] && p->desc.start[d] == c->desc.start[d];
+			if (!ok) return fail(GCMX_ERR_INVALID_ARG, "slabs are not X-adjacent with equal y/z extents");
+		}
+	}
+	auto L = std::make_shared<LocalComm>();
+	L->n = n;
+	L->ctx.assign(ctxs, ctxs + n);
+	L->posted.assign(n, 0);
+	L->issued.assign(n > 1 ? n - 1 : 0, 0);
+	for (int t = 0; t < 2; t++) {
+		L->issuer[t].assign(n > 1 ? n - 1 : 0, 0);
+		L->layer[t].assign(n, nullptr);
+		L->ready[t].assign(n, nullptr);
+		for (int sd = 0; sd < 2; sd++) L->done[t][sd].assign(n > 1 ? n - 1 : 0, nullptr);
+	}
+	for (int i = 0; i < n; i++) {
+		HIP_TRY(hipSetDevice(ctxs[i]->device));
+		for (int t = 0; t < 2; t++) {
+			HIP_TRY(hipEventCreateWithFlags(&L->ready[t][i], hipEventDisableTiming));
+			// done[t][0][i] is issued by rank i, done[t][1][i-1] by rank i
+			if (i + 1 < n) HIP_TRY(hipEventCreateWithFlags(&L->done[t][0][i], hipEventDisableTiming));
+			if (i > 0) HIP_TRY(hipEventCreateWithFlags(&L->done[t][1][i - 1], hipEventDisableTiming));
+		}
+	}
+	for (int i = 0; i < n; i++) {
+		gcmx_ctx* c = ctxs[i];
+		gcmx_status s = halo_wait(c);
+		if (s) return s;
+		c->lc = L;
+		c->lrank = i;
+		c->nranks = n;
+		c->rank = i;
+		c->left = i > 0 ? i - 1 : -1;
+		c->right = i + 1 < n ? i + 1 : -1;
+		c->halo_gen = 0;
+		c->halo_fresh = false;
+	}
+	HIP_TRY(hipSetDevice(ctxs[0]->device));
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_local_group_steps(gcmx_ctx* const* ctxs, int n, double tau, int steps) {
+	if (!ctxs || n < 1 || steps < 0) return fail(GCMX_ERR_INVALID_ARG, "bad group arguments");
+	std::shared_ptr<LocalComm> L = ctxs[0] ? ctxs[0]->lc : nullptr;
+	for (int i = 0; i < n; i++)
+		if (!ctxs[i] || (n > 1 && (ctxs[i]->lc != L || ctxs[i]->lrank != i)))
+			return fail(GCMX_ERR_INVALID_ARG, "contexts are not the ranks of one in-process group, in order");
+	std::vector<gcmx_status> st(n, GCMX_OK);
+	std::vector<std::string> msg(n);
+	auto run = [&](int i) {
+		for (int k = 0; k < steps && st[i] == GCMX_OK; k++) st[i] = gcmx_step(ctxs[i], tau);
+		if (st[i] == GCMX_OK) st[i] = gcmx_sync(ctxs[i]);
+		if (st[i] != GCMX_OK) {
+			msg[i] = g_last_error;
+			local_abort(ctxs[i], "rank " + std::to_string(i) + ": " + msg[i]);
+		}
+	};
+	std::vector<std::thread> th;
+	for (int i = 1; i < n; i++) th.emplace_back(run, i);
+	run(0);
+	for (auto& t : th) t.join();
+	for (int i = 0; i < n; i++)
+		if (st[i] != GCMX_OK) return fail(st[i], "rank " + std::to_string(i) + ": " + msg[i]);
+	return GCMX_OK;
+}
+
 gcmx_status gcmx_sync(gcmx_ctx* c) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
+	if (c->lc) {  // the exchange may run on a neighbour's comm stream: wait through the group
+		s = halo_wait(c);
+		if (s) return s;
+	}
 	HIP_TRY(hipStreamSynchronize(c->comm_stream));
 	HIP_TRY(hipStreamSynchronize(c->inner_stream));
 	HIP_TRY(hipStreamSynchronize(c->bnd_stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
-	c->halo_pending = false;  // the comm stream has drained
+	if (c->halo_pending) {  // the comm stream has drained
+		c->halo_pending = false;
+		c->halo_fresh = c->halo_layer == c->cur;
+	}
 	drain_timings(c);
 	return GCMX_OK;
 }

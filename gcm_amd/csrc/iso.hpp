@@ -237,4 +237,23 @@ struct PlanesW {
 	}
 };
 
+// Byte-offset form: the 32-bit per-lane offset is made opaque, so every access
+// is `global_load_dwordx2 v, v_off, s[base]` (SGPR base + 32-bit VGPR offset,
+// the global "saddr" form) and the components that share an offset share its
+// VGPR; otherwise hipcc tends to materialise 64-bit addresses
+// (v_lshl_add_u64 per load).  `boff` = element offset * 8 (< 2^32: planes are
+// < 2^32 bytes, fast_layout_ok).  The asm is not volatile, so equal offsets CSE.
+__device__ __forceinline__ unsigned opaque_u32(unsigned x) {
+	asm("" : "+v"(x));
+	return x;
+}
+__device__ __forceinline__ double ld_b(const Planes& p, int j, unsigned boff) {
+	typedef const __attribute__((address_space(1))) char* gcb;
+	return *reinterpret_cast<gcptr>(reinterpret_cast<gcb>(p.b[j]) + (unsigned long long)boff);
+}
+__device__ __forceinline__ void st_nt_b(const PlanesW& p, int j, unsigned boff, double v) {
+	typedef __attribute__((address_space(1))) char* gb;
+	__builtin_nontemporal_store(v, reinterpret_cast<gptr>(reinterpret_cast<gb>(p.b[j]) + (unsigned long long)boff));
+}
+
 }  // namespace gcmx

@@ -243,6 +243,12 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #ifndef GCMX_TX2_SLEEP  // NB: s_sleep argument while a neighbour wave's edges are not there yet
 #define GCMX_TX2_SLEEP 1
 #endif
+#ifndef GCMX_TX2_BUF  // buffer loads/stores: block-uniform offsets in SGPRs (no VALU address math)
+#define GCMX_TX2_BUF 1
+#endif
+#ifndef GCMX_TX2_XFIRST  // X stage of the entering row between the Z-edge publish and the poll
+#define GCMX_TX2_XFIRST 0
+#endif
 #ifndef GCMX_TX2_DIAG  // tuning builds only: per-wave phase cycle counters (s_memtime)
 #define GCMX_TX2_DIAG 0
 #endif
@@ -363,14 +369,32 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const unsigned stx = (unsigned)g.stride[0];
 	const unsigned sty = (unsigned)g.stride[1];
 	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
+	const unsigned zo = live ? (unsigned)z : (unsigned)Z;
+	// Memory accessors.  ldx(j, k, r): component j of plane x - BS + k (the last
+	// plane clamped when x + 1 is not ours), row r, this lane's column;
+	// stz(c, t, y, v): component c of node (x + t, y) of the output layer.
+#if GCMX_TX2_BUF
+	const Planes src(in, g.cs);
+	const PlanesW out_p(outl, g.cs);
+	const unsigned lv = (unsigned)zc * 8u, sv = zo * 8u;  // per-lane byte offsets
+	const unsigned pxm = plane - (unsigned)BS * stx;      // plane x - BS, row 0, column 0
+	auto ldx = [&](int j, int k, int r) {
+		const int d = (k == WX - 1 && !two) ? 2 * BS : k;
+		return ld_b(src, j, opaque_u32(lv + (pxm + (unsigned)d * stx + (unsigned)r * sty) * 8u));
+	};
+	auto stz = [&](int c, int t, int y, double v) {
+		st_nt_b(out_p, c, opaque_u32(sv + (plane + (unsigned)t * stx + (unsigned)y * sty) * 8u), v);
+	};
+#else
 	const unsigned base = plane + zc;
 	const Planes src(in, g.cs);
 	const PlanesW out_p(outl, g.cs);
-	// element offset of plane x - BS + k (the last one clamped when x + 1 is not ours)
-	auto xoff = [&](int k) {
+	auto ldx = [&](int j, int k, int r) {
 		const int d = (k == WX - 1 && !two) ? BS : k - BS;
-		return (unsigned)d * stx;
+		return src.ld(j, base + (unsigned)r * sty + (unsigned)d * stx);
 	};
+	auto stz = [&](int c, int t, int y, double v) { out_p.st_nt(c, plane + (unsigned)y * sty + zo + (unsigned)t * stx, v); };
+#endif
 	// ghost value of component j on face f: -inner + 2 f(t) if overridden, else the mirror
 	auto ghost = [&](int f, int j, double v) { return ((fb.mask[f] >> j) & 1u) ? -v + fb.two_v[f][j] : v; };
 
@@ -394,12 +418,12 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	}
 
 	typedef double PairWin[2][WX];  // [vel/sig][plane]
-	auto pair_load = [&](auto PC, PairWin& w, unsigned o) {
+	auto pair_load = [&](auto PC, PairWin& w, int r) {
 		constexpr int P = decltype(PC)::value;
 #pragma unroll
 		for (int k = 0; k < WX; k++) {
-			w[0][k] = src.ld(pair_vel(0, P), o + xoff(k));
-			w[1][k] = src.ld(pair_sig(0, P), o + xoff(k));
+			w[0][k] = ldx(pair_vel(0, P), k, r);
+			w[1][k] = ldx(pair_sig(0, P), k, r);
 		}
 	};
 	// Rows 2P, 2P+1 of r = diag(U * V) for both nodes.
@@ -465,26 +489,25 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	struct XPre {
 		PairWin a, b;
 	};
-	auto cv_load = [&](double (&cv)[2][9], unsigned o) {
+	auto cv_load = [&](double (&cv)[2][9], int r) {
 #pragma unroll
 		for (int t = 0; t < 2; t++)
 #pragma unroll
 			for (int j = 0; j < 9; j++)
-				if ((CMX >> j) & 1u) cv[t][j] = src.ld(j, o + (unsigned)t * stx);
+				if ((CMX >> j) & 1u) cv[t][j] = ldx(j, BS + t, r);
 	};
 	auto x_load_ahead = [&](XPre& pre, int r) {
-		pair_load(P0{}, pre.a, base + (unsigned)r * sty);
-		pair_load(P1{}, pre.b, base + (unsigned)r * sty);
+		pair_load(P0{}, pre.a, r);
+		pair_load(P1{}, pre.b, r);
 	};
 	// X stage of row r for both nodes: pair 2 and the node-only components are
 	// issued first, then the pairs are consumed in order.
 	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9]) {
-		const unsigned o = base + (unsigned)r * sty;
 		double rr[2][9], n0[2][9];
 		PairWin wc;
 		double cv[2][9];
-		pair_load(P2{}, wc, o);
-		cv_load(cv, o);
+		pair_load(P2{}, wc, r);
+		cv_load(cv, r);
 		sched_fence();
 		pair_rows(P0{}, pre.a, rr);
 		pair_rows(P1{}, pre.b, rr);
@@ -508,15 +531,18 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 
 	double win[2][NWY][W];
+	// node-only Y components: ring slot of row r; per-lane pointer with the
+	// (node, component) part as a constant LDS offset
+	auto cl_at = [&](int r) { return &cl[(r + BS) % (BS + 1)][0][0][z]; };
 	// row r's X result enters window slot `slot`; its node-only components go to the ring
 	auto push = [&](const double (&xr)[2][9], int slot, int r) {
-		const int ring = (r + BS) % (BS + 1);
+		double* cp = cl_at(r);
 #pragma unroll
 		for (int t = 0; t < 2; t++)
 #pragma unroll
 			for (int j = 0; j < 9; j++) {
 				if ((WMY >> j) & 1u) win[t][wslot(WMY, j)][slot] = xr[t][j];
-				if ((CMY >> j) & 1u) cl[ring][t][wslot(CMY, j)][z] = xr[t][j];
+				if ((CMY >> j) & 1u) cp[(t * NCY + wslot(CMY, j)) * ZT] = xr[t][j];
 			}
 	};
 	// window slot k := ghost of face f mirrored from window slot ks (a runtime
@@ -564,27 +590,30 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		}
 	}
 	auto clamp_row = [&](int r) { return r < Y + BS - 1 ? r : Y + BS - 1; };
-	const unsigned zo = live ? (unsigned)z : (unsigned)Z;
 
 #if GCMX_TX2_DIAG
 	unsigned long long dt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
 #endif
-	auto row = [&](int y) {
-		double yv[2][9];
-		const int ring = (y + BS) % (BS + 1);
-		XPre pre;
-		const int rn = clamp_row(y + BS + 1);
+	// Y stage of row y for both nodes (window + node-only ring)
+	auto y_stage = [&](int y, double (&yv)[2][9]) {
+		const double* cp = cl_at(y);
 #pragma unroll
 		for (int t = 0; t < 2; t++)
 			node_update<1, BS, KF0>(
 			    AY, [&](int j, int o) { return win[t][wslot(WMY, j)][BS + o]; },
-			    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cl[ring][t][wslot(CMY, j)][z]; },
+			    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cp[(t * NCY + wslot(CMY, j)) * ZT]; },
 			    yv[t]);
-		TX2_T(0);
+	};
+	// hand the Y results of row y to the Z stage: NB, own region + edge ring +
+	// counter; otherwise the block buffer between two barriers
+	auto publish = [&](int y, const double (&yv)[2][9]) {
 		const int es = y & 1;  // NB: edge ring slot of this row
 		if constexpr (NB) {
-			TX2_T(1);
+			// this lane's edge slot (lanes < BS: left side, >= 64 - BS: right side);
+			// (node, component) as a constant LDS offset
+			double* egp = ln < BS ? &eg[es][wv][0][0][0][ln] : &eg[es][wv][1][0][0][ln - (64 - BS)];
+			const bool edge = ln < BS || ln >= 64 - BS;
 			asm volatile("" ::: "memory");  // after the previous row's Z-stage reads of rg
 #pragma unroll
 			for (int t = 0; t < 2; t++)
@@ -598,16 +627,13 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 							if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
 								rg[NW - 1][t][q][BS + 2 * (Z - 1) - z - 64 * (NW - 1)] = ghost(3, j, yv[t][j]);
 						}
-						if (ln < BS) eg[es][wv][0][t][q][ln] = yv[t][j];
-						if (ln >= 64 - BS) eg[es][wv][1][t][q][ln - (64 - BS)] = yv[t][j];
+						if (edge) egp[(t * NWZ + q) * BS] = yv[t][j];
 					}
 			// edges in LDS before the counter says so (LDS only: global memory keeps flowing)
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			__hip_atomic_store(&rdy[wv], y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-			TX2_T(2);
 		} else {
 			__syncthreads();  // every wave has finished reading zl (previous row's Z stage)
-			TX2_T(1);
 #pragma unroll
 			for (int t = 0; t < 2; t++)
 #pragma unroll
@@ -625,12 +651,116 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 						}
 					}
 			__syncthreads();
-			TX2_T(2);
 		}
-		const unsigned offo = plane + (unsigned)y * sty + zo;
+	};
+	// NB: wait for the neighbour waves' edges of row y, copy them into the own halo slots
+	auto collect = [&](int y) {
+		if constexpr (NB && NW > 1) {
+			const int es = y & 1;
+			for (;;) {
+				const int a = wv > 0 ? __hip_atomic_load(&rdy[wv - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
+				const int b =
+				    wv < NW - 1 ? __hip_atomic_load(&rdy[wv + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
+				if (__builtin_amdgcn_readfirstlane(min(a, b)) >= y) break;
+				if constexpr (GCMX_TX2_SLEEP > 0) __builtin_amdgcn_s_sleep(GCMX_TX2_SLEEP);
+			}
+			asm volatile("" ::: "memory");
+			if (ln < BS && wv > 0) {
+#pragma unroll
+				for (int t = 0; t < 2; t++)
+#pragma unroll
+					for (int q = 0; q < NWZ; q++) rg[wv][t][q][ln] = eg[es][wv - 1][1][t][q][ln];
+			}
+			if (ln >= 64 - BS && wv < NW - 1) {
+#pragma unroll
+				for (int t = 0; t < 2; t++)
+#pragma unroll
+					for (int q = 0; q < NWZ; q++) rg[wv][t][q][ln + 2 * BS] = eg[es][wv + 1][0][t][q][ln - (64 - BS)];
+			}
+			asm volatile("" ::: "memory");
+		}
+	};
+	// Z stage of node t of row y and its 9 stores
+	auto z_stage_store = [&](int t, int y, const double (&yv)[2][9]) {
+		double zv[9];
+		if constexpr (NB)
+			node_update<2, BS, KF0>(
+			    AZ, [&](int j, int o) { return rg[wv][t][wslot(WMZ, j)][BS + ln + o]; },
+			    [&](int j) { return ((WMZ >> j) & 1u) ? rg[wv][t][wslot(WMZ, j)][BS + ln] : yv[t][j]; }, zv);
+		else
+			node_update<2, BS, KF0>(
+			    AZ, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
+			    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
+		if (t == 0 || two) {
+#pragma unroll
+			for (int c = 0; c < 9; c++) stz(c, t, y, live ? zv[c] : 0.0);
+		}
+	};
+	// X stage of row y+BS+1 -> window slot W-1 (ghost rows: zero, or the y+ face's mirror)
+	auto x_enter = [&](int y, const XPre& pre) {
+#pragma unroll
+		for (int t = 0; t < 2; t++)
+#pragma unroll
+			for (int q = 0; q < NWY; q++)
+#pragma unroll
+				for (int o = 0; o < W - 1; o++) win[t][q][o] = win[t][q][o + 1];
+		double xr[2][9];
+		sched_fence();
+		x_stage(pre, clamp_row(y + BS + 1), xr);
+		push(xr, W - 1, y + BS + 1);
+		sched_fence();
+		if constexpr (FACES) {
+			const int r = y + BS + 1;
+			if ((fb.on & 2u) && r >= Y) {
+				const int ks = 2 * (Y - 1) - r - (y - BS + 1);
+				if (ks >= 0) mirror_slot(W - 1, ks, 1);
+			}
+		}
+	};
+#if GCMX_TX2_XFIRST
+	// Row order: Y(y), publish the Z edges, X stage of the entering row (its two
+	// load pairs were issued one row ahead), issue the next row's pairs, then
+	// collect the neighbours' edges, Z stages and stores.  A whole X stage lies
+	// between a wave's publish and its poll, so the waves of a block rarely wait
+	// for each other; the pairs issued before the stores keep every vmcnt wait
+	// clear of the stores (loads and stores retire in order).
+	// GCMX_TX2_XFIRST == 2: only pair 0 is issued a row ahead (fewer live VGPRs
+	// across the Z stages); pair 1 is issued when the X stage starts.
+	XPre pre;
+	if constexpr (GCMX_TX2_XFIRST == 2) pair_load(P0{}, pre.a, clamp_row(yb + BS + 1));
+	else x_load_ahead(pre, clamp_row(yb + BS + 1));
+	auto row = [&](int y) {
+		double yv[2][9];
+		y_stage(y, yv);
+		TX2_T(0);
+		publish(y, yv);
+		TX2_T(1);
+		if constexpr (GCMX_TX2_XFIRST == 2) pair_load(P1{}, pre.b, clamp_row(y + BS + 1));
+		x_enter(y, pre);
+		TX2_T(5);
+		sched_fence();
+		if constexpr (GCMX_TX2_XFIRST == 2) pair_load(P0{}, pre.a, clamp_row(y + BS + 2));
+		else x_load_ahead(pre, clamp_row(y + BS + 2));
+		sched_fence();
+		TX2_T(6);
+		collect(y);
+		TX2_T(4);
+#pragma unroll
+		for (int t = 0; t < 2; t++) z_stage_store(t, y, yv);
+		TX2_T(3);
+	};
+#else
+	auto row = [&](int y) {
+		double yv[2][9];
+		XPre pre;
+		const int rn = clamp_row(y + BS + 1);
+		y_stage(y, yv);
+		TX2_T(0);
+		publish(y, yv);
+		TX2_T(2);
 		if constexpr (ZS2) {
 			sched_fence();
-			pair_load(P0{}, pre.a, base + (unsigned)rn * sty);
+			pair_load(P0{}, pre.a, rn);
 			sched_fence();
 		} else {  // loads older than this row's stores
 			sched_fence();
@@ -638,79 +768,37 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			sched_fence();
 		}
 		TX2_T(6);
-		if constexpr (NB) {
-			if constexpr (NW > 1) {  // neighbours' edges of this row -> own halo slots
-				for (;;) {
-					const int a = wv > 0 ? __hip_atomic_load(&rdy[wv - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
-					const int b =
-					    wv < NW - 1 ? __hip_atomic_load(&rdy[wv + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
-					if (__builtin_amdgcn_readfirstlane(min(a, b)) >= y) break;
-					if constexpr (GCMX_TX2_SLEEP > 0) __builtin_amdgcn_s_sleep(GCMX_TX2_SLEEP);
-				}
-				asm volatile("" ::: "memory");
-				if (ln < BS && wv > 0) {
-#pragma unroll
-					for (int t = 0; t < 2; t++)
-#pragma unroll
-						for (int q = 0; q < NWZ; q++) rg[wv][t][q][ln] = eg[es][wv - 1][1][t][q][ln];
-				}
-				if (ln >= 64 - BS && wv < NW - 1) {
-#pragma unroll
-					for (int t = 0; t < 2; t++)
-#pragma unroll
-						for (int q = 0; q < NWZ; q++) rg[wv][t][q][ln + 2 * BS] = eg[es][wv + 1][0][t][q][ln - (64 - BS)];
-				}
-			}
-			asm volatile("" ::: "memory");
-		}
+		collect(y);
 		TX2_T(4);
 #pragma unroll
 		for (int t = 0; t < 2; t++) {  // each node's stores right after its Z stage
 			if constexpr (ZS2) {
 				if (t == 1) {
 					sched_fence();
-					pair_load(P1{}, pre.b, base + (unsigned)rn * sty);
+					pair_load(P1{}, pre.b, rn);
 					sched_fence();
 				}
 			}
-			double zv[9];
-			if constexpr (NB)
-				node_update<2, BS, KF0>(
-				    AZ, [&](int j, int o) { return rg[wv][t][wslot(WMZ, j)][BS + ln + o]; },
-				    [&](int j) { return ((WMZ >> j) & 1u) ? rg[wv][t][wslot(WMZ, j)][BS + ln] : yv[t][j]; }, zv);
-			else
-				node_update<2, BS, KF0>(
-				    AZ, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
-				    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
-			if (t == 0 || two) {
-#pragma unroll
-				for (int c = 0; c < 9; c++) out_p.st_nt(c, offo + (unsigned)t * stx, live ? zv[c] : 0.0);
-			}
+			z_stage_store(t, y, yv);
 		}
 		TX2_T(3);
-		{  // X stage of row y+BS+1 -> window slot W-1 (ghost rows: zero, or the y+ face's mirror)
-#pragma unroll
-			for (int t = 0; t < 2; t++)
-#pragma unroll
-				for (int q = 0; q < NWY; q++)
-#pragma unroll
-					for (int o = 0; o < W - 1; o++) win[t][q][o] = win[t][q][o + 1];
-			double xr[2][9];
-			sched_fence();
-			x_stage(pre, rn, xr);
-			push(xr, W - 1, y + BS + 1);
-			sched_fence();
-			if constexpr (FACES) {
-				const int r = y + BS + 1;
-				if ((fb.on & 2u) && r >= Y) {
-					const int ks = 2 * (Y - 1) - r - (y - BS + 1);
-					if (ks >= 0) mirror_slot(W - 1, ks, 1);
-				}
-			}
-		}
+		x_enter(y, pre);
 		TX2_T(5);
 	};
-	for (int y = yb; y < ye; y++) row(y);
+#endif
+#ifndef GCMX_TX2_ROWUNROLL  // unroll the row loop (fewer window-rotation moves)
+#define GCMX_TX2_ROWUNROLL 1
+#endif
+	if constexpr (GCMX_TX2_ROWUNROLL == 2) {
+		int y = yb;
+		for (; y + 1 < ye; y += 2) {
+			row(y);
+			row(y + 1);
+		}
+		if (y < ye) row(y);
+	} else {
+		for (int y = yb; y < ye; y++) row(y);
+	}
 #if GCMX_TX2_DIAG
 	if ((threadIdx.x & 63) == 0) {
 		const int wv = threadIdx.x / 64;

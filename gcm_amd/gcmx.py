@@ -42,6 +42,7 @@ SYMBOLS = [
     "gcmx_copy_box",
     "gcmx_ode_maxwell",
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
+    "gcmx_comm_init_local", "gcmx_local_group_steps",
     "gcmx_sync", "gcmx_stream",
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_inner_nodes",
     "gcmx_all_nodes", "gcmx_device_bytes", "gcmx_copy_ceiling",
@@ -124,6 +125,8 @@ def lib() -> ctypes.CDLL:
                                  ctypes.c_int, ctypes.c_int]
     L.gcmx_halo_exchange.argtypes = [vp]
     L.gcmx_halo_exchange_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.gcmx_comm_init_local.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.gcmx_local_group_steps.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_double, ctypes.c_int]
     L.gcmx_sync.argtypes = [vp]
     L.gcmx_stream.argtypes = [vp]
     L.gcmx_stream.restype = vp
@@ -374,6 +377,21 @@ def halo_exchange_group(slabs: Sequence["Context"]):
     """Refresh X ghosts of in-process X slabs (ordered by increasing X)."""
     arr = (ctypes.c_void_p * len(slabs))(*[c.ptr.value for c in slabs])
     _check(lib().gcmx_halo_exchange_group(arr, len(slabs)))
+
+
+def comm_init_local(slabs: Sequence["Context"]):
+    """Make `slabs` (ordered by increasing X) the ranks of one in-process group:
+    the RCCL X-slab exchange with device copies (gcmx_comm_init_local).  Drive
+    them concurrently: local_group_steps, or one thread per context."""
+    arr = (ctypes.c_void_p * len(slabs))(*[c.ptr.value for c in slabs])
+    _check(lib().gcmx_comm_init_local(arr, len(slabs)))
+
+
+def local_group_steps(slabs: Sequence["Context"], tau: float, steps: int):
+    """`steps` gcmx_step calls on every context of an in-process group, one host
+    thread per context, then gcmx_sync (gcmx_local_group_steps)."""
+    arr = (ctypes.c_void_p * len(slabs))(*[c.ptr.value for c in slabs])
+    _check(lib().gcmx_local_group_steps(arr, len(slabs), float(tau), int(steps)))
 
 
 def unique_id() -> bytes:

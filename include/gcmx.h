@@ -212,6 +212,23 @@ gcmx_status gcmx_halo_exchange(gcmx_ctx* ctx);
  * any slab.  Call it before each time step, like the RCCL exchange. */
 gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n);
 
+/* In-process slab group: the RCCL X-slab exchange of gcmx_comm_init with
+ * device-to-device copies (hipMemcpyPeerAsync on the contexts' comm streams)
+ * instead of ncclSend/Recv, so the exchange code paths of gcmx_step (the
+ * X-slab schedule: the new boundary planes posted while the interior runs,
+ * the next step's boundary waiting for them) and of gcmx_stage(axis 0) run
+ * unchanged on one or several devices of one process.  ctxs[i] becomes rank i
+ * of n X-adjacent slabs (ordered by increasing X).  Like RCCL ranks, the
+ * contexts must be driven concurrently, one host thread each (a wait for a
+ * neighbour that never posts fails with GCMX_ERR_COMM after 60 s, or
+ * GCMX_LOCAL_WAIT_SECONDS); the
+ * semantics are those of the (dead) MPI slab design, src/test/TestMPI.cpp:33-50. */
+gcmx_status gcmx_comm_init_local(gcmx_ctx* const* ctxs, int n);
+/* Drive an in-process group: one host thread per context, each calling
+ * gcmx_step(ctxs[i], tau) `steps` times and then gcmx_sync.  The first failure
+ * aborts the group and is returned (with its rank in gcmx_last_error). */
+gcmx_status gcmx_local_group_steps(gcmx_ctx* const* ctxs, int n, double tau, int steps);
+
 /* ---- simplex (tetrahedral) stage ----------------------------------------------
  * The device half of simplex::GridCharacteristicMethodInRiemannInvariants
  * (engine/simplex/GridCharacteristicMethodInRiemannInvariants.hpp:44-198) for one

@@ -1,0 +1,232 @@
+"""BASELINE config 3 on one device: X slabs of one grid as the ranks of an
+in-process group (gcmx_comm_init_local), so the exchange code that RCCL drives
+on a multi-GPU node -- the X-slab step schedule (interior beside the boundary
+planes, the new boundary planes posted while the interior runs, the next step's
+boundary kernels waiting for them) and the per-stage exchange of the split path
+-- runs unchanged, with device copies in place of ncclSend/Recv.
+
+The reference's own check of its (dead) MPI slab design is slab == sequential,
+bitwise (src/test/TestMPI.cpp:92-155, ASSERT_EQ at :150; the exchange itself at
+:33-50); these tests compare the slabs with one undivided context or with the
+oracle, bitwise."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import oracle_body
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def G():
+    import gcm_amd.gcmx as G
+    try:
+        G.lib()
+    except Exception as e:  # pragma: no cover
+        pytest.fail(f"libgcmx.so not loadable: {e}")
+    return G
+
+
+def _mats():
+    from gcm_amd.host import isotropic_elastic_matrices
+    return isotropic_elastic_matrices(3, 4, 2, 1)
+
+
+def _group(G, xs, Y, Z, seed, sched=None, path=None):
+    """Contexts for X slabs of widths `xs` of an (sum(xs), Y, Z) grid, one group."""
+    import gcm_amd
+    U, U1, L = _mats()
+    Xg = sum(xs)
+    out, x0 = [], 0
+    for X in xs:
+        c = gcm_amd.Context(3, 2, [X, Y, Z], start=[x0, 0, 0])
+        c.set_materials(U[None], U1[None], L[None])
+        c.fill_random([Xg, Y, Z], seed)
+        if sched is not None:
+            c.set_schedule(sched)
+        if path is not None:
+            c.set_path(path)
+        out.append(c)
+        x0 += X
+    G.comm_init_local(out)
+    return out
+
+
+def _whole(G, X, Y, Z, seed, path=None):
+    import gcm_amd
+    U, U1, L = _mats()
+    c = gcm_amd.Context(3, 2, [X, Y, Z])
+    c.set_materials(U[None], U1[None], L[None])
+    c.fill_random([X, Y, Z], seed)
+    if path is not None:
+        c.set_path(path)
+    return c
+
+
+def _inner(c, arr, bs=2):
+    return arr.reshape(tuple(s + 2 * bs for s in c.sizes) + (9,))[bs:-bs, bs:-bs, bs:-bs]
+
+
+def _concat(slabs):
+    return np.concatenate([_inner(c, c.download()) for c in slabs], axis=0)
+
+
+def _run_threads(fns):
+    """One host thread per rank, as RCCL ranks run (ctypes releases the GIL)."""
+    errs = [None] * len(fns)
+
+    def go(i):
+        try:
+            fns[i]()
+        except Exception as e:  # reported below
+            errs[i] = e
+    th = [threading.Thread(target=go, args=(i,)) for i in range(len(fns))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+@pytest.mark.parametrize("sched", ["auto", "single", "xslab"])
+@pytest.mark.parametrize("xs", [[17, 23], [12, 9, 19]])
+def test_local_group_fused_equals_whole(G, sched, xs):
+    """Ragged slabs on the fused path: the X-slab schedule (auto: a configured
+    exchange selects it) with the in-step overlapped exchange, and the one-launch
+    schedule with the exchange in front; 4 steps == one context, bitwise."""
+    Y, Z, seed, steps = 40, 64, 0x5EED, 4
+    sc = {"auto": None, "single": G.SCHED_SINGLE, "xslab": G.SCHED_XSLAB}[sched]
+    slabs = _group(G, xs, Y, Z, seed, sched=sc)
+    whole = _whole(G, sum(xs), Y, Z, seed)
+    G.local_group_steps(slabs, 0.9, steps)
+    for _ in range(steps):
+        whole.step(0.9)
+    assert all(c.last_path == "fused" for c in slabs)
+    want = _inner(whole, whole.download())
+    assert np.array_equal(_concat(slabs), want)
+    for c in slabs + [whole]:
+        c.close()
+
+
+def test_local_group_split_path_per_stage_exchange(G):
+    """Split path (gcmx_stage per axis): the X stage's halo is exchanged inside
+    stage(0) (halo_ensure), per stage, as gcmx_stage with a communicator does."""
+    xs, Y, Z, seed, steps = [10, 14, 8], 24, 40, 0x5EED, 3
+    slabs = _group(G, xs, Y, Z, seed, path=G.PATH_SPLIT)
+    whole = _whole(G, sum(xs), Y, Z, seed, path=G.PATH_SPLIT)
+
+    def stepper(c):
+        def f():
+            for _ in range(steps):
+                for s in range(3):
+                    c.stage(s, 0.9)
+            c.sync()
+        return f
+    _run_threads([stepper(c) for c in slabs])
+    for _ in range(steps):
+        for s in range(3):
+            whole.stage(s, 0.9)
+    assert all(c.last_path == "split" for c in slabs)
+    assert np.array_equal(_concat(slabs), _inner(whole, whole.download()))
+    for c in slabs + [whole]:
+        c.close()
+
+
+@pytest.mark.parametrize("path", ["fused", "split"])
+def test_local_group_with_x_faces(G, path):
+    """Free-surface and force conditions on all six faces (gcmx_step_faces): the
+    x faces belong to the outer slabs only, the inner X boundaries are halos; the
+    fused path forms the y/z face ghosts in the one pass, the split path fills
+    every face per stage and exchanges the halo inside stage(0)."""
+    xs, Y, Z, seed, steps = [11, 13], 30, 48, 0x5EED, 3
+    p = G.PATH_FUSED if path == "fused" else G.PATH_SPLIT
+    slabs = _group(G, xs, Y, Z, seed, path=p)
+    whole = _whole(G, sum(xs), Y, Z, seed, path=p)
+    q = G.QUANTITY_CODES
+    free = [(q["Sxx"], 0.0), (q["Sxy"], 0.0), (q["Sxz"], 0.0)]
+    pull = [(q["Syy"], -0.25), (q["Syz"], 0.0)]
+    faces_all = [free, free, pull, pull, [(q["Vz"], 0.0)], [(q["Szz"], 0.5)]]
+
+    def faces_for(r):
+        f = list(faces_all)
+        if r > 0:
+            f[0] = None
+        if r < len(xs) - 1:
+            f[1] = None
+        return f
+
+    def stepper(r, c):
+        def f():
+            for _ in range(steps):
+                c.step_faces(0.9, faces_for(r))
+            c.sync()
+        return f
+    _run_threads([stepper(r, c) for r, c in enumerate(slabs)])
+    for _ in range(steps):
+        whole.step_faces(0.9, faces_all)
+    assert whole.last_path == path and all(c.last_path == path for c in slabs)
+    assert np.array_equal(_concat(slabs), _inner(whole, whole.download()))
+    for c in slabs + [whole]:
+        c.close()
+
+
+@pytest.mark.timeout(60)
+def test_local_group_unpaired_rank_times_out(G, monkeypatch):
+    """A rank whose neighbour never steps fails with GCMX_ERR_COMM (the wait is
+    bounded) instead of reading stale ghosts."""
+    monkeypatch.setenv("GCMX_LOCAL_WAIT_SECONDS", "2")
+    slabs = _group(G, [8, 8], 16, 32, 1)
+    with pytest.raises(G.GcmxError) as ei:
+        slabs[0].step(0.9)
+    assert ei.value.status == 7  # GCMX_ERR_COMM
+    for c in slabs:
+        c.close()
+
+
+def _oracle_steps(X, Y, Z, seed, steps):
+    b = oracle_body(3, 2, [X, Y, Z])
+    O.fill_random(b, [X, Y, Z], seed)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    for _ in range(steps):
+        for s in range(3):
+            b.stage(s, 0.9, threads)
+    return b.inner_view()
+
+
+@pytest.mark.timeout(600)
+def test_local_group_two_64x512x512_slabs_match_oracle(G):
+    """Config 3's slab shape (512^3 over 8 GPUs = 64 x 512 x 512 per rank): two
+    such ranks in one group, 2 steps with the overlapped in-step exchange, ==
+    the oracle on the undivided 128 x 512 x 512 box, bitwise."""
+    X, Y, Z, seed, steps = 64, 512, 512, 0x5EED, 2
+    slabs = _group(G, [X, X], Y, Z, seed)
+    G.local_group_steps(slabs, 0.9, steps)
+    assert all(c.last_path == "fused" for c in slabs)
+    got = _concat(slabs)
+    for c in slabs:
+        c.close()
+    assert np.array_equal(got, _oracle_steps(2 * X, Y, Z, seed, steps))
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_local_group_eight_slabs_whole_512_match_oracle(G):
+    """The whole config-3 decomposition on one device: 512^3 as eight 64 x 512
+    x 512 ranks (about 22 GB of layers), 2 steps with the overlapped in-step
+    exchange, == the oracle on the undivided 512^3 grid, bitwise."""
+    X, N, seed, steps = 64, 512, 0x5EED, 2
+    slabs = _group(G, [X] * 8, N, N, seed)
+    G.local_group_steps(slabs, 0.9, steps)
+    assert all(c.last_path == "fused" for c in slabs)
+    got = _concat(slabs)
+    for c in slabs:
+        c.close()
+    want = _oracle_steps(N, N, N, seed, steps)
+    for r in range(8):
+        assert np.array_equal(got[r * X:(r + 1) * X], want[r * X:(r + 1) * X]), f"slab {r}"
