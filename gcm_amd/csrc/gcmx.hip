@@ -1440,12 +1440,23 @@ size_t gcmx_device_bytes(gcmx_ctx* c) { return c ? 2 * c->layer_elems * sizeof(d
 }  // extern "C"
 
 namespace {
+// The yardstick copy: 16 B per lane per access, four independent 16-B loads in
+// flight per lane before their stores (grid-stride over 64-B lane chunks),
+// non-temporal stores; a 2048-block grid (8 per CU).
 typedef double copy_d2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_copy_ceiling(const copy_d2* __restrict__ in, copy_d2* __restrict__ out,
                                                       long long n2) {
-	const long long stride = (long long)gridDim.x * blockDim.x;
-	for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride)
-		__builtin_nontemporal_store(in[i], out + i);
+	const long long nth = (long long)gridDim.x * blockDim.x;
+	const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	long long i = t;
+	for (; i + 3 * nth < n2; i += 4 * nth) {
+		const copy_d2 a = in[i], b = in[i + nth], c = in[i + 2 * nth], d = in[i + 3 * nth];
+		__builtin_nontemporal_store(a, out + i);
+		__builtin_nontemporal_store(b, out + i + nth);
+		__builtin_nontemporal_store(c, out + i + 2 * nth);
+		__builtin_nontemporal_store(d, out + i + 3 * nth);
+	}
+	for (; i < n2; i += nth) __builtin_nontemporal_store(in[i], out + i);
 }
 }  // namespace
 
@@ -1471,7 +1482,7 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 	} else {
 		for (int r = 0; r <= reps && st == GCMX_OK; r++) {
 			hipEventRecord(e0, c->stream);
-			hipLaunchKernelGGL(k_copy_ceiling, dim3(32768), dim3(256), 0, c->stream,
+			hipLaunchKernelGGL(k_copy_ceiling, dim3(2048), dim3(256), 0, c->stream,
 			                   static_cast<const copy_d2*>(a), static_cast<copy_d2*>(b), n2);
 			hipEventRecord(e1, c->stream);
 			float t = 0.0f;

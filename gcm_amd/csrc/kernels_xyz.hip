@@ -249,6 +249,9 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #ifndef GCMX_TX2_XFIRST  // X stage of the entering row between the Z-edge publish and the poll
 #define GCMX_TX2_XFIRST 0
 #endif
+#ifndef GCMX_TX2_PROBE_NOX
+#define GCMX_TX2_PROBE_NOX 0
+#endif
 #ifndef GCMX_TX2_DIAG  // tuning builds only: per-wave phase cycle counters (s_memtime)
 #define GCMX_TX2_DIAG 0
 #endif
@@ -379,6 +382,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const unsigned lv = (unsigned)zc * 8u, sv = zo * 8u;  // per-lane byte offsets
 	const unsigned pxm = plane - (unsigned)BS * stx;      // plane x - BS, row 0, column 0
 	auto ldx = [&](int j, int k, int r) {
+#if GCMX_TX2_PROBE_NOX  // timing probe only (wrong results): x-neighbour loads re-read the own planes
+		k = k < BS ? BS : (k > BS + 1 ? BS + 1 : k);
+#endif
 		const int d = (k == WX - 1 && !two) ? 2 * BS : k;
 		return ld_b(src, j, opaque_u32(lv + (pxm + (unsigned)d * stx + (unsigned)r * sty) * 8u));
 	};
