@@ -46,6 +46,10 @@ def parse():
                    help="skip the flat-copy measurement reported beside the roofline")
     p.add_argument("--no-profile", action="store_true",
                    help="no hipEvent bracketing of the launches in the timed repetitions")
+    p.add_argument("--emulate-slabs", type=int, default=0, metavar="K",
+                   help="one GPU: split the grid into K X-slab contexts of one in-process group "
+                        "(gcmx_comm_init_local: the X-slab step schedule with its overlapped "
+                        "in-step exchange, device copies instead of RCCL), one host thread each")
     return p.parse_args()
 
 
@@ -114,6 +118,38 @@ def copy_ceiling(ctx, step_bytes, achieved_gbps):
                    f"bytes counted read + write"}
 
 
+def lib_sha256() -> str:
+    """Digest of the libgcmx.so this process loaded (gcm_amd.gcmx.LIB_PATH)."""
+    import hashlib
+    from gcm_amd import gcmx
+    with open(gcmx.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic(n, ranks, bucket, symbol):
+    """HBM bytes per launch from profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes, tools/pmc_traffic.py), used only when that profile was
+    taken of THIS library build (sha256), the same grid, rank count and kernel
+    instance; otherwise (None, reason)."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc):
+        return None, "no PMC profile"
+    try:
+        rec = json.load(open(pmc))
+    except Exception as e:
+        return None, f"unreadable PMC profile: {e}"
+    k = rec.get("kernels", {}).get(bucket)
+    if not k:
+        return None, f"PMC profile has no '{bucket}' kernel"
+    if rec.get("n") != n or rec.get("ranks", 1) != ranks:
+        return None, "PMC profile of another grid / rank count"
+    if k.get("symbol") != symbol:
+        return None, f"PMC profile of another kernel instance ({k.get('symbol')})"
+    if rec.get("lib_sha256") != lib_sha256():
+        return None, "PMC profile of another libgcmx.so build"
+    return k.get("hbm_bytes_per_launch"), f"{rec.get('source')} (same build, sha256 match)"
+
+
 def multi_gpu_parity(dist, world, rank, device, U, U1, L):
     """N > 1 self-check of the RCCL X-slab path (halo exchange overlapped with the
     interior X stage): 3 steps on a 12*N x 40 x 64 grid split into N slabs must
@@ -153,8 +189,94 @@ def multi_gpu_parity(dist, world, rank, device, U, U1, L):
     return {"ok": res[0], "grid": [Xg, Y, Z], "slabs": world, "steps": 3, "path": path}
 
 
+def emulate_slabs(a):
+    """--emulate-slabs K on one GPU: the config-3 decomposition (K X slabs of the
+    N^3 grid) as the ranks of an in-process group, so every step runs the exact
+    code RCCL ranks run -- interior beside the boundary planes, the new boundary
+    planes posted while the interior runs, the next step's boundary waiting for
+    them -- with device copies for the exchange.  All K slabs share the one GPU,
+    so the group's step time is the sum of K ranks' work plus the copies; the
+    per-rank figure divides it by K (the chip is work-conserving across the
+    slabs' streams).  Compared with one undivided context on the same GPU."""
+    import gcm_amd
+    from gcm_amd import gcmx
+    from gcm_amd.host import isotropic_elastic_matrices
+    N, K = a.n, a.emulate_slabs
+    if N % K:
+        raise SystemExit("grid edge must be divisible by the number of slabs")
+    X = N // K
+    U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
+    tau = 0.9
+    slabs = []
+    for r in range(K):
+        c = gcm_amd.Context(3, 2, [X, N, N], start=[r * X, 0, 0], device=0)
+        c.set_materials(U[None], U1[None], L[None])
+        c.fill_random([N, N, N], 0x5EED)
+        slabs.append(c)
+    gcmx.comm_init_local(slabs)
+    gcmx.local_group_steps(slabs, tau, max(1, a.warmup))
+    for c in slabs:
+        c.profile(True)
+        c.profile_reset()
+    rep_s = []
+    for _ in range(max(1, a.reps)):
+        t0 = time.perf_counter()
+        gcmx.local_group_steps(slabs, tau, a.steps)  # ends with every slab synced
+        rep_s.append(time.perf_counter() - t0)
+    kern = {}
+    for c in slabs:
+        for k, v in c.profile_read().items():
+            d = kern.setdefault(k, {"total_ms": 0.0, "launches": 0, "kernel": v["kernel"]})
+            d["total_ms"] += v["total_ms"]
+            d["launches"] += v["launches"]
+    paths = sorted({c.last_path for c in slabs})
+    for c in slabs:
+        c.close()
+    el = sorted(rep_s)[len(rep_s) // 2]
+    # the same grid as one context, same GPU, same repetitions
+    w = gcm_amd.Context(3, 2, [N, N, N], device=0)
+    w.set_materials(U[None], U1[None], L[None])
+    w.fill_random([N, N, N], 0x5EED)
+    for _ in range(max(1, a.warmup)):
+        w.step(tau)
+    w.sync()
+    whole = []
+    for _ in range(max(1, a.reps)):
+        w.sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            w.step(tau)
+        w.sync()
+        whole.append(time.perf_counter() - t0)
+    w.close()
+    ew = sorted(whole)[len(whole) // 2]
+    ms = el / a.steps * 1e3
+    msw = ew / a.steps * 1e3
+    out = {
+        "metric": "Mnode-steps/sec, 3D isotropic elastic CubicGrid, X-slab group emulated on one GPU",
+        "value": round(N ** 3 * a.steps / el / 1e6, 1), "unit": "Mnode-steps/s", "n_gpus": 1,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4),
+        "rep_ms_per_step": [round(r / a.steps * 1e3, 4) for r in rep_s],
+        "higher_is_better": True, "dtype": "f64", "data": "synthetic parity-random field (seed 0x5EED)",
+        "config": {"workload": f"3-D isotropic elastic CubicGrid {N}^3 as {K} X slabs of {X} x {N} x {N}, "
+                               f"borderSize 2, tau 0.9", "slabs": K, "paths": paths,
+                   "parallelism": f"x-slab{K} in-process group on one GPU (gcmx_comm_init_local, "
+                                  f"one host thread per slab, device-copy exchange)"},
+        "per_rank_ms_per_step": round(ms / K, 4),
+        "whole_grid_ms_per_step": round(msw, 4),
+        "decomposition_overhead": round(ms / msw, 4),
+        "projected_speedup_if_exchange_hidden": round(K * msw / ms, 3),
+        "kernels": {k: {"avg_ms": round(v["total_ms"] / max(1, v["launches"]), 4),
+                        "launches_per_step": round(v["launches"] / (a.steps * max(1, a.reps)), 2),
+                        "kernel": v["kernel"]} for k, v in kern.items()},
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse()
+    if a.emulate_slabs:
+        return emulate_slabs(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -246,24 +368,13 @@ def main():
         dom_name, dom = max(kernels.items(), key=lambda kv: kv[1]["total_ms"])
         avg_ms = dom["total_ms"] / max(1, dom["launches"])
         achieved = dom["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                rec = json.load(open(pmc))
-                k = rec.get("kernels", {}).get(dom_name)
-                if k and rec.get("n") == N and rec.get("ranks", 1) == world:
-                    traffic = k.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic, traffic_src = pmc_traffic(N, world, dom_name, dom["kernel"])
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": dom_name, "kernel_avg_ms": round(avg_ms, 4),
-                # the library's "fused_xyz" bucket is the one-pass step; with bs 2 and
-                # Z <= 512 it launches k_step_tx2 (kernels_xyz.hip), else k_fused_xyz
-                "kernel_symbol": ("k_step_tx2<2, 512, KF0, UNI, !FACES>" if N <= 512
-                                  else "k_fused_xyz<2, 1024, KF0, UNI>")
-                if dom_name.startswith("fused_xyz") else dom_name,
+                # the instance the library reports it launched (gcmx_profile_kernel)
+                "kernel_symbol": dom["kernel"],
                 "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
                 "kernels": {k: {"avg_ms": round(v["total_ms"] / max(1, v["launches"]), 4),
                                 "GBps": round(v["bytes_per_launch"] /
@@ -285,7 +396,7 @@ def main():
             log(f"cpu baseline failed: {e}")
 
     if rank == 0:
-        step_bytes = 3 * BYTES_PER_NODE_STAGE * total_nodes  # per-stage algorithmic model
+        step_bytes = 3 * BYTES_PER_NODE_STAGE * total_nodes  # three separate stage passes
         out = {
             "metric": "Mnode-steps/sec + achieved HBM GB/s, 3D isotropic elastic 512³ CubicGrid",
             "value": round(value, 1),
@@ -305,7 +416,9 @@ def main():
                                    f"Courant 0.9, tau 0.9, one full time step (3 stages)",
                        "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,
                        "parallelism": f"x-slab{world}" if world > 1 else "single"},
-            "effective_GBps_per_stage_model": round(step_bytes * a.steps / el / 1e9, 1),
+            # NOT an HBM rate: the bytes three separate stage passes (SURVEY §8d, 432 B per
+            # node-step) would move, over the measured step time; the one-pass step moves 144 B
+            "equivalent_GBps_if_three_stage_passes": round(step_bytes * a.steps / el / 1e9, 1),
             "roofline": roof,
             "cpu_baseline": cpu,
             "multi_gpu_parity": parity,

@@ -57,7 +57,8 @@ struct Bucket {
 	std::string name;
 	double total_ms = 0;
 	long long launches = 0;
-	double bytes = 0;  // algorithmic bytes summed over all timed launches
+	double bytes = 0;    // algorithmic bytes summed over all timed launches
+	std::string kernel;  // the instance the last launch of the bucket ran
 };
 
 }  // namespace
@@ -179,6 +180,7 @@ struct Timed {
 	double bytes;
 	hipEvent_t a = nullptr, e = nullptr;
 	hipStream_t st;
+	const char* kname = nullptr;  // set by the launcher: the instance it ran
 	Timed(gcmx_ctx* c_, const char* name, double bytes_, hipStream_t s)
 	    : c(c_), b(-1), bytes(bytes_), st(s) {
 		if (!c->prof) return;
@@ -191,6 +193,7 @@ struct Timed {
 		if (b < 0) return;
 		hipEventRecord(e, st);
 		c->pending.push_back({b, bytes, a, e});
+		if (kname) c->buckets[b].kernel = kname;
 	}
 };
 
@@ -540,12 +543,15 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	if (p == GCMX_PATH_GENERIC) {
 		Timed t(c, "stage_generic", bytes, c->stream);
 		ok = launch_stage_generic(c->cur, c->nxt, g, axis, c->tabs_d, c->mat_d, c->stream);
+		t.kname = "k_stage_generic";
 	} else if (axis < 2) {
 		Timed t(c, axis == 0 ? "march_x" : "march_y", bytes, c->stream);
 		ok = launch_march(c->cur, c->nxt, g, axis, c->iso[axis], 0, g.sizes[0], c->stream);
+		t.kname = axis == 0 ? "k_march<0>" : "k_march<1>";
 	} else {
 		Timed t(c, "line_z", bytes, c->stream);
 		ok = launch_line_z(c->cur, c->nxt, g, c->iso[2], 0, g.sizes[0], c->stream);
+		t.kname = "k_line_z";
 	}
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "no kernel variant for this configuration");
 	HIP_TRY(hipGetLastError());
@@ -906,7 +912,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 	const bool halo = has_halo(c);
 	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows) {
 		Timed t(c, name, plane_bytes * (x1 - x0), st);
-		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb);
+		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb, &t.kname);
 	};
 	const gcmx_schedule sched =
 	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_XSLAB : GCMX_SCHED_SINGLE) : c->sched;
@@ -1431,6 +1437,11 @@ int gcmx_profile_read(gcmx_ctx* c, int index, const char** name, double* total_m
 			*bytes = c->buckets[index].launches ? c->buckets[index].bytes / c->buckets[index].launches : 0;
 	}
 	return n;
+}
+
+const char* gcmx_profile_kernel(gcmx_ctx* c, int index) {
+	if (!c || index < 0 || index >= (int)c->buckets.size()) return "";
+	return c->buckets[index].kernel.c_str();
 }
 
 long long gcmx_inner_nodes(gcmx_ctx* c) { return c ? c->geo.n_inner : 0; }

@@ -5,6 +5,7 @@
 #include "iso.hpp"
 
 #include <cstring>
+#include <string>
 #include <type_traits>
 
 namespace gcmx {
@@ -820,6 +821,21 @@ static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
 	return std::memcmp(&p, &q, sizeof(IsoAxis)) == 0;
 }
 
+// The instance a launch runs, as a readable symbol (gcmx_profile_kernel).
+template <int BS, int ZT, bool KF0, bool UNI, bool FACES>
+static const char* tx2_name() {
+	static const std::string s = "k_step_tx2<" + std::to_string(BS) + ", " + std::to_string(ZT) + ", " +
+	                             (KF0 ? "KF0" : "!KF0") + ", " + (UNI ? "UNI" : "!UNI") + ", " +
+	                             (FACES ? "FACES" : "!FACES") + ">";
+	return s.c_str();
+}
+template <int BS, int ZT, bool KF0, bool UNI>
+static const char* xyz_name() {
+	static const std::string s = "k_fused_xyz<" + std::to_string(BS) + ", " + std::to_string(ZT) + ", " +
+	                             (KF0 ? "KF0" : "!KF0") + ", " + (UNI ? "UNI" : "!UNI") + ">";
+	return s.c_str();
+}
+
 // Rows per block (k_fused_xyz): GCMX_XYZ_CHUNK (128) while the launch still has >= 1024 blocks
 // (two rounds of the 512 resident blocks, 2 per CU); thinner slabs (multi-GPU
 // X slabs, the boundary planes) halve it, down to 16 rows, to keep every CU
@@ -834,7 +850,7 @@ static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK
 
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                         int x1, hipStream_t st, int req_chunk, const FaceBC* fb) {
+                         int x1, hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname) {
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
 	const bool uni = kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
@@ -847,43 +863,48 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair);
 			const FaceBC none{};
 			const FaceBC& f = fb ? *fb : none;
-			auto go = [&](auto K) {
+			auto go = [&](auto K, const char* name) {
 				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, f);
+				*kname = name;
 			};
 			if (fb) {
-				if (uni) go(k_step_tx2<BS, ZT, true, true, true>);
-				else if (kf0) go(k_step_tx2<BS, ZT, true, false, true>);
-				else go(k_step_tx2<BS, ZT, false, false, true>);
+				if (uni) go(k_step_tx2<BS, ZT, true, true, true>, tx2_name<BS, ZT, true, true, true>());
+				else if (kf0) go(k_step_tx2<BS, ZT, true, false, true>, tx2_name<BS, ZT, true, false, true>());
+				else go(k_step_tx2<BS, ZT, false, false, true>, tx2_name<BS, ZT, false, false, true>());
 			} else {
-				if (uni) go(k_step_tx2<BS, ZT, true, true, false>);
-				else if (kf0) go(k_step_tx2<BS, ZT, true, false, false>);
-				else go(k_step_tx2<BS, ZT, false, false, false>);
+				if (uni) go(k_step_tx2<BS, ZT, true, true, false>, tx2_name<BS, ZT, true, true, false>());
+				else if (kf0) go(k_step_tx2<BS, ZT, true, false, false>, tx2_name<BS, ZT, true, false, false>());
+				else go(k_step_tx2<BS, ZT, false, false, false>, tx2_name<BS, ZT, false, false, false>());
 			}
 			return;
 		}
 	}
 	const int chunk = xyz_chunk_for(g.sizes[1], x1 - x0, req_chunk);
 	const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * (x1 - x0));
-	if (uni)
-		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true, true>), grid, dim3(ZT), 0, st, in, out, g, a[0],
-		                   a[1], a[2], x0, chunk, x1 - x0);
-	else if (kf0)
-		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true, false>), grid, dim3(ZT), 0, st, in, out, g, a[0],
-		                   a[1], a[2], x0, chunk, x1 - x0);
-	else
-		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, false, false>), grid, dim3(ZT), 0, st, in, out, g,
-		                   a[0], a[1], a[2], x0, chunk, x1 - x0);
+	if (uni) {
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true, true>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk, x1 - x0);
+		*kname = xyz_name<BS, ZT, true, true>();
+	} else if (kf0) {
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, true, false>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk, x1 - x0);
+		*kname = xyz_name<BS, ZT, true, false>();
+	} else {
+		hipLaunchKernelGGL((k_fused_xyz<BS, ZT, false, false>), grid, dim3(ZT), 0, st, in, out, g, a[0], a[1],
+		                   a[2], x0, chunk, x1 - x0);
+		*kname = xyz_name<BS, ZT, false, false>();
+	}
 }
 
 template <int BS>
 static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                          int x1, hipStream_t st, int ch, const FaceBC* fb) {
+                          int x1, hipStream_t st, int ch, const FaceBC* fb, const char** kn) {
 	const int Z = g.sizes[2];
-	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st, ch, fb);
-	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st, ch, fb);
-	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st, ch, fb);
-	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st, ch, fb);
-	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st, ch, fb);
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st, ch, fb, kn);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st, ch, fb, kn);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st, ch, fb, kn);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st, ch, fb, kn);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st, ch, fb, kn);
 	return true;
 }
 
@@ -901,13 +922,15 @@ bool fused_faces_supported(const Geo& g) {
 }
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                      int x1, hipStream_t st, int chunk, const FaceBC* faces) {
+                      int x1, hipStream_t st, int chunk, const FaceBC* faces, const char** kname) {
+	const char* dummy = nullptr;
+	const char** kn = kname ? kname : &dummy;
 	if (!fused_supported(g) || x1 <= x0) return false;
 	if (faces && !fused_faces_supported(g)) return false;
 	switch (g.bs) {
-	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk, faces);
-	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk, faces);
-	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st, chunk, faces);
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk, faces, kn);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk, faces, kn);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st, chunk, faces, kn);
 	default: return false;
 	}
 }

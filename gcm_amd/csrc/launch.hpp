@@ -66,7 +66,9 @@ bool fused_faces_supported(const Geo& g);
 // One pass per time step: X, Y, Z stages of planes [x0, x1), `a` = the three axes.
 // `chunk`: y rows per block (0 = automatic, kernels_xyz.hip: xyz_chunk_for).
 // `faces`: y/z face conditions (null: y/z ghosts of both layers are zero).
+// `kname`: set to the launched instance's symbol (a static string).
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                      int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr);
+                      int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,
+                      const char** kname = nullptr);
 
 }  // namespace gcmx

@@ -85,6 +85,7 @@ struct StageDev {
 	// border list, and no border foot reads wn: the stage may run as one launch
 	// (k_sx_stage_l8) whose inner groups wait for exactly those border nodes
 	bool fusable = false;
+	int waitFeet = 0;  // inner feet that wait for border nodes in the one-launch stage
 	// border corrector records by position t in `border` (k_sx_border_rec): plan
 	// entry, condition, outer code, which sides are solvable; B; B * Omega and det
 	int4* rec = nullptr;
@@ -125,6 +126,7 @@ struct gsx_ctx {
 	int fuseMode = 1;  // gsx_set_stage_fusion: 0 never, 1 border + inner, 2 gradient + border + inner,
 	                   // 3 border + inner without the grid-size cap (tuning)
 	bool lastFused = false;  // the last gsx_stage ran as one launch
+	int waitBudget = 1 << 20;  // polls per device wait (gsx_set_wait_budget)
 };
 
 // The host-side state a simplex step changes (pointer swaps, chaining flag).
@@ -733,6 +735,7 @@ struct StageWait {
 	unsigned gtarget;   // gcount once this launch's gradient blocks are done
 	int epoch;
 	int* err;
+	int budget;         // polls before a wait gives up (gsx_set_wait_budget; < 0: every wait reports a timeout)
 };
 // Hand-offs inside k_sx_stage_l8 (cdna_hip_programming.md Guideline 16, the
 // write-through form): every handed-off byte (gradients, wn) is stored sc1 by its
@@ -741,10 +744,17 @@ struct StageWait {
 // the consumer needs no agent acquire (whose L1 invalidate costs ~1.7 us per wave),
 // only a wavefront-scope fence that keeps the compiler from moving the loads above
 // the poll.
+// A wait that gives up sets a bit of the context's error word and goes on (the
+// grid must drain); the word stays set until gsx_sync or gsx_download reports
+// it, so no result of a timed-out stage reaches the host as GCMX_OK.
 __device__ __forceinline__ void wait_flag(const StageWait& sw, const int* flags, int node) {
+	if (sw.budget < 0) {  // test hook: report a timeout without waiting
+		atomicOr(sw.err, 1);
+		return;
+	}
 	int polls = 0;
 	while (__hip_atomic_load(flags + node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sw.epoch) {
-		if (++polls > (1 << 20)) {
+		if (++polls > sw.budget) {
 			atomicOr(sw.err, 1);
 			break;
 		}
@@ -758,9 +768,13 @@ __device__ __forceinline__ void wait_flag(const StageWait& sw, const int* flags,
 #define GCMX_SX_GPOLL_SLEEP 2
 #endif
 __device__ __forceinline__ void wait_gradients(const StageWait& sw) {
+	if (sw.budget < 0) {  // test hook: report a timeout without waiting
+		atomicOr(sw.err, 2);
+		return;
+	}
 	int polls = 0;
 	while ((int)(__hip_atomic_load(sw.gcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - sw.gtarget) < 0) {
-		if (++polls > (1 << 20)) {
+		if (++polls > sw.budget) {
 			atomicOr(sw.err, 2);
 			break;
 		}
@@ -800,7 +814,7 @@ __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const
                                              const double* __restrict__ w,
                                              const double* __restrict__ grad,
                                              const double* __restrict__ wn, int N,
-                                             const StageWait& sw = StageWait{nullptr, nullptr, 0u, 0, nullptr}) {
+                                             const StageWait& sw = StageWait{nullptr, nullptr, 0u, 0, nullptr, 0}) {
 	double s0 = sh.d[0][0], s1 = sh.d[0][1], s2 = sh.d[0][2];  // shift of invariant k (selects)
 #pragma unroll
 	for (int kk = 1; kk < 6; kk++)
@@ -880,7 +894,7 @@ __device__ __forceinline__ void group_invariants(int n, int c, int pos, int P, c
                                                  const double* __restrict__ w,
                                                  const double* __restrict__ grad,
                                                  const double* __restrict__ wn, int N, double (&o)[kM],
-                                                 const StageWait& sw = StageWait{nullptr, nullptr, 0u, 0, nullptr}) {
+                                                 const StageWait& sw = StageWait{nullptr, nullptr, 0u, 0, nullptr, 0}) {
 	const double mine = c < 6 ? foot_value<WAIT>(n, c, pos, P, fv, flam, fmeta, sh, coords, w, grad, wn, N, sw)
 	                          : w[(size_t)n * kM + c];
 	const double w8 = w[(size_t)n * kM + 8];
@@ -1003,7 +1017,7 @@ __global__ __launch_bounds__(256) void k_sx_inner_l8(
     const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int N, int pos0, int P) {
 	inner_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
-	                U1, Unext, un, wnext, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr});
+	                U1, Unext, un, wnext, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr, 0});
 }
 
 // The matrix part of calculateOuterWaveCorrection for every border-plan entry t,
@@ -1227,7 +1241,7 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
     const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
 	border_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
-	                 deferred, bp, argp, U, U1, Unext, un, wnext, stage, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr});
+	                 deferred, bp, argp, U, U1, Unext, un, wnext, stage, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr, 0});
 }
 
 // One launch for a whole stage of one body (gsx_stage, nothing between its
@@ -1237,9 +1251,13 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
 // every gradient block has finished.
 // An inner foot interpolating in space-time with border nodes' NEW invariants
 // (interpolateInOwner; engine/simplex/Engine.cpp:119-135 orders the border
-// stage first) waits for exactly those nodes' flags.  Border blocks never wait
-// and have the lower block ids, and workgroups are dispatched in id order, so
-// every block an inner group waits for is resident or finished.
+// stage first) waits for exactly those nodes' flags.  Every wait is on blocks
+// with LOWER ids: inner groups wait on border and gradient blocks, border groups
+// (their CELL feet, mode 2) only on gradient blocks, gradient blocks never wait.
+// ASSUMPTION (how the hardware dispatches, not a HIP guarantee): workgroups of
+// one launch are dispatched in id order on each XCD, so every block a waiting
+// block depends on is resident or finished.  The launch is capped at
+// kFuseMaxBlocks (4096) blocks, and every wait is bounded (StageWait::budget).
 __global__ __launch_bounds__(256) void k_sx_stage_l8(
     const int* __restrict__ border, int nBorder, const int* __restrict__ inner, int nInner, int nbBlk,
     const int4* __restrict__ fv, const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
@@ -1700,18 +1718,23 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 	// node of the border list (its flag is set in the same launch), and no border
 	// foot may read wn (border groups never wait)
 	bool fusable = true;
+	int waitFeet = 0;  // inner feet that read border nodes' new invariants (they wait in one launch)
 	{
 		std::vector<char> inBorder(N, 0);
 		for (int i = 0; i < nb; i++) inBorder[border[i]] = 1;
-		for (int pos = 0; pos < P && fusable; pos++)
-			for (int k = 0; k < 6 && fusable; k++) {
+		for (int pos = 0; pos < P; pos++)
+			for (int k = 0; k < 6; k++) {
 				const size_t e = (size_t)k * P + pos;
 				if ((fmeta[e] & 15) != GSX_FOOT_SPACETIME) continue;
 				const int vs[4] = {fv[e].x, fv[e].y, fv[e].z, fv[e].w};
+				bool reads_wn = false;
 				for (int i = 0; i < 4; i++) {
 					const int sl = (fmeta[e] >> (4 + 4 * i)) & 15;
-					if (sl >= 3 && (pos < nb || !inBorder[vs[sl - 3]])) fusable = false;
+					if (sl < 3) continue;
+					reads_wn = true;
+					if (pos < nb || !inBorder[vs[sl - 3]]) fusable = false;
 				}
+				if (reads_wn && pos >= nb) waitFeet++;
 			}
 	}
 	SX_TRY(hipStreamSynchronize(c->stream));
@@ -1732,9 +1755,26 @@ gcmx_status gsx_set_stage_plan(gsx_ctx* c, int stage, const gsx_foot* feet, cons
 	st.nBorder = nb;
 	st.nInner = ni;
 	st.fusable = fusable;
+	st.waitFeet = waitFeet;
 	st.set = true;
 	return prep_border(c);
 }
+
+}  // extern "C"
+
+// After a stream synchronisation: the error word of the one-launch stages (a
+// device wait that gave up), reported once and cleared.
+static gcmx_status report_wait_error(gsx_ctx* c) {
+	if (!c->ready) return GCMX_OK;
+	int err = 0;
+	SX_TRY(hipMemcpy(&err, c->ready + (size_t)c->N + 1, sizeof(int), hipMemcpyDeviceToHost));
+	if (!err) return GCMX_OK;
+	SX_TRY(hipMemset(c->ready + (size_t)c->N + 1, 0, sizeof(int)));
+	return fail(GCMX_ERR_STATE, err & 2 ? "one-launch simplex stage: a gradient wait timed out (results invalid)"
+	                                    : "one-launch simplex stage: a border-node wait timed out (results invalid)");
+}
+
+extern "C" {
 
 gcmx_status gsx_upload(gsx_ctx* c, const double* aos) {
 	gcmx_status s = check(c);
@@ -1757,6 +1797,7 @@ gcmx_status gsx_download(gsx_ctx* c, double* aos) {
 	const size_t N = (size_t)c->N;
 	std::vector<double> soa(kM * N);
 	SX_TRY(hipStreamSynchronize(c->stream));
+	if ((s = report_wait_error(c)) != GCMX_OK) return s;  // a timed-out stage made this layer
 	SX_TRY(hipMemcpy(soa.data(), c->u, soa.size() * sizeof(double), hipMemcpyDeviceToHost));
 	for (size_t n = 0; n < N; n++)
 		for (int k = 0; k < kM; k++) aos[kM * n + k] = soa[k * N + n];
@@ -1892,9 +1933,10 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 		                   c->mats + stage * 81, N);
 	c->wStage = -1;
 	// one-launch stage (k_sx_stage_l8: gradient, border and inner groups side by side)
-	// a few hundred blocks at most: every block is resident beside the ones it
-	// waits for (at 64^3 with eight lanes, 8 600 blocks of waiting groups measured
-	// 1.45x slower than separate launches)
+	// for grids of at most kFuseMaxBlocks (4096) blocks, where it measured faster
+	// (32^3 meshes: 1 120 blocks); at 64^3 with eight lanes, 8 600 blocks of waiting
+	// groups measured 1.45x slower than separate launches.  Mode 3 (tuning only)
+	// lifts the cap.
 	const size_t nblk =
 	    ((size_t)((c->fuseMode == 2 ? N : 0) + st.nBorder + st.nInner) * kL + kL8Block - 1) / kL8Block;
 	bool one = fuse && l8 && c->fuseMode && st.fusable && st.nBorder > 0 && st.nInner > 0 &&
@@ -1913,9 +1955,10 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 		const BorderDevArgs bp = {c->corrOf, (bd.set && bd.n) ? bd.cond : nullptr, bd.B, bd.S,
 		                          bd.outer, bd.n, bd.nCond, st.rec, st.recB, st.recMd};
 		const int ngBlk = withGrad ? (int)(((size_t)N * kL + kL8Block - 1) / kL8Block) : 0;
-		c->gTarget += (unsigned)ngBlk;  // the counter wraps like the target
-		const StageWait sw{c->ready, withGrad ? reinterpret_cast<unsigned*>(c->ready + N) : nullptr, c->gTarget,
-		                   ++c->epoch, c->ready + N + 1};
+		// the counter wraps like the target; both advance only with a launched grid
+		const unsigned target = c->gTarget + (unsigned)ngBlk;
+		const StageWait sw{c->ready, withGrad ? reinterpret_cast<unsigned*>(c->ready + N) : nullptr, target,
+		                   c->epoch + 1, c->ready + N + 1, c->waitBudget};
 		if (!withGrad)
 			hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
 			                   c->stream, c->w, c->grad, c->gOff, c->gNb, c->coords, c->gW, c->gM, c->gDet, N);
@@ -1927,6 +1970,8 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 		                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, sw, ngBlk,
 		                   c->grad, c->gOff, c->gNb, c->gW, c->gM, c->gDet);
 		SX_TRY(hipGetLastError());
+		c->gTarget = target;
+		c->epoch++;
 		*fused = true;
 		return GCMX_OK;
 	}
@@ -2016,6 +2061,14 @@ gcmx_status gsx_set_stage_fusion(gsx_ctx* c, int on) {
 	if (s) return s;
 	if (on < 0 || on > 3) return fail(GCMX_ERR_INVALID_ARG, "stage fusion must be 0..3");
 	c->fuseMode = on;
+	return GCMX_OK;
+}
+
+gcmx_status gsx_stage_plan_info(const gsx_ctx* c, int stage, int* fusable, int* wait_feet) {
+	if (!c || !fusable || !wait_feet) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	if (stage < 0 || stage > 2 || !c->st[stage].set) return fail(GCMX_ERR_STATE, "stage plan not set");
+	*fusable = c->st[stage].fusable ? 1 : 0;
+	*wait_feet = c->st[stage].waitFeet;
 	return GCMX_OK;
 }
 
@@ -2250,13 +2303,13 @@ gcmx_status gsx_sync(gsx_ctx* c) {
 	gcmx_status s = check(c);
 	if (s) return s;
 	SX_TRY(hipStreamSynchronize(c->stream));
-	int err = 0;  // a one-launch stage's wait that timed out (k_sx_stage_l8)
-	SX_TRY(hipMemcpy(&err, c->ready + (size_t)c->N + 1, sizeof(int), hipMemcpyDeviceToHost));
-	if (err) {  // reported once: the word is cleared for the calls that follow
-		SX_TRY(hipMemset(c->ready + (size_t)c->N + 1, 0, sizeof(int)));
-		return fail(GCMX_ERR_STATE, err & 2 ? "one-launch simplex stage: a gradient wait timed out"
-		                                    : "one-launch simplex stage: a border-node wait timed out");
-	}
+	return report_wait_error(c);
+}
+
+gcmx_status gsx_set_wait_budget(gsx_ctx* c, int polls) {
+	gcmx_status s = check(c);
+	if (s) return s;
+	c->waitBudget = polls;
 	return GCMX_OK;
 }
 

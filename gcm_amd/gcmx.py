@@ -44,14 +44,15 @@ SYMBOLS = [
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_comm_init_local", "gcmx_local_group_steps",
     "gcmx_sync", "gcmx_stream",
-    "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_inner_nodes",
+    "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_profile_kernel",
+    "gcmx_inner_nodes",
     "gcmx_all_nodes", "gcmx_device_bytes", "gcmx_copy_ceiling",
     "gsx_create", "gsx_destroy", "gsx_set_matrices", "gsx_set_gradient_plan",
     "gsx_set_stage_plan", "gsx_set_border_plan", "gsx_set_border_values",
     "gsx_plain_correction", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
     "gsx_stage_nodes", "gsx_stage_finish", "gsx_contact_create", "gsx_contact_destroy",
     "gsx_contact_plain", "gsx_contact_correct", "gsx_step", "gsx_set_node_lanes",
-    "gsx_set_stage_fusion", "gsx_last_stage_fused",
+    "gsx_set_stage_fusion", "gsx_last_stage_fused", "gsx_stage_plan_info", "gsx_set_wait_budget",
 ]
 
 
@@ -135,6 +136,8 @@ def lib() -> ctypes.CDLL:
     L.gcmx_profile_read.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), dp,
                                     ctypes.POINTER(ctypes.c_longlong), dp]
     L.gcmx_profile_read.restype = ctypes.c_int
+    L.gcmx_profile_kernel.argtypes = [vp, ctypes.c_int]
+    L.gcmx_profile_kernel.restype = ctypes.c_char_p
     L.gcmx_inner_nodes.argtypes = [vp]
     L.gcmx_inner_nodes.restype = ctypes.c_longlong
     L.gcmx_all_nodes.argtypes = [vp]
@@ -337,8 +340,9 @@ class Context:
             byt = ctypes.c_double()
             lib().gcmx_profile_read(self._ptr, i, ctypes.byref(name), ctypes.byref(tot),
                                     ctypes.byref(cnt), ctypes.byref(byt))
+            kern = lib().gcmx_profile_kernel(self._ptr, i) or b""
             out[name.value.decode()] = {"total_ms": tot.value, "launches": cnt.value,
-                                        "bytes_per_launch": byt.value}
+                                        "bytes_per_launch": byt.value, "kernel": kern.decode()}
         return out
 
     @property

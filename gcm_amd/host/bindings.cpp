@@ -490,8 +490,18 @@ PYBIND11_MODULE(_gcm_host, m) {
 		         return p;
 	         }),
 	         py::arg("task"), py::arg("device") = 0)
-	    .def("run", [](PySimplexEngine& p) { p.e->run(); })
-	    .def("run_steps", [](PySimplexEngine& p, int n) { p.e->runSteps(n); })
+	    // both end with a device check: a one-launch stage whose wait gave up
+	    // (gsx_sync: GCMX_ERR_STATE) raises here instead of returning stale results
+	    .def("run", [](PySimplexEngine& p) { p.e->run(); p.e->sync(); })
+	    .def("run_steps", [](PySimplexEngine& p, int n, bool check) {
+		         p.e->runSteps(n);
+		         if (check) p.e->sync();
+	         }, py::arg("n"), py::arg("check") = true)
+	    .def("stage_plan_info", [](PySimplexEngine& p, size_t body, int stage) { return p.e->stagePlanInfo(body, stage); },
+	         "(the plan admits the one-launch stage, inner feet that wait there)", py::arg("body"), py::arg("stage"))
+	    .def("set_wait_budget", [](PySimplexEngine& p, int polls) { p.e->setWaitBudget(polls); },
+	         "polls per device wait of the one-launch stages; < 0: every wait reports a timeout (tests)",
+	         py::arg("polls"))
 	    .def("pde", &PySimplexEngine::pde, "current layer of a body [n_vertices, 9]",
 	         py::arg("body") = 0)
 	    .def_property_readonly("number_of_bodies", [](PySimplexEngine& p) { return p.e->numberOfBodies(); })

@@ -322,34 +322,48 @@ HipBorderConditions<D>::HipBorderConditions(const Task& task, const HipMesh<D>& 
 			if (d != f / 2) n *= (size_t)mesh.sizes[d];
 		effective[f].assign(n, -1);
 	}
-	for (const auto& bc : found->second) {
-		Condition c;
-		c.direction = bc.direction;
-		if (!(bc.direction >= 0 && bc.direction < D)) throw Exception("border direction out of range");
-		for (const auto& q : bc.values) {
-			if (!hasQuantity(D, q.first)) throw Exception("border quantity not in the PDE vector");
-			c.values.push_back({q.first, q.second});  // std::map order == reference order
+	try {
+		for (const auto& bc : found->second) {
+			Condition c;
+			c.direction = bc.direction;
+			if (!(bc.direction >= 0 && bc.direction < D)) throw Exception("border direction out of range");
+			for (const auto& q : bc.values) {
+				if (!hasQuantity(D, q.first)) throw Exception("border quantity not in the PDE vector");
+				c.values.push_back({q.first, q.second});  // std::map order == reference order
+			}
+			if (c.values.size() > GCMX_MAX_BORDER_Q) throw Exception("too many border quantities");
+			const int index = (int)conditions.size();
+			auto collect = [&](int side, std::vector<int>& out) {
+				std::vector<int>& eff = effective[2 * bc.direction + side];
+				size_t k = 0;
+				forEachInner<D>(mesh.sizes, [&](const std::array<int, D>& it) {
+					if (bc.area->contains(mesh.coords(it))) {
+						for (int d = 0; d < D; d++) out.push_back(it[d]);
+						eff[k] = index;
+					}
+					k++;
+				}, bc.direction, side ? mesh.sizes[bc.direction] - 1 : 0);
+			};
+			collect(0, c.leftNodes);
+			collect(1, c.rightNodes);
+			try {
+				gcmxCheck(gcmx_border_nodes_create(mesh.ctx(), c.direction, -1, (int)(c.leftNodes.size() / D),
+				                                   c.leftNodes.data(), &c.leftD), "gcmx_border_nodes_create");
+				gcmxCheck(gcmx_border_nodes_create(mesh.ctx(), c.direction, +1, (int)(c.rightNodes.size() / D),
+				                                   c.rightNodes.data(), &c.rightD), "gcmx_border_nodes_create");
+			} catch (...) {
+				gcmx_border_nodes_destroy(c.leftD);
+				throw;
+			}
+			conditions.push_back(std::move(c));
 		}
-		if (c.values.size() > GCMX_MAX_BORDER_Q) throw Exception("too many border quantities");
-		const int index = (int)conditions.size();
-		auto collect = [&](int side, std::vector<int>& out) {
-			std::vector<int>& eff = effective[2 * bc.direction + side];
-			size_t k = 0;
-			forEachInner<D>(mesh.sizes, [&](const std::array<int, D>& it) {
-				if (bc.area->contains(mesh.coords(it))) {
-					for (int d = 0; d < D; d++) out.push_back(it[d]);
-					eff[k] = index;
-				}
-				k++;
-			}, bc.direction, side ? mesh.sizes[bc.direction] - 1 : 0);
-		};
-		collect(0, c.leftNodes);
-		collect(1, c.rightNodes);
-		gcmxCheck(gcmx_border_nodes_create(mesh.ctx(), c.direction, -1, (int)(c.leftNodes.size() / D),
-		                                   c.leftNodes.data(), &c.leftD), "gcmx_border_nodes_create");
-		gcmxCheck(gcmx_border_nodes_create(mesh.ctx(), c.direction, +1, (int)(c.rightNodes.size() / D),
-		                                   c.rightNodes.data(), &c.rightD), "gcmx_border_nodes_create");
-		conditions.push_back(std::move(c));
+	} catch (...) {  // the destructor does not run for a constructor that throws
+		for (auto& done : conditions) {
+			gcmx_border_nodes_destroy(done.leftD);
+			gcmx_border_nodes_destroy(done.rightD);
+		}
+		conditions.clear();
+		throw;
 	}
 	uniform = true;
 	for (int f = 0; f < 2 * D; f++) {

@@ -1277,6 +1277,16 @@ void Engine::sync() const {
 	for (const auto& b : bodies) gcmxCheck(gsx_sync(b.ctx), "gsx_sync");
 }
 
+std::pair<bool, int> Engine::stagePlanInfo(size_t body, int stage) const {
+	int fusable = 0, waits = 0;
+	gcmxCheck(gsx_stage_plan_info(bodies.at(body).ctx, stage, &fusable, &waits), "gsx_stage_plan_info");
+	return {fusable != 0, waits};
+}
+
+void Engine::setWaitBudget(int polls) {
+	for (auto& b : bodies) gcmxCheck(gsx_set_wait_budget(b.ctx, polls), "gsx_set_wait_budget");
+}
+
 size_t Engine::numberOfContactPairs() const { return contactPairs; }
 
 std::vector<real> Engine::pde(size_t body) const {

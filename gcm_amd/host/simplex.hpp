@@ -21,6 +21,7 @@
 #include <array>
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/gcmx.h"
@@ -259,6 +260,11 @@ public:
 	void setStageFusion(int mode);
 	/// stages run as one launch since construction
 	long long fusedStages() const { return fusedStages_; }
+	/// (plan admits the one launch, inner feet that wait there) of a body's stage
+	std::pair<bool, int> stagePlanInfo(size_t body, int stage) const;
+	/// polls per device wait of the one-launch stages (gsx_set_wait_budget; < 0:
+	/// every wait reports a timeout, for tests of the error path)
+	void setWaitBudget(int polls);
 
 protected:
 	void nextTimeStep() override;

@@ -328,6 +328,17 @@ gcmx_status gsx_set_node_lanes(gsx_ctx* ctx, int lanes);
  * gsx_last_stage_fused reports whether the last gsx_stage ran as one launch. */
 gcmx_status gsx_set_stage_fusion(gsx_ctx* ctx, int on);
 gcmx_status gsx_last_stage_fused(const gsx_ctx* ctx, int* fused);
+/* Tuning only: on = 3 is mode 1 without the 4096-block grid cap.  The one
+ * launch relies on workgroups being dispatched in block-id order (each block
+ * waits only on blocks with lower ids); every device wait is bounded: a wait
+ * that gives up sets the context's error word, which gsx_sync and gsx_download
+ * report (GCMX_ERR_STATE, "results invalid") and clear.
+ * gsx_stage_plan_info: whether stage `stage`'s plan admits the one launch and
+ * how many inner feet wait there for border nodes' new invariants.
+ * gsx_set_wait_budget: polls per device wait (default 2^20); < 0 makes every
+ * wait report a timeout at once (tests of the error path). */
+gcmx_status gsx_stage_plan_info(const gsx_ctx* ctx, int stage, int* fusable, int* wait_feet);
+gcmx_status gsx_set_wait_budget(gsx_ctx* ctx, int polls);
 
 /* ---- simplex contact correctors ----------------------------------------------
  * ContactCorrectorInRiemannInvariants<Elastic, Elastic, AdhesionContactMatrixCreator>
@@ -378,6 +389,9 @@ gcmx_status gcmx_profile_reset(gcmx_ctx* ctx);
 int         gcmx_profile_read(gcmx_ctx* ctx, int index, const char** name,
                               double* total_ms, long long* launches,
                               double* bytes_per_launch);
+/* The kernel instance the last launch of bucket `index` ran (e.g.
+ * "k_step_tx2<2, 512, KF0, UNI, !FACES>"); "" when unknown. */
+const char* gcmx_profile_kernel(gcmx_ctx* ctx, int index);
 
 /* Device-side layout facts (for DESIGN.md-style reporting and tests). */
 long long   gcmx_inner_nodes(gcmx_ctx* ctx);
@@ -385,8 +399,8 @@ long long   gcmx_all_nodes(gcmx_ctx* ctx);
 size_t      gcmx_device_bytes(gcmx_ctx* ctx);
 /* Measurement only (bench.py's roofline.copy_ceiling): the practical HBM rate
  * of this device for a flat copy of `bytes` bytes (half read, half written;
- * double2 per lane, non-temporal stores, 32 768 blocks of 256 threads, the
- * fastest of tools/copy_probe.hip's grids).  Median of `reps` timed copies
+ * 16 B per lane per access, four loads in flight per lane, non-temporal
+ * stores, 2048 blocks of 256 threads, grid-stride).  Median of `reps` timed copies
  * after one warm copy; *ms_out = that copy's duration (HIP events on the
  * ctx stream).  Allocates and frees 2 x bytes / 2 on the context's device. */
 gcmx_status gcmx_copy_ceiling(gcmx_ctx* ctx, size_t bytes, int reps, float* ms_out);

@@ -216,10 +216,113 @@ def test_one_launch_stage_equals_two_launches(H, case, mode):
         e = H.SimplexEngine(mk())
         e.set_node_lanes(8)
         e.set_stage_fusion(fuse)
+        info = [e.stage_plan_info(0, s) for s in range(3)]
         e.run_steps(3)
         e.sync()
         out.append((e.pde(), e.fused_stages))
     (fused, n_fused), (split, n_split) = out
     assert n_fused == 9 and n_split == 0
+    assert all(f for f, _ in info)
+    if case in ("free-c2", "fracture-c1.7"):
+        # the hand-off protocol is exercised: inner feet wait for border nodes' wn
+        assert sum(w for _, w in info) > 0, info
     assert np.array_equal(fused, split), f"{int((fused != split).sum())} values differ"
     assert np.abs(fused).max() > 0
+
+
+def test_one_launch_stage_timeout_is_reported(H):
+    """A device wait of the one-launch stage that gives up (forced here: a wait
+    budget < 0 makes every wait report a timeout) must not hand stale results to
+    the host as success: run_steps (which ends with gsx_sync) and gsx_download
+    raise; the error is reported once and cleared."""
+    e = H.SimplexEngine(host_task(5, 2.0, 0.1, 7, border=FREE_BORDER))
+    e.set_node_lanes(8)
+    e.set_stage_fusion(1)
+    assert sum(w for _, w in (e.stage_plan_info(0, s) for s in range(3))) > 0
+    e.set_wait_budget(-1)
+    with pytest.raises(Exception, match="timed out"):
+        e.run_steps(1)
+    e.set_wait_budget(1 << 20)
+    e.run_steps(1)  # reported once, cleared, and a healthy launch reports nothing
+    e.set_wait_budget(-1)
+    e.run_steps(1, check=False)
+    with pytest.raises(Exception, match="timed out"):
+        e.pde()  # gsx_download
+
+
+def _raw_simplex_plan(G, border, inner, wn_vertex):
+    """A hand-made 8-node stage plan through the C-ABI: ZERO feet everywhere
+    except one inner node's foot 0, a SPACETIME foot whose weights multiply the
+    NEW invariants of `wn_vertex` (slot 3)."""
+    import ctypes
+    L = G.lib()
+
+    class Foot(ctypes.Structure):
+        _fields_ = [("kind", ctypes.c_int), ("v", ctypes.c_int * 4), ("slot", ctypes.c_int * 4),
+                    ("lam", ctypes.c_double * 4), ("q", ctypes.c_double * 3)]
+    N = 8
+    vp = ctypes.c_void_p
+    L.gsx_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(vp)]
+    L.gsx_set_matrices.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    L.gsx_set_gradient_plan.argtypes = [vp] + [ctypes.c_void_p] * 6
+    L.gsx_set_stage_plan.argtypes = [vp, ctypes.c_int, ctypes.POINTER(Foot), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_int)]
+    L.gsx_stage.argtypes = [vp, ctypes.c_int]
+    L.gsx_stage_plan_info.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.gsx_last_stage_fused.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.gsx_set_node_lanes.argtypes = [vp, ctypes.c_int]
+    L.gsx_sync.argtypes = [vp]
+    L.gsx_destroy.argtypes = [vp]
+    L.gsx_destroy.restype = None
+    dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    coords = np.random.default_rng(1).random((N, 3))
+    ctx = vp()
+    G._check(L.gsx_create(0, N, dp(coords), ctypes.byref(ctx)))
+    eye = np.tile(np.eye(9).reshape(-1), 3)
+    G._check(L.gsx_set_matrices(ctx, dp(eye), dp(eye)))
+    # gradient plan: every node one neighbour (the next), unit weight, identity normal matrix
+    off = np.arange(N + 1, dtype=np.int32)
+    nb = ((np.arange(N) + 1) % N).astype(np.int32)
+    rows = (coords[nb] - coords).reshape(-1).copy()
+    wts = np.ones(N)
+    M = np.tile(np.eye(3).reshape(-1), N)
+    det = np.ones(N)
+    G._check(L.gsx_set_gradient_plan(ctx, off.ctypes.data, nb.ctypes.data, rows.ctypes.data, wts.ctypes.data,
+                                     M.ctypes.data, det.ctypes.data))
+    feet = (Foot * (N * 6))()
+    for i in range(N * 6):
+        feet[i].kind = 3  # GSX_FOOT_ZERO
+    f = feet[inner[0] * 6 + 0]
+    f.kind = 2  # GSX_FOOT_SPACETIME over the face (wn_vertex, border[0], border[0])
+    f.v[0], f.v[1], f.v[2] = wn_vertex, border[0], border[0]
+    f.slot[0], f.slot[1], f.slot[2], f.slot[3] = 3, 0, 0, 0
+    f.lam[0], f.lam[1], f.lam[2], f.lam[3] = 0.5, 0.5, 0.0, 0.0
+    shift = np.zeros(18)
+    bl = np.array(border, dtype=np.int32)
+    il = np.array(inner, dtype=np.int32)
+    for st in range(3):
+        G._check(L.gsx_set_stage_plan(ctx, st, feet, dp(shift), len(bl),
+                                      bl.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), len(il),
+                                      il.ctypes.data_as(ctypes.POINTER(ctypes.c_int))))
+    G._check(L.gsx_set_node_lanes(ctx, 8))
+    fus, waits = ctypes.c_int(), ctypes.c_int()
+    G._check(L.gsx_stage_plan_info(ctx, 0, ctypes.byref(fus), ctypes.byref(waits)))
+    G._check(L.gsx_stage(ctx, 0))
+    G._check(L.gsx_sync(ctx))
+    fused = ctypes.c_int()
+    G._check(L.gsx_last_stage_fused(ctx, ctypes.byref(fused)))
+    L.gsx_destroy(ctx)
+    return fus.value, waits.value, fused.value
+
+
+def test_unfusable_plan_runs_two_launches():
+    """gsx_set_stage_plan's fusable check decides the launch shape: an inner foot
+    that reads the new invariants of a node OUTSIDE the border list (nothing in
+    the launch would ever publish them) makes the plan unfusable, and gsx_stage
+    then runs the border and inner halves as two launches; the same foot over a
+    border node is fusable, waits, and runs as one launch."""
+    import gcm_amd.gcmx as G
+    border, inner = [0, 1], [2, 3, 4, 5, 6, 7]
+    assert _raw_simplex_plan(G, border, inner, wn_vertex=5) == (0, 1, 0)
+    assert _raw_simplex_plan(G, border, inner, wn_vertex=1) == (1, 1, 1)

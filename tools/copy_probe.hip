@@ -32,6 +32,40 @@ __global__ __launch_bounds__(256) void k_flat(const d2* __restrict__ in, d2* __r
 		__builtin_nontemporal_store(in[i], out + i);
 }
 
+// flat-copy variants for the yardstick (gcmx_copy_ceiling): U loads in flight
+// per lane before their stores, non-temporal (NT) or plain stores, nt loads (NTL)
+template <int U, bool NT, bool NTL>
+__global__ __launch_bounds__(256) void k_flat_u(const d2* __restrict__ in, d2* __restrict__ out, long long n2) {
+	const long long nth = (long long)gridDim.x * blockDim.x;
+	long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	for (; i + (U - 1) * nth < n2; i += U * nth) {
+		d2 v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) v[u] = NTL ? __builtin_nontemporal_load(in + i + u * nth) : in[i + u * nth];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			if (NT) __builtin_nontemporal_store(v[u], out + i + u * nth);
+			else out[i + u * nth] = v[u];
+		}
+	}
+	for (; i < n2; i += nth) out[i] = in[i];
+}
+// each block copies one contiguous chunk (no grid stride): 256 threads x U x 16 B per step
+template <int U>
+__global__ __launch_bounds__(256) void k_flat_chunk(const d2* __restrict__ in, d2* __restrict__ out, long long n2,
+                                                   long long per_block) {
+	const long long b0 = (long long)blockIdx.x * per_block, b1 = min(b0 + per_block, n2);
+	for (long long i = b0 + threadIdx.x; i < b1; i += 256 * U) {
+		d2 v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (i + u * 256 < b1) v[u] = in[i + u * 256];
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (i + u * 256 < b1) __builtin_nontemporal_store(v[u], out + i + u * 256);
+	}
+}
+
 __global__ __launch_bounds__(512) void k_layout(const double* __restrict__ in, double* __restrict__ out,
                                                 long long cs, int chunk) {
 	const int z = threadIdx.x;
@@ -79,6 +113,22 @@ int main() {
 		float ms = timeit([&] { hipLaunchKernelGGL(k_flat, dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
 		std::printf("flat copy grid %6d: %.3f ms (%.0f GB/s)\n", g, ms, 144.0 * nodes / (ms * 1e6));
 	}
+	auto rate = [&](float ms) { return 144.0 * nodes / (ms * 1e6); };
+	for (int g : {1024, 2048, 4096, 8192, 16384}) {
+		float a = timeit([&] { hipLaunchKernelGGL((k_flat_u<1, true, false>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		float b = timeit([&] { hipLaunchKernelGGL((k_flat_u<4, true, false>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		float c = timeit([&] { hipLaunchKernelGGL((k_flat_u<4, false, false>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		float d = timeit([&] { hipLaunchKernelGGL((k_flat_u<4, true, true>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		float e = timeit([&] { hipLaunchKernelGGL((k_flat_u<8, true, false>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		std::printf("flat grid %6d: U1 nt %.0f  U4 nt %.0f  U4 plain %.0f  U4 nt+ntload %.0f  U8 nt %.0f GB/s\n", g, rate(a),
+		            rate(b), rate(c), rate(d), rate(e));
+	}
+	for (int nb : {2048, 4096, 16384, 65536}) {
+		const long long per = (n2 + nb - 1) / nb;
+		float a = timeit([&] { hipLaunchKernelGGL((k_flat_chunk<4>), dim3(nb), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2, per); });
+		std::printf("chunked %6d blocks (U4, nt stores): %.0f GB/s\n", nb, rate(a));
+	}
+	if (std::getenv("COPY_ONLY")) return 0;
 	for (int chunk : {128, 32}) {
 		for (long long pad : {0LL, 16LL, 32LL, 48LL, 64LL, 96LL, 160LL, 256LL, 544LL, 1024LL, 2048LL, 4096LL}) {
 			const long long cs = CS + pad;

@@ -17,7 +17,20 @@ def agg(path, counter):
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 
-def main(prof_dir, out, n=512):
+def readable(rocprof_name):
+    """'void gcmx::k_step_tx2<2, 512, true, true, false>(...)' -> the library's
+    symbol form 'k_step_tx2<2, 512, KF0, UNI, !FACES>' (gcmx_profile_kernel)."""
+    import re
+    m = re.search(r"(k_step_tx2|k_fused_xyz)<([^>]*)>", rocprof_name)
+    if not m:
+        return rocprof_name
+    a = [x.strip() for x in m.group(2).split(",")]
+    flags = ["KF0", "UNI", "FACES"]
+    out = a[:2] + [(f if v == "true" else "!" + f) for f, v in zip(flags, a[2:])]
+    return f"{m.group(1)}<{', '.join(out)}>"
+
+
+def main(prof_dir, out, n=512, lib_path="gcm_amd/lib/libgcmx.so"):
     f = agg(f"{prof_dir}/fetch/run_counter_collection.csv", "FETCH_SIZE")
     w = agg(f"{prof_dir}/write/run_counter_collection.csv", "WRITE_SIZE")
     true = 8 * (1 << 30)
@@ -31,7 +44,10 @@ def main(prof_dir, out, n=512):
         r8, w8 = old["read8_fetch_bytes"], old["write8_write_bytes"]
     ff, wf = true / r8, true / w8
     alg = 144 * n ** 3
+    import hashlib
+    sha = hashlib.sha256(open(lib_path, "rb").read()).hexdigest()
     res = {"n": n, "ranks": 1, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, {prof_dir}",
+           "lib_sha256": sha,
            "calibration": {"tool": "tools/calib_fetch.hip", "true_bytes": true,
                            "read8_fetch_bytes": r8, "fetch_factor": ff,
                            "write8_write_bytes": w8, "write_factor": wf},
@@ -45,7 +61,9 @@ def main(prof_dir, out, n=512):
             continue
         fk = fks[0] * 1024 * ff
         wk = wks[0] * 1024 * wf
-        res["kernels"][short] = {"fetch_bytes_per_launch": fk, "write_bytes_per_launch": wk,
+        full = [k for k in f if frag in k][0]
+        res["kernels"][short] = {"symbol": readable(full), "rocprof_name": full,
+                                 "fetch_bytes_per_launch": fk, "write_bytes_per_launch": wk,
                                  "hbm_bytes_per_launch": fk + wk,
                                  "algorithmic_bytes_per_launch": alg,
                                  "traffic_over_algorithmic": (fk + wk) / alg}
