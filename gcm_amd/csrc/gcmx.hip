@@ -121,6 +121,7 @@ struct gcmx_ctx {
 	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso structure)
 	IsoAxis iso[3] = {};           // per-axis values for the fast kernels (tau part in build_tables)
 	bool ghosts_touched = false;   // node-list border fills / contact copies / ghost uploads happened
+	bool last_ode_fused = false;   // the last gcmx_step_ode scaled the stresses in the step's epilogue
 	unsigned faces_written = 0;    // faces (bit 2*axis + side) whose ghosts a face fill wrote
 	gcmx_path path = GCMX_PATH_AUTO;
 	gcmx_schedule sched = GCMX_SCHED_AUTO;
@@ -966,20 +967,69 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 	return GCMX_OK;
 }
 
-gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
-	gcmx_status s = check_ctx(c);
+}  // extern "C"
+
+namespace {
+
+// The Maxwell ODE a step may carry (gcmx_step_ode): one factor per material.
+struct StepOde {
+	bool on = false;
+	std::vector<double> f;
+};
+
+gcmx_status ode_factors(gcmx_ctx* c, double tau, const double* tau0, int n_mat, StepOde& ode) {
+	if (c->n_mat == 0) return fail(GCMX_ERR_STATE, "materials not set");
+	if (!tau0 || n_mat != c->n_mat) return fail(GCMX_ERR_INVALID_ARG, "one tau0 per material expected");
+	ode.on = true;
+	ode.f.resize(n_mat);
+	for (int m = 0; m < n_mat; m++) ode.f[m] = std::exp(-tau / tau0[m]);  // Ode.hpp:34-35
+	return GCMX_OK;
+}
+
+gcmx_status ode_apply(gcmx_ctx* c, const std::vector<double>& f);
+
+// The ODE rides in the one-pass step's store epilogue when the step runs
+// k_step_tx2 over one material (the factor is then one number).
+bool ode_foldable(const gcmx_ctx* c, const StepOde& ode) {
+	return ode.on && c->mat_d == nullptr && ode.f.size() == 1 && c->bs <= 2 && c->geo.sizes[2] <= 512;
+}
+
+gcmx_status step_impl(gcmx_ctx* c, double tau, const StepOde& ode) {
+	gcmx_status s = build_tables(c, tau);
 	if (s) return s;
-	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
-	s = build_tables(c, tau);
-	if (s) return s;
+	c->last_ode_fused = false;
 	if (effective_path(c) != GCMX_PATH_FUSED || c->faces_written != 0) {
 		for (int a = 0; a < c->D; a++) {
 			s = stage_impl(c, a, tau);
 			if (s) return s;
 		}
+		return ode.on ? ode_apply(c, ode.f) : GCMX_OK;
+	}
+	if (ode_foldable(c, ode)) {
+		FaceBC fb{};
+		fb.ode_on = 1;
+		fb.ode = ode.f[0];
+		s = fused_step(c, &fb);
+		if (s) return s;
+		c->last_ode_fused = true;
 		return GCMX_OK;
 	}
-	return fused_step(c, nullptr);
+	s = fused_step(c, nullptr);
+	if (s) return s;
+	return ode.on ? ode_apply(c, ode.f) : GCMX_OK;
+}
+
+gcmx_status step_faces_impl(gcmx_ctx* c, double tau, const gcmx_face* faces, const StepOde& ode);
+
+}  // namespace
+
+extern "C" {
+
+gcmx_status gcmx_step(gcmx_ctx* c, double tau) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	return step_impl(c, tau, StepOde{});
 }
 
 gcmx_status gcmx_step_faces(gcmx_ctx* c, double tau, const gcmx_face* faces) {
@@ -987,6 +1037,27 @@ gcmx_status gcmx_step_faces(gcmx_ctx* c, double tau, const gcmx_face* faces) {
 	if (s) return s;
 	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
 	if (!faces) return fail(GCMX_ERR_INVALID_ARG, "null faces");
+	return step_faces_impl(c, tau, faces, StepOde{});
+}
+
+gcmx_status gcmx_step_ode(gcmx_ctx* c, double tau, const gcmx_face* faces, const double* tau0, int n_mat) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	StepOde ode;
+	if ((s = ode_factors(c, tau, tau0, n_mat, ode)) != GCMX_OK) return s;
+	return faces ? step_faces_impl(c, tau, faces, ode) : step_impl(c, tau, ode);
+}
+
+int gcmx_last_ode_fused(gcmx_ctx* c) { return c && c->last_ode_fused ? 1 : 0; }
+
+}  // extern "C"
+
+namespace {
+
+gcmx_status step_faces_impl(gcmx_ctx* c, double tau, const gcmx_face* faces, const StepOde& ode) {
+	gcmx_status s = GCMX_OK;
+	c->last_ode_fused = false;
 	const int D = c->D;
 	BorderQ bq[6] = {};
 	unsigned on = 0;
@@ -1032,7 +1103,15 @@ gcmx_status gcmx_step_faces(gcmx_ctx* c, double tau, const gcmx_face* faces) {
 				s = fill(f);
 				if (s) return s;
 			}
-		return fused_step(c, fb.on ? &fb : nullptr);
+		const bool fold = ode_foldable(c, ode);
+		if (fold) {
+			fb.ode_on = 1;
+			fb.ode = ode.f[0];
+		}
+		s = fused_step(c, (fb.on || fold) ? &fb : nullptr);
+		if (s) return s;
+		c->last_ode_fused = fold;
+		return (ode.on && !fold) ? ode_apply(c, ode.f) : GCMX_OK;
 	}
 	for (int a = 0; a < D; a++) {
 		for (int f = 2 * a; f < 2 * a + 2; f++)
@@ -1043,8 +1122,12 @@ gcmx_status gcmx_step_faces(gcmx_ctx* c, double tau, const gcmx_face* faces) {
 		s = stage_impl(c, a, tau);
 		if (s) return s;
 	}
-	return GCMX_OK;
+	return ode.on ? ode_apply(c, ode.f) : GCMX_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 gcmx_status gcmx_set_step_schedule(gcmx_ctx* c, gcmx_schedule sched, int rows_per_block) {
 	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");
@@ -1166,20 +1249,32 @@ void gcmx_border_nodes_destroy(gcmx_border_nodes* h) {
 gcmx_status gcmx_ode_maxwell(gcmx_ctx* c, double tau, const double* tau0, int n_mat) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
-	if (c->n_mat == 0) return fail(GCMX_ERR_STATE, "materials not set");
-	if (!tau0 || n_mat != c->n_mat) return fail(GCMX_ERR_INVALID_ARG, "one tau0 per material expected");
 	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
-	s = halo_wait(c);
+	StepOde ode;
+	if ((s = ode_factors(c, tau, tau0, n_mat, ode)) != GCMX_OK) return s;
+	return ode_apply(c, ode.f);
+}
+
+}  // extern "C"
+
+namespace {
+
+// k_scale_stress over the current layer (the separate ODE pass).
+gcmx_status ode_apply(gcmx_ctx* c, const std::vector<double>& f) {
+	gcmx_status s = halo_wait(c);
 	if (s) return s;
-	std::vector<double> f(n_mat);
-	for (int m = 0; m < n_mat; m++) f[m] = std::exp(-tau / tau0[m]);  // Ode.hpp:34-35
+	const int n_mat = (int)f.size();
 	if (!c->mat_d) {
 		Timed t(c, "ode_maxwell", 2.0 * 8.0 * (c->M - c->D) * (double)c->geo.n_inner, c->stream);
 		launch_scale_stress(c->cur, c->geo, nullptr, nullptr, f[0], c->stream);
 	} else {
-		HIP_TRY(hipStreamSynchronize(c->stream));  // scratch reuse
+		// the factors travel as kernel arguments into the context's device slot,
+		// ordered on the stream after the previous scaling that read it: no host sync
 		if (!c->ode_d) HIP_TRY(hipMalloc(&c->ode_d, 256 * sizeof(double)));
-		HIP_TRY(hipMemcpy(c->ode_d, f.data(), n_mat * sizeof(double), hipMemcpyHostToDevice));
+		OdeFactors v{};
+		v.n = n_mat;
+		for (int m = 0; m < n_mat; m++) v.f[m] = f[m];
+		launch_set_factors(c->ode_d, v, c->stream);
 		Timed t(c, "ode_maxwell", (2.0 * 8.0 * (c->M - c->D) + 1.0) * (double)c->geo.n_inner, c->stream);
 		launch_scale_stress(c->cur, c->geo, c->mat_d, c->ode_d, 0.0, c->stream);
 	}
@@ -1187,6 +1282,10 @@ gcmx_status gcmx_ode_maxwell(gcmx_ctx* c, double tau, const double* tau0, int n_
 	touch_layer(c);
 	return GCMX_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dmin[3], const int dmax[3], gcmx_ctx* src,
                           const int smin[3]) {
@@ -1451,23 +1550,17 @@ size_t gcmx_device_bytes(gcmx_ctx* c) { return c ? 2 * c->layer_elems * sizeof(d
 }  // extern "C"
 
 namespace {
-// The yardstick copy: 16 B per lane per access, four independent 16-B loads in
-// flight per lane before their stores (grid-stride over 64-B lane chunks),
-// non-temporal stores; a 2048-block grid (8 per CU).
+// The yardstick copy: 16 B per lane, non-temporal stores, 32768 blocks of 256
+// threads, grid-stride -- the fastest of the 28 flat-copy shapes tools/copy_probe.hip
+// times (1 or 4 or 8 loads in flight per lane, nt or plain stores and loads,
+// 1 024-65 536 blocks, grid-stride or one chunk per block: all 4.4-5.2 TB/s on
+// the same box, profiles/r3/copy/variants.txt).
 typedef double copy_d2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_copy_ceiling(const copy_d2* __restrict__ in, copy_d2* __restrict__ out,
                                                       long long n2) {
-	const long long nth = (long long)gridDim.x * blockDim.x;
-	const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-	long long i = t;
-	for (; i + 3 * nth < n2; i += 4 * nth) {
-		const copy_d2 a = in[i], b = in[i + nth], c = in[i + 2 * nth], d = in[i + 3 * nth];
-		__builtin_nontemporal_store(a, out + i);
-		__builtin_nontemporal_store(b, out + i + nth);
-		__builtin_nontemporal_store(c, out + i + 2 * nth);
-		__builtin_nontemporal_store(d, out + i + 3 * nth);
-	}
-	for (; i < n2; i += nth) __builtin_nontemporal_store(in[i], out + i);
+	const long long stride = (long long)gridDim.x * blockDim.x;
+	for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride)
+		__builtin_nontemporal_store(in[i], out + i);
 }
 }  // namespace
 
@@ -1493,7 +1586,7 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 	} else {
 		for (int r = 0; r <= reps && st == GCMX_OK; r++) {
 			hipEventRecord(e0, c->stream);
-			hipLaunchKernelGGL(k_copy_ceiling, dim3(2048), dim3(256), 0, c->stream,
+			hipLaunchKernelGGL(k_copy_ceiling, dim3(32768), dim3(256), 0, c->stream,
 			                   static_cast<const copy_d2*>(a), static_cast<copy_d2*>(b), n2);
 			hipEventRecord(e1, c->stream);
 			float t = 0.0f;

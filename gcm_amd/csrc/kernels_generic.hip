@@ -274,6 +274,17 @@ __global__ __launch_bounds__(256) void k_scale_stress(double* __restrict__ cur, 
 	for (int c = g.D; c < g.M; c++) cur[c * g.cs + off] = cur[c * g.cs + off] * f;
 }
 
+// The per-material factors into device memory, ordered on the stream (no host
+// synchronisation): kernel-argument values read with uniform indices only.
+__global__ __launch_bounds__(64) void k_set_factors(double* __restrict__ dst, OdeFactors v) {
+	if (threadIdx.x != 0) return;
+	for (int m = 0; m < v.n; m++) dst[m] = v.f[m];
+}
+
+void launch_set_factors(double* dst_d, const OdeFactors& v, hipStream_t st) {
+	hipLaunchKernelGGL(k_set_factors, dim3(1), dim3(64), 0, st, dst_d, v);
+}
+
 void launch_scale_stress(double* cur, const Geo& g, const uint8_t* mat_d, const double* f_d,
                          double f0, hipStream_t st) {
 	if (g.n_inner <= 0) return;

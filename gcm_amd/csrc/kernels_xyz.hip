@@ -698,6 +698,10 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			node_update<2, BS, KF0>(
 			    AZ, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
 			    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
+		if (fb.ode_on) {  // MaxwellViscosityOde: sigma *= exp(-tau / tau0), the stored product (Ode.hpp:34-35)
+#pragma unroll
+			for (int c = 3; c < 9; c++) zv[c] = zv[c] * fb.ode;
+		}
 		if (t == 0 || two) {
 #pragma unroll
 			for (int c = 0; c < 9; c++) stz(c, t, y, live ? zv[c] : 0.0);
@@ -867,7 +871,7 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, f);
 				*kname = name;
 			};
-			if (fb) {
+			if (fb && fb->on) {
 				if (uni) go(k_step_tx2<BS, ZT, true, true, true>, tx2_name<BS, ZT, true, true, true>());
 				else if (kf0) go(k_step_tx2<BS, ZT, true, false, true>, tx2_name<BS, ZT, true, false, true>());
 				else go(k_step_tx2<BS, ZT, false, false, true>, tx2_name<BS, ZT, false, false, true>());
@@ -926,7 +930,8 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	const char* dummy = nullptr;
 	const char** kn = kname ? kname : &dummy;
 	if (!fused_supported(g) || x1 <= x0) return false;
-	if (faces && !fused_faces_supported(g)) return false;
+	if (faces && faces->on && !fused_faces_supported(g)) return false;
+	if (faces && faces->ode_on && !(g.bs <= 2 && g.sizes[2] <= 512)) return false;  // k_fused_xyz has no epilogue
 	switch (g.bs) {
 	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk, faces, kn);
 	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk, faces, kn);

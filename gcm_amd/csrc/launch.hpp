@@ -19,6 +19,12 @@ void launch_copy_box(double* dst, const Geo& gd, const double* src, const Geo& g
                      const int dmin[3], const int smin[3], const int ext[3], hipStream_t st);
 void launch_scale_stress(double* cur, const Geo& g, const uint8_t* mat_d, const double* f_d,
                          double f0, hipStream_t st);
+// Per-material ODE factors by value (at most 255 materials).
+struct OdeFactors {
+	int n;
+	double f[255];
+};
+void launch_set_factors(double* dst_d, const OdeFactors& v, hipStream_t st);
 // The quantities of one cubic border condition, by value (kernel arguments):
 // PhysicalQuantities codes and timeDependency(t), in the reference's map order.
 constexpr int kMaxBorderQ = 16;
@@ -60,12 +66,18 @@ struct FaceBC {
 	unsigned on;          // bit f: face f has a condition
 	unsigned mask[4];     // overridden components
 	double two_v[4][9];
+	// MaxwellViscosityOde folded into the store epilogue (gcmx_step_ode): every
+	// stress component of the step's result times `ode` (Ode.hpp:28-37) when ode_on
+	unsigned ode_on;
+	double ode;
 };
-// The one-pass step with FaceBC needs bs <= 2, Z <= 512 and Y, Z >= 2*bs + 2.
+// The one-pass step with FaceBC face conditions (on != 0) needs bs <= 2, Z <= 512
+// and Y, Z >= 2*bs + 2; a FaceBC with on == 0 carries only the ODE factor.
 bool fused_faces_supported(const Geo& g);
 // One pass per time step: X, Y, Z stages of planes [x0, x1), `a` = the three axes.
 // `chunk`: y rows per block (0 = automatic, kernels_xyz.hip: xyz_chunk_for).
-// `faces`: y/z face conditions (null: y/z ghosts of both layers are zero).
+// `faces`: y/z face conditions and the ODE factor (null, or on == 0: y/z ghosts of
+// both layers are zero); the ODE factor needs the k_step_tx2 path (bs <= 2, Z <= 512).
 // `kname`: set to the launched instance's symbol (a static string).
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,

@@ -40,7 +40,7 @@ SYMBOLS = [
     "gcmx_border_fill",
     "gcmx_border_nodes_create", "gcmx_border_apply", "gcmx_border_nodes_destroy", "gcmx_step_faces",
     "gcmx_copy_box",
-    "gcmx_ode_maxwell",
+    "gcmx_ode_maxwell", "gcmx_step_ode", "gcmx_last_ode_fused",
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_comm_init_local", "gcmx_local_group_steps",
     "gcmx_sync", "gcmx_stream",
@@ -121,6 +121,8 @@ def lib() -> ctypes.CDLL:
     L.gcmx_step_faces.argtypes = [vp, ctypes.c_double, ctypes.POINTER(Face)]
     L.gcmx_copy_box.argtypes = [vp, ip, ip, vp, ip]
     L.gcmx_ode_maxwell.argtypes = [vp, ctypes.c_double, dp, ctypes.c_int]
+    L.gcmx_step_ode.argtypes = [vp, ctypes.c_double, ctypes.POINTER(Face), dp, ctypes.c_int]
+    L.gcmx_last_ode_fused.argtypes = [vp]
     L.gcmx_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
     L.gcmx_comm_init.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int]
@@ -280,9 +282,7 @@ class Context:
         v = (ctypes.c_double * max(1, len(values)))(*values)
         _check(lib().gcmx_border_apply(self._ptr, handle.ptr, len(quantities), q, v))
 
-    def step_faces(self, tau: float, faces: Sequence[Optional[Sequence[tuple]]]):
-        """gcmx_step_faces: faces[2*axis + (side > 0)] is None (no condition) or a
-        list of (quantity code, value) in the reference's application order."""
+    def _faces(self, faces):
         arr = (Face * (2 * self.dim))()
         for f, lst in enumerate(faces[:2 * self.dim]):
             if lst is None:
@@ -292,7 +292,23 @@ class Context:
             for k, (q, v) in enumerate(lst):
                 arr[f].quantities[k] = q
                 arr[f].values[k] = v
-        _check(lib().gcmx_step_faces(self._ptr, tau, arr))
+        return arr
+
+    def step_faces(self, tau: float, faces: Sequence[Optional[Sequence[tuple]]]):
+        """gcmx_step_faces: faces[2*axis + (side > 0)] is None (no condition) or a
+        list of (quantity code, value) in the reference's application order."""
+        _check(lib().gcmx_step_faces(self._ptr, tau, self._faces(faces)))
+
+    def step_ode(self, tau: float, tau0: Sequence[float], faces=None):
+        """gcmx_step_ode: the step (gcmx_step, or gcmx_step_faces with `faces`) then
+        MaxwellViscosityOde, folded into the one-pass step's stores where it can be."""
+        t0 = np.ascontiguousarray(tau0, dtype=np.float64).reshape(-1)
+        arr = self._faces(faces) if faces is not None else None
+        _check(lib().gcmx_step_ode(self._ptr, tau, arr, _dp(t0), t0.shape[0]))
+
+    @property
+    def last_ode_fused(self) -> bool:
+        return bool(lib().gcmx_last_ode_fused(self._ptr))
 
     def copy_box(self, dst_min, dst_max, src: "Context", src_min):
         pad = lambda s: list(s) + [0] * (3 - len(s))

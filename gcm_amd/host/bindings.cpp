@@ -101,6 +101,14 @@ struct PyEngine {
 		static const char* names[] = {"auto", "generic", "split", "fused"};
 		return names[gcmx_last_step_path(c)];
 	}
+	/// Whether the body's last step folded its Maxwell ODE into the one-pass step (gcmx_last_ode_fused).
+	bool odeFused(size_t id) {
+		gcmx_ctx* c = nullptr;
+		if (D == 1) c = as<1>().getMesh(id)->ctx();
+		else if (D == 2) c = as<2>().getMesh(id)->ctx();
+		else c = as<3>().getMesh(id)->ctx();
+		return gcmx_last_ode_fused(c) != 0;
+	}
 	real maximalEigenvalue(size_t id) {
 		if (D == 1) return as<1>().getMesh(id)->getMaximalEigenvalue();
 		if (D == 2) return as<2>().getMesh(id)->getMaximalEigenvalue();
@@ -535,6 +543,7 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    .def("pde", &PyEngine::pde, "current layer of a body, all nodes incl. ghosts [..., M]")
 	    .def("path", &PyEngine::path)
 	    .def("last_path", &PyEngine::lastPath)
+	    .def("ode_fused", &PyEngine::odeFused)
 	    .def("sync", &PyEngine::sync, py::arg("body") = 0)
 	    .def("maximal_eigenvalue", &PyEngine::maximalEigenvalue)
 	    .def_property_readonly("steps", [](PyEngine& p) { return p.e->stepsDone(); })

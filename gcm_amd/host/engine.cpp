@@ -518,13 +518,26 @@ void Engine<D>::nextTimeStep() {
 		plain = plain && b.border->empty() && b.contacts.empty();
 		faces = faces && b.border->uniformFaces() && b.contacts.empty();
 	}
+	// A body whose only ODE is MaxwellViscosityOde hands it to the library with
+	// the step (gcmx_step_ode): the same results as the stages followed by the ODE
+	// (Engine.cpp:115-119), in one pass over the layer where the step is fused.
+	auto oneMaxwell = [](const Body& b) {
+		return b.odes.size() == 1 && dynamic_cast<const HipMaxwellViscosityOde<D>*>(b.odes[0].get()) != nullptr;
+	};
 	if (plain) {
 		// No border or contact work between the stages: one gcmx_step per body
 		// (identical results; lets the library use its fused kernels).
-		for (Body& b : bodies)
-			std::static_pointer_cast<HipGridCharacteristicMethod<D>>(b.gcm)->step(
-			    Clock::TimeStep(), dynamic_cast<HipMesh<D>&>(*b.mesh));
-		applyOdes();
+		for (Body& b : bodies) {
+			HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(*b.mesh);
+			if (oneMaxwell(b)) {
+				const auto& tau0 = mesh.deviceTau0();
+				gcmxCheck(gcmx_step_ode(mesh.ctx(), Clock::TimeStep(), nullptr, tau0.data(), (int)tau0.size()),
+				          "gcmx_step_ode");
+				continue;
+			}
+			std::static_pointer_cast<HipGridCharacteristicMethod<D>>(b.gcm)->step(Clock::TimeStep(), mesh);
+			for (auto& ode : b.odes) ode->apply(*b.mesh, Clock::TimeStep());
+		}
 		return;
 	}
 	if (faces) {
@@ -535,10 +548,16 @@ void Engine<D>::nextTimeStep() {
 		for (Body& b : bodies) {
 			gcmx_face f[6];
 			b.border->faces(f);
-			gcmxCheck(gcmx_step_faces(dynamic_cast<HipMesh<D>&>(*b.mesh).ctx(), Clock::TimeStep(), f),
-			          "gcmx_step_faces");
+			HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(*b.mesh);
+			if (oneMaxwell(b)) {
+				const auto& tau0 = mesh.deviceTau0();
+				gcmxCheck(gcmx_step_ode(mesh.ctx(), Clock::TimeStep(), f, tau0.data(), (int)tau0.size()),
+				          "gcmx_step_ode");
+				continue;
+			}
+			gcmxCheck(gcmx_step_faces(mesh.ctx(), Clock::TimeStep(), f), "gcmx_step_faces");
+			for (auto& ode : b.odes) ode->apply(*b.mesh, Clock::TimeStep());
 		}
-		applyOdes();
 		return;
 	}
 	for (int stage = 0; stage < D; stage++) {

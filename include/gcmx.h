@@ -191,6 +191,18 @@ gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dst_min[3], const int dst_max
  * them).  The factor is computed on the host with the C library's exp. */
 gcmx_status gcmx_ode_maxwell(gcmx_ctx* ctx, double tau, const double* tau0, int n_mat);
 
+/* One time step followed by the Maxwell ODE, as cubic::Engine::nextTimeStep runs
+ * them (the stages, then the bodies' ODEs, Engine.cpp:90-121): identical results
+ * to gcmx_step (faces == NULL) or gcmx_step_faces, then gcmx_ode_maxwell.  When
+ * the step runs the one-pass kernel over one material, the factor multiplies the
+ * stresses in the kernel's store epilogue (no second pass over the layer; with an
+ * X-slab exchange the neighbours receive the scaled planes); otherwise the
+ * separate scaling pass follows.  gcmx_last_ode_fused: 1 when the last
+ * gcmx_step_ode folded the ODE into the step. */
+gcmx_status gcmx_step_ode(gcmx_ctx* ctx, double tau, const gcmx_face* faces, const double* tau0,
+                          int n_mat);
+int         gcmx_last_ode_fused(gcmx_ctx* ctx);
+
 /* ---- multi-GPU X-slab halo (replaces the dead MPI slab design,
  * src/test/TestMPI.cpp:33-50, 92-155, and the in-process ContactCopier for
  * bodies split along X) ---------------------------------------------------------*/
@@ -399,8 +411,8 @@ long long   gcmx_all_nodes(gcmx_ctx* ctx);
 size_t      gcmx_device_bytes(gcmx_ctx* ctx);
 /* Measurement only (bench.py's roofline.copy_ceiling): the practical HBM rate
  * of this device for a flat copy of `bytes` bytes (half read, half written;
- * 16 B per lane per access, four loads in flight per lane, non-temporal
- * stores, 2048 blocks of 256 threads, grid-stride).  Median of `reps` timed copies
+ * 16 B per lane, non-temporal stores, 32 768 blocks of 256 threads, grid-stride:
+ * the fastest of the flat-copy shapes tools/copy_probe.hip times).  Median of `reps` timed copies
  * after one warm copy; *ms_out = that copy's duration (HIP events on the
  * ctx stream).  Allocates and frees 2 x bytes / 2 on the context's device. */
 gcmx_status gcmx_copy_ceiling(gcmx_ctx* ctx, size_t bytes, int reps, float* ms_out);

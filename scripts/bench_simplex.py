@@ -4,6 +4,9 @@ The reference's simplex configs run on CGAL meshes of cube.off (config 4) and
 layers_with_fracture.off (config 5); CGAL is absent, so the meshes are jittered
 Kuhn tetrahedralisations:
 
+* cubetask: BASELINE config 4 itself, parseTaskCube (launcher/main.cpp:547-639):
+            cube.off at spatial step 0.05, Courant 1, FIXED_FORCE zero everywhere
+            and the step traction t < 0.25 ? -1 : 0 on the x <= 0.01 face (--n ignored);
 * cube:     the unit cube, n^3 cubes, free surface on every face (the reference's
             parseTaskCgal3d: FIXED_FORCE 0 from an InfiniteArea), pressure sphere;
 * fracture: the 0.16 x 0.16 x 0.04 layer of layers_with_fracture.off with its
@@ -16,7 +19,7 @@ contact correctors included).  Timed: K steps of SimplexEngine.run_steps between
 two stream synchronisations, inputs resident on the device.  Prints one JSON line
 per workload.
 
-    python scripts/bench_simplex.py [--workloads cube,fracture,layered] [--n 64]
+    python scripts/bench_simplex.py [--workloads cubetask,cube,fracture,layered] [--n 64]
 """
 import argparse
 import json
@@ -29,7 +32,11 @@ sys.path.insert(0, ROOT)
 
 
 def build(name, n):
-    from tests.simplex_spec import FREE_BORDER, fracture_task, host_task, layered_task
+    from tests.simplex_spec import FREE_BORDER, cube_task, fracture_task, host_task, layered_task
+    if name == "cubetask":
+        return cube_task(), ("parseTaskCube (main.cpp:547-639): cube.off at spatial step 0.05 "
+                             "(20^3 Kuhn cubes), Courant 1, free surface + the x <= 0.01 traction "
+                             "(0, 0, t < 0.25 ? -1 : 0)")
     if name == "cube":
         return host_task(n, 1.0, 0.1, 7, border=FREE_BORDER), f"unit cube, {n}^3 Kuhn cubes"
     if name == "fracture":

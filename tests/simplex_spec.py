@@ -56,6 +56,35 @@ MIXED_BORDER = [(("infinite",), "FIXED_FORCE", ZERO, True),
                  (lambda t: 0.1 * t, lambda t: 0.0, lambda t: -0.05), True)]
 
 
+# BASELINE config 4: parseTaskCube (launcher/main.cpp:547-639) -- meshes/cube.off
+# meshed at spatial step 0.05 (here: the jittered Kuhn box mesh of the unit cube
+# at h = 0.05, carved by the .off surface, which keeps every cell), Courant 1,
+# FIXED_FORCE zero everywhere and, on the x <= 0.01 face, the traction
+# (0, 0, t < 0.25 ? -1 : 0); no initial perturbation (the load drives the wave).
+CUBE_OFF = os.path.join(os.path.dirname(__file__), "golden", "cube.off")
+CUBE_BORDER = [(("infinite",), "FIXED_FORCE", ZERO, True),
+               (("box", (-10.0, -10.0, -10.0), (0.01, 10.0, 10.0)), "FIXED_FORCE",
+                (lambda t: 0.0, lambda t: 0.0, lambda t: -1.0 if t < 0.25 else 0.0), True)]
+
+
+def cube_task(h=0.05, courant=1.0, jitter=0.1, seed=7, snaps=100):
+    from gcm_amd import _gcm_host as H
+    n = int(round(1.0 / h))
+    t = H.Task()
+    t.dimensionality = 3
+    t.grid = "SIMPLEX"
+    t.courant = courant
+    t.number_of_snaps = snaps
+    t.add_body(0, [1, 1, 1], [0, 0, 0])
+    t.set_body_material(0, 4, 2, 1)
+    t.calculation_basis = [1, 0, 0, 0, 1, 0, 0, 0, 1]
+    t.set_simplex_box([n, n, n], [0, 0, 0], [1, 1, 1], jitter, seed)
+    t.set_simplex_domain_off(CUBE_OFF)
+    for area, kind, values, multi in CUBE_BORDER:
+        t.add_simplex_border_condition(area, kind, list(values), multi)
+    return t
+
+
 # BASELINE config 5: meshes/layers_with_fracture.off -- the 0.16 x 0.16 x 0.04
 # layer with a tetrahedral fracture (cavity) inside, free surface everywhere
 # (the reference's data file, copied as a fixture into tests/golden/).

@@ -19,6 +19,12 @@ def H():
     return _gcm_host
 
 
+@pytest.fixture(scope="module")
+def G():
+    import gcm_amd.gcmx as G
+    return G
+
+
 def inner(arr, bs, D):
     sl = tuple(slice(bs, -bs) for _ in range(D))
     return arr[sl]
@@ -194,6 +200,35 @@ def test_engine_maxwell_ode(H, D, tau0_b, path):
     assert he.path(0) == path
     oe, he = run_both(H, s)
     assert_bodies_equal(oe, he, s)
+    # one material on the one-pass path: the ODE rides in the step's store epilogue
+    assert he.ode_fused(0) == (path == "fused")
+
+
+@pytest.mark.parametrize("faces", [False, True])
+def test_step_ode_fused_equals_step_then_ode(G, faces):
+    """gcmx_step_ode == gcmx_step / gcmx_step_faces followed by gcmx_ode_maxwell,
+    bitwise, with the ODE folded into k_step_tx2's stores (one material; tau0 = 0
+    gives the factor exp(-inf) = 0).  Several materials keep the separate pass
+    (test_engine_maxwell_ode: the generic path)."""
+    from tests.helpers import context_for, oracle_body, random_state
+    q = G.QUANTITY_CODES
+    fc = [[(q["Sxx"], 0.0), (q["Sxy"], 0.0), (q["Sxz"], 0.0)], None,
+          [(q["Syy"], -0.3), (q["Syz"], 0.0)], [(q["Vy"], 0.1)],
+          [(q["Szz"], 0.0), (q["Sxz"], 0.0), (q["Syz"], 0.0)], None] if faces else None
+    for tau0, fused in ((3.0, True), (0.0, True)):
+        b = oracle_body(3, 2, [6, 20, 32])
+        random_state(b, seed=11, ghosts=False)
+        a, c = context_for(b), context_for(b)
+        for _ in range(3):
+            if faces:
+                a.step_faces(0.9, fc)
+            else:
+                a.step(0.9)
+            a.ode_maxwell(0.9, [tau0])
+            c.step_ode(0.9, [tau0], fc)
+        assert c.last_ode_fused == fused and c.last_path == "fused"
+        assert np.array_equal(a.download(), c.download())
+        a.close(); c.close()
 
 
 def test_engine_rejects_uncompilable_odes(H):

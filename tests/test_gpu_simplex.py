@@ -326,3 +326,33 @@ def test_unfusable_plan_runs_two_launches():
     border, inner = [0, 1], [2, 3, 4, 5, 6, 7]
     assert _raw_simplex_plan(G, border, inner, wn_vertex=5) == (0, 1, 0)
     assert _raw_simplex_plan(G, border, inner, wn_vertex=1) == (1, 1, 1)
+
+
+from tests.simplex_spec import CUBE_BORDER, cube_task  # noqa: E402
+
+
+@pytest.mark.timeout(600)
+def test_cube_task_matches_oracle_across_the_load_switch(H):
+    """BASELINE config 4 (parseTaskCube, launcher/main.cpp:547-639): meshes/cube.off
+    at spatial step 0.05 (9 261 vertices), Courant 1, free surface everywhere and
+    the traction (0, 0, t < 0.25 ? -1 : 0) on the x <= 0.01 face.  10 steps of
+    tau = 0.0336 run past t = 0.25, where the load switches off; the GPU (the
+    default engine: eight lanes, one launch per stage) equals the oracle bitwise
+    at the switch step and at the end."""
+    t = cube_task()
+    p = H.simplex_plans(t)
+    e = H.SimplexEngine(t)
+    o = oracle_engine(p, 1.0, CUBE_BORDER)
+    tau = e.time_step
+    assert tau == p["tau"]
+    switch = next(k for k in range(1, 20) if k * tau >= 0.25)  # b(t + tau) turns 0 at this step
+    done = 0
+    for target in (switch + 1, 10):
+        e.run_steps(target - done)
+        for _ in range(target - done):
+            o.step()
+        done = target
+        got, want = e.pde(), np.array(o.u)
+        assert np.array_equal(got, want), f"step {done}: {int((got != want).sum())} values differ"
+    assert e.fused_stages > 0
+    assert np.abs(got).max() > 0

@@ -410,3 +410,39 @@ def test_inm_mesher_rejects_unknown_materials(H, tmp_path):
     write_inm(path, P, C, [7] * len(C))
     with pytest.raises(Exception):
         H.simplex_plans(layered_task(3, inm=path))
+
+
+# ---- BASELINE config 4: parseTaskCube on meshes/cube.off ----------------------
+
+from tests.simplex_spec import CUBE_BORDER, CUBE_OFF, cube_task  # noqa: E402
+
+
+def test_cube_off_fixture():
+    """meshes/cube.off: the unit cube as 8 vertices and 12 triangles."""
+    pts, faces = _read_off(CUBE_OFF)
+    assert pts.shape == (8, 3) and faces.shape == (12, 3)
+    assert pts.min(0).tolist() == [0, 0, 0] and pts.max(0).tolist() == [1, 1, 1]
+
+
+def test_cube_task_plans_match_oracle(H):
+    """parseTaskCube (main.cpp:547-639) at its spatial step 0.05: the carved mesh
+    keeps every cell of the unit cube, the left-face traction condition owns
+    exactly the x <= 0.01 border nodes (the last containing condition wins), and
+    the border plan (nodes, conditions, normals, matrices, wave codes) equals the
+    oracle's decisions."""
+    p = H.simplex_plans(cube_task())
+    P = p["coords"]
+    assert len(P) == 21 ** 3 and len(p["cells"]) == 6 * 20 ** 3
+    e = oracle_engine(p, 1.0, CUBE_BORDER)
+    assert e.tau == p["tau"]
+    b = p["border_plan"]
+    assert list(b["nodes"]) == [x[0] for x in e.corrected]
+    assert list(b["cond"]) == [x[1] for x in e.corrected]
+    left = {int(i) for i, c in zip(b["nodes"], b["cond"]) if c == 1}
+    assert left == {int(i) for i in b["nodes"] if P[i][0] <= 0.01}
+    assert 0 < len(left) < len(b["nodes"])
+    nn = len(e.corrected)
+    for s in range(3):
+        for i, (it, ci, nrm) in enumerate(e.corrected):
+            outers = tuple(e.outers[s].get(it, []))
+            assert b["outer"][s * nn + i] == CODE.get(outers, 0 if not outers else 3)
