@@ -120,6 +120,10 @@ struct gcmx_ctx {
 	double tabs_tau = NAN;
 	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso structure)
 	IsoAxis iso[3] = {};           // per-axis values for the fast kernels (tau part in build_tables)
+	bool iso_het = false;          // per-node materials, every material of the iso structure (k_step_tx2 HET)
+	bool het_ok = false;           // this tau: floor(q) = 0 and equal axes for every material
+	std::vector<IsoAxis> het_iso;  // [mat]: tau-independent part (axis 0)
+	IsoAxis* het_d = nullptr;      // [mat] on the device, per tau
 	bool ghosts_touched = false;   // node-list border fills / contact copies / ghost uploads happened
 	bool last_ode_fused = false;   // the last gcmx_step_ode scaled the stresses in the step's epilogue
 	unsigned faces_written = 0;    // faces (bit 2*axis + side) whose ghosts a face fill wrote
@@ -285,6 +289,39 @@ gcmx_status build_tables(gcmx_ctx* c, double tau) {
 	}
 	HIP_TRY(hipMemcpyAsync(c->tabs_d, h.data(), h.size() * sizeof(AxisTable),
 	                       hipMemcpyHostToDevice, c->stream));
+	if (c->iso_het) {
+		// one IsoAxis per material for all three stages: the axes' tables must be
+		// bitwise equal (equal h) and every foot in [node, node + 1) (floor(q) = 0)
+		std::vector<IsoAxis> ht(c->n_mat);
+		bool ok = true;
+		for (int m = 0; m < c->n_mat && ok; m++) {
+			IsoAxis A[3];
+			for (int s = 0; s < 3 && ok; s++) {
+				const AxisTable& t = h[(size_t)m * D + s];
+				ok = iso_axis_extract(s, &c->U[((size_t)m * D + s) * M * M], &c->U1[((size_t)m * D + s) * M * M],
+				                      &c->L[((size_t)m * D + s) * M], A[s]);
+				for (int k = 1; k < 6 && ok; k++) {
+					const int ref = (k < 2) ? 0 : 2;
+					ok = t.kf[k] == t.kf[ref] && std::memcmp(t.coef[k], t.coef[ref], sizeof(t.coef[k])) == 0;
+				}
+				for (int i = 0; i < 3; i++) {
+					A[s].c1[i] = i < bs ? t.coef[0][i] : 0.0;
+					A[s].c2[i] = i < bs ? t.coef[2][i] : 0.0;
+				}
+				A[s].kf1 = t.kf[0];
+				A[s].kf2 = t.kf[2];
+				ok = ok && A[s].kf1 == 0 && A[s].kf2 == 0;
+			}
+			ok = ok && std::memcmp(&A[0], &A[1], sizeof(IsoAxis)) == 0 && std::memcmp(&A[0], &A[2], sizeof(IsoAxis)) == 0;
+			ht[m] = A[0];
+		}
+		c->het_ok = ok;
+		if (ok) {
+			if (!c->het_d) HIP_TRY(hipMalloc(&c->het_d, 256 * sizeof(IsoAxis)));
+			HIP_TRY(hipMemcpyAsync(c->het_d, ht.data(), ht.size() * sizeof(IsoAxis), hipMemcpyHostToDevice,
+			                       c->stream));
+		}
+	}
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	c->tabs_tau = tau;
 	return GCMX_OK;
@@ -489,10 +526,25 @@ void refresh_fast(gcmx_ctx* c) {
 		fits = iso_axis_extract(sx, &c->U[(size_t)sx * M * M], &c->U1[(size_t)sx * M * M],
 		                        &c->L[(size_t)sx * M], c->iso[sx]);
 	c->iso_fast = fits;
+	// heterogeneous one-pass step: per-node ids and every material of the structure
+	bool het = !fits && D == 3 && c->mat_d != nullptr && c->n_mat >= 1 && fast_layout_ok(c->geo) &&
+	           het_supported(c->geo);
+	for (int m = 0; het && m < c->n_mat; m++)
+		for (int sx = 0; het && sx < D; sx++) {
+			IsoAxis tmp{};
+			het = iso_axis_extract(sx, &c->U[((size_t)m * D + sx) * M * M], &c->U1[((size_t)m * D + sx) * M * M],
+			                       &c->L[((size_t)m * D + sx) * M], tmp);
+		}
+	c->iso_het = het;
+	c->het_ok = false;
 	c->tabs_tau = NAN;
 }
 
 gcmx_path effective_path(gcmx_ctx* c) {
+	if (c->iso_het) {  // per-node materials: the one-pass step or the generic stages
+		if (c->path == GCMX_PATH_GENERIC || c->path == GCMX_PATH_SPLIT || c->ghosts_touched) return GCMX_PATH_GENERIC;
+		return GCMX_PATH_FUSED;
+	}
 	if (c->D != 3 || !c->iso_fast || c->bs > 3) return GCMX_PATH_GENERIC;
 	if (c->path == GCMX_PATH_GENERIC) return GCMX_PATH_GENERIC;
 	if (c->path == GCMX_PATH_SPLIT) return GCMX_PATH_SPLIT;
@@ -539,7 +591,7 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	}
 	const Geo& g = c->geo;
 	const double bytes = node_stage_bytes(c) * (double)g.n_inner;
-	const gcmx_path p = effective_path(c);
+	const gcmx_path p = c->iso_het ? GCMX_PATH_GENERIC : effective_path(c);  // no per-stage het kernels
 	bool ok;
 	if (p == GCMX_PATH_GENERIC) {
 		Timed t(c, "stage_generic", bytes, c->stream);
@@ -696,6 +748,7 @@ void gcmx_destroy(gcmx_ctx* c) {
 	hipFree(c->mat_d);
 	hipFree(c->nodes_d);
 	hipFree(c->ode_d);
+	hipFree(c->het_d);
 	if (c->ev_ready) hipEventDestroy(c->ev_ready);
 	if (c->ev_halo) hipEventDestroy(c->ev_halo);
 	if (c->ev_fork) hipEventDestroy(c->ev_fork);
@@ -913,7 +966,9 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 	const bool halo = has_halo(c);
 	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows) {
 		Timed t(c, name, plane_bytes * (x1 - x0), st);
-		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb, &t.kname);
+		const HetMaterials het{c->het_d, c->mat_d};
+		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb, &t.kname,
+		                        c->iso_het ? &het : nullptr);
 	};
 	const gcmx_schedule sched =
 	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_XSLAB : GCMX_SCHED_SINGLE) : c->sched;
@@ -998,7 +1053,7 @@ gcmx_status step_impl(gcmx_ctx* c, double tau, const StepOde& ode) {
 	gcmx_status s = build_tables(c, tau);
 	if (s) return s;
 	c->last_ode_fused = false;
-	if (effective_path(c) != GCMX_PATH_FUSED || c->faces_written != 0) {
+	if (effective_path(c) != GCMX_PATH_FUSED || c->faces_written != 0 || (c->iso_het && !c->het_ok)) {
 		for (int a = 0; a < c->D; a++) {
 			s = stage_impl(c, a, tau);
 			if (s) return s;
@@ -1073,7 +1128,7 @@ gcmx_status step_faces_impl(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 	// free of PRESSURE (its trace needs components the fused ghosts do not form)
 	// and no face may hold ghosts written earlier but not refreshed now.
 	bool fused = D == 3 && effective_path(c) == GCMX_PATH_FUSED && fused_faces_supported(c->geo) &&
-	             (c->faces_written & ~on) == 0;
+	             (c->faces_written & ~on) == 0 && (!c->iso_het || c->het_ok);
 	FaceBC fb{};
 	for (int f = 2; f < 6 && fused; f++) {
 		if (!((on >> f) & 1u)) continue;

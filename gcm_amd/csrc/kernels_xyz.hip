@@ -270,6 +270,20 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	} while (0)
 #endif
 
+// Runs f(k) once for every distinct key among the active lanes, with k uniform
+// (an SGPR value: per-material tables indexed by it are scalar loads), every lane
+// inside the call whose key is k.  One pass when the wave's key is uniform.
+template <class F>
+__device__ __forceinline__ void waterfall(unsigned key, F f) {
+	for (;;) {
+		const unsigned k = __builtin_amdgcn_readfirstlane(key);
+		if (key == k) {
+			f(k);
+			break;
+		}
+	}
+}
+
 // Component held in window slot q of a stage whose window mask is `mask`.
 __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 	int n = 0;
@@ -323,10 +337,20 @@ __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 //
 // If the launch has an odd number of planes the last thread's second node is
 // computed from clamped (valid) planes and not stored.
-template <int BS, int ZT, bool KF0, bool UNI, bool FACES>
+//
+// HET: per-node materials (heterogeneous media, TestEngine.cpp:139-296's layers).
+// Every node's stages use its own material's tables mtab[mat[node]] (per material
+// the three axes' tables are identical and floor(q) = 0, checked on the host), as
+// GridCharacteristicMethod::stage takes each node's own matrices.  The tables are
+// applied through `waterfall` over the materials present in a wave, so they stay
+// scalar operands; where the two nodes of a lane differ in material, their X
+// stages run without the shared differences (pair_update per node).
+template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET>
 __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
     const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY_,
-    IsoAxis AZ_, int x0, int chunk, int nplanes, FaceBC fb) {
+    IsoAxis AZ_, int x0, int chunk, int nplanes, FaceBC fb, const IsoAxis* __restrict__ mtab,
+    const uint8_t* __restrict__ mat) {
+	static_assert(!HET || (KF0 && UNI), "heterogeneous step: floor(q) = 0, Z == ZT, equal axes");
 	const IsoAxis& AY = UNI ? AX : AY_;
 	const IsoAxis& AZ = UNI ? AX : AZ_;
 	constexpr unsigned WMX = iso_window(0);
@@ -433,11 +457,20 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			w[1][k] = ldx(pair_sig(0, P), k, r);
 		}
 	};
-	// Rows 2P, 2P+1 of r = diag(U * V) for both nodes.
-	auto pair_rows = [&](auto PC, const PairWin& w, double (&rr)[2][9]) {
+	// Rows 2P, 2P+1 of r = diag(U * V) for both nodes; A0 / A1: the nodes' tables
+	// (`same`: one table, the shared-difference form).
+	auto pair_rows = [&](auto PC, const PairWin& w, double (&rr)[2][9], const IsoAxis& A0, const IsoAxis& A1,
+	                     bool same) {
 		constexpr int P = decltype(PC)::value;
-		if constexpr (KF0) {
-			const double* c = (P == 0) ? AX.c1 : AX.c2;
+		if (KF0 && !same) {  // HET, two materials in the lane: per node, no shared differences
+#pragma unroll
+			for (int t = 0; t < 2; t++)
+				pair_update<0, BS, true, P>(
+				    t ? A1 : A0, [&](int j, int o) { return j == pair_vel(0, P) ? w[0][t + BS + o] : w[1][t + BS + o]; },
+				    rr[t][2 * P], rr[t][2 * P + 1]);
+		} else if constexpr (KF0) {
+			const IsoAxis& AS = A0;  // one table for both nodes
+			const double* c = (P == 0) ? AS.c1 : AS.c2;
 			double im[2][2], ip[2][2];  // [vel/sig][node]
 #pragma unroll
 			for (int v = 0; v < 2; v++) {
@@ -476,15 +509,15 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll
 			for (int t = 0; t < 2; t++) {
 				rr[t][2 * P] = RowSum<0, false, 2 * P>::go(
-				    AX, [&](int j) { return j == pair_vel(0, P) ? im[0][t] : im[1][t]; }, 0.0, true);
+				    AS, [&](int j) { return j == pair_vel(0, P) ? im[0][t] : im[1][t]; }, 0.0, true);
 				rr[t][2 * P + 1] = RowSum<0, false, 2 * P + 1>::go(
-				    AX, [&](int j) { return j == pair_vel(0, P) ? ip[0][t] : ip[1][t]; }, 0.0, true);
+				    AS, [&](int j) { return j == pair_vel(0, P) ? ip[0][t] : ip[1][t]; }, 0.0, true);
 			}
 		} else {
 #pragma unroll
 			for (int t = 0; t < 2; t++)
 				pair_update<0, BS, KF0, P>(
-				    AX, [&](int j, int o) { return j == pair_vel(0, P) ? w[0][t + BS + o] : w[1][t + BS + o]; },
+				    t ? A1 : A0, [&](int j, int o) { return j == pair_vel(0, P) ? w[0][t + BS + o] : w[1][t + BS + o]; },
 				    rr[t][2 * P], rr[t][2 * P + 1]);
 		}
 	};
@@ -509,17 +542,20 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 	// X stage of row r for both nodes: pair 2 and the node-only components are
 	// issued first, then the pairs are consumed in order.
-	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9]) {
+	// material of node (x + t, r) (HET; rows outside [0, Y) take row Y-1's: their
+	// X results come from zero ghost rows or are replaced by a face's mirror)
+	auto mat_of = [&](int t, int r) -> unsigned {
+		const int xx = (t == 1 && !two) ? x : x + t;
+		const int rr_ = r < Y ? r : Y - 1;
+		return mat[((size_t)xx * Y + rr_) * Z + z];
+	};
+	auto x_compute = [&](const XPre& pre, const PairWin& wc, const double (&cv)[2][9], double (&xr)[2][9],
+	                     const IsoAxis& A0, const IsoAxis& A1, bool same) {
 		double rr[2][9], n0[2][9];
-		PairWin wc;
-		double cv[2][9];
-		pair_load(P2{}, wc, r);
-		cv_load(cv, r);
+		pair_rows(P0{}, pre.a, rr, A0, A1, same);
+		pair_rows(P1{}, pre.b, rr, A0, A1, same);
 		sched_fence();
-		pair_rows(P0{}, pre.a, rr);
-		pair_rows(P1{}, pre.b, rr);
-		sched_fence();
-		pair_rows(P2{}, wc, rr);
+		pair_rows(P2{}, wc, rr, A0, A1, same);
 #pragma unroll
 		for (int t = 0; t < 2; t++) {
 			n0[t][pair_vel(0, 0)] = pre.a[0][t + BS];
@@ -532,8 +568,26 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		sched_fence();
 #pragma unroll
 		for (int t = 0; t < 2; t++) {
-			center_update<0>(AX, [&](int j) { return ((WMX >> j) & 1u) ? n0[t][j] : cv[t][j]; }, rr[t]);
-			u1_apply<0>(AX, rr[t], xr[t]);
+			const IsoAxis& A = t ? A1 : A0;
+			center_update<0>(A, [&](int j) { return ((WMX >> j) & 1u) ? n0[t][j] : cv[t][j]; }, rr[t]);
+			u1_apply<0>(A, rr[t], xr[t]);
+		}
+	};
+	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9]) {
+		PairWin wc;
+		double cv[2][9];
+		unsigned key = 0;
+		if constexpr (HET) key = mat_of(0, r) | (mat_of(1, r) << 8);
+		pair_load(P2{}, wc, r);
+		cv_load(cv, r);
+		sched_fence();
+		if constexpr (HET) {
+			waterfall(key, [&](unsigned k) {
+				const unsigned m0 = k & 255u, m1 = k >> 8;
+				x_compute(pre, wc, cv, xr, mtab[m0], mtab[m1], m0 == m1);
+			});
+		} else {
+			x_compute(pre, wc, cv, xr, AX, AX, true);
 		}
 	};
 
@@ -606,11 +660,16 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	auto y_stage = [&](int y, double (&yv)[2][9]) {
 		const double* cp = cl_at(y);
 #pragma unroll
-		for (int t = 0; t < 2; t++)
-			node_update<1, BS, KF0>(
-			    AY, [&](int j, int o) { return win[t][wslot(WMY, j)][BS + o]; },
-			    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cp[(t * NCY + wslot(CMY, j)) * ZT]; },
-			    yv[t]);
+		for (int t = 0; t < 2; t++) {
+			auto go = [&](const IsoAxis& A) {
+				node_update<1, BS, KF0>(
+				    A, [&](int j, int o) { return win[t][wslot(WMY, j)][BS + o]; },
+				    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cp[(t * NCY + wslot(CMY, j)) * ZT]; },
+				    yv[t]);
+			};
+			if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mtab[k]); });
+			else go(AY);
+		}
 	};
 	// hand the Y results of row y to the Z stage: NB, own region + edge ring +
 	// counter; otherwise the block buffer between two barriers
@@ -690,14 +749,18 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// Z stage of node t of row y and its 9 stores
 	auto z_stage_store = [&](int t, int y, const double (&yv)[2][9]) {
 		double zv[9];
-		if constexpr (NB)
-			node_update<2, BS, KF0>(
-			    AZ, [&](int j, int o) { return rg[wv][t][wslot(WMZ, j)][BS + ln + o]; },
-			    [&](int j) { return ((WMZ >> j) & 1u) ? rg[wv][t][wslot(WMZ, j)][BS + ln] : yv[t][j]; }, zv);
-		else
-			node_update<2, BS, KF0>(
-			    AZ, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
-			    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
+		auto go = [&](const IsoAxis& A) {
+			if constexpr (NB)
+				node_update<2, BS, KF0>(
+				    A, [&](int j, int o) { return rg[wv][t][wslot(WMZ, j)][BS + ln + o]; },
+				    [&](int j) { return ((WMZ >> j) & 1u) ? rg[wv][t][wslot(WMZ, j)][BS + ln] : yv[t][j]; }, zv);
+			else
+				node_update<2, BS, KF0>(
+				    A, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
+				    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
+		};
+		if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mtab[k]); });
+		else go(AZ);
 		if (fb.ode_on) {  // MaxwellViscosityOde: sigma *= exp(-tau / tau0), the stored product (Ode.hpp:34-35)
 #pragma unroll
 			for (int c = 3; c < 9; c++) zv[c] = zv[c] * fb.ode;
@@ -826,11 +889,11 @@ static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
 }
 
 // The instance a launch runs, as a readable symbol (gcmx_profile_kernel).
-template <int BS, int ZT, bool KF0, bool UNI, bool FACES>
+template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET>
 static const char* tx2_name() {
 	static const std::string s = "k_step_tx2<" + std::to_string(BS) + ", " + std::to_string(ZT) + ", " +
 	                             (KF0 ? "KF0" : "!KF0") + ", " + (UNI ? "UNI" : "!UNI") + ", " +
-	                             (FACES ? "FACES" : "!FACES") + ">";
+	                             (FACES ? "FACES" : "!FACES") + (HET ? ", HET" : "") + ">";
 	return s.c_str();
 }
 template <int BS, int ZT, bool KF0, bool UNI>
@@ -854,7 +917,8 @@ static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK
 
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                         int x1, hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname) {
+                         int x1, hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname,
+                         const HetMaterials* het) {
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
 	const bool uni = kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
@@ -867,18 +931,26 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair);
 			const FaceBC none{};
 			const FaceBC& f = fb ? *fb : none;
+			const IsoAxis* mt = het ? het->tab : nullptr;
+			const uint8_t* mi = het ? het->ids : nullptr;
 			auto go = [&](auto K, const char* name) {
-				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, f);
+				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, f,
+				                   mt, mi);
 				*kname = name;
 			};
+			if (het) {  // the caller checked Z == ZT, KF0 and equal axes per material
+				if (fb && fb->on) go(k_step_tx2<BS, ZT, true, true, true, true>, tx2_name<BS, ZT, true, true, true, true>());
+				else go(k_step_tx2<BS, ZT, true, true, false, true>, tx2_name<BS, ZT, true, true, false, true>());
+				return;
+			}
 			if (fb && fb->on) {
-				if (uni) go(k_step_tx2<BS, ZT, true, true, true>, tx2_name<BS, ZT, true, true, true>());
-				else if (kf0) go(k_step_tx2<BS, ZT, true, false, true>, tx2_name<BS, ZT, true, false, true>());
-				else go(k_step_tx2<BS, ZT, false, false, true>, tx2_name<BS, ZT, false, false, true>());
+				if (uni) go(k_step_tx2<BS, ZT, true, true, true, false>, tx2_name<BS, ZT, true, true, true, false>());
+				else if (kf0) go(k_step_tx2<BS, ZT, true, false, true, false>, tx2_name<BS, ZT, true, false, true, false>());
+				else go(k_step_tx2<BS, ZT, false, false, true, false>, tx2_name<BS, ZT, false, false, true, false>());
 			} else {
-				if (uni) go(k_step_tx2<BS, ZT, true, true, false>, tx2_name<BS, ZT, true, true, false>());
-				else if (kf0) go(k_step_tx2<BS, ZT, true, false, false>, tx2_name<BS, ZT, true, false, false>());
-				else go(k_step_tx2<BS, ZT, false, false, false>, tx2_name<BS, ZT, false, false, false>());
+				if (uni) go(k_step_tx2<BS, ZT, true, true, false, false>, tx2_name<BS, ZT, true, true, false, false>());
+				else if (kf0) go(k_step_tx2<BS, ZT, true, false, false, false>, tx2_name<BS, ZT, true, false, false, false>());
+				else go(k_step_tx2<BS, ZT, false, false, false, false>, tx2_name<BS, ZT, false, false, false, false>());
 			}
 			return;
 		}
@@ -902,13 +974,14 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 
 template <int BS>
 static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                          int x1, hipStream_t st, int ch, const FaceBC* fb, const char** kn) {
+                          int x1, hipStream_t st, int ch, const FaceBC* fb, const char** kn,
+                          const HetMaterials* het) {
 	const int Z = g.sizes[2];
-	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st, ch, fb, kn);
-	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st, ch, fb, kn);
-	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st, ch, fb, kn);
-	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st, ch, fb, kn);
-	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st, ch, fb, kn);
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
 	return true;
 }
 
@@ -920,22 +993,29 @@ extern "C" int gcmx_diag_tx2(unsigned long long* out) {  // 16 x 8 counters, the
 }
 #endif
 
+bool het_supported(const Geo& g) {
+	const int Z = g.sizes[2];
+	return fused_supported(g) && g.bs <= 2 && (Z == 64 || Z == 128 || Z == 256 || Z == 512);
+}
+
 bool fused_faces_supported(const Geo& g) {
 	return fused_supported(g) && g.bs <= 2 && g.sizes[2] <= 512 && g.sizes[1] >= 2 * g.bs + 2 &&
 	       g.sizes[2] >= 2 * g.bs + 2;
 }
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                      int x1, hipStream_t st, int chunk, const FaceBC* faces, const char** kname) {
+                      int x1, hipStream_t st, int chunk, const FaceBC* faces, const char** kname,
+                      const HetMaterials* het) {
 	const char* dummy = nullptr;
 	const char** kn = kname ? kname : &dummy;
 	if (!fused_supported(g) || x1 <= x0) return false;
+	if (het && !het_supported(g)) return false;
 	if (faces && faces->on && !fused_faces_supported(g)) return false;
 	if (faces && faces->ode_on && !(g.bs <= 2 && g.sizes[2] <= 512)) return false;  // k_fused_xyz has no epilogue
 	switch (g.bs) {
-	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk, faces, kn);
-	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk, faces, kn);
-	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st, chunk, faces, kn);
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk, faces, kn, het);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk, faces, kn, het);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st, chunk, faces, kn, het);
 	default: return false;
 	}
 }

@@ -78,9 +78,18 @@ bool fused_faces_supported(const Geo& g);
 // `chunk`: y rows per block (0 = automatic, kernels_xyz.hip: xyz_chunk_for).
 // `faces`: y/z face conditions and the ODE factor (null, or on == 0: y/z ghosts of
 // both layers are zero); the ODE factor needs the k_step_tx2 path (bs <= 2, Z <= 512).
+// Per-node materials for the one-pass step (k_step_tx2<..., HET>): per material
+// one IsoAxis (the three axes' tables identical, floor(q) = 0), the device ids of
+// the inner nodes in linear [x][y][z] order.
+struct HetMaterials {
+	const IsoAxis* tab;
+	const uint8_t* ids;
+};
+// The heterogeneous one-pass step needs bs <= 2 and Z in {64, 128, 256, 512}.
+bool het_supported(const Geo& g);
 // `kname`: set to the launched instance's symbol (a static string).
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,
-                      const char** kname = nullptr);
+                      const char** kname = nullptr, const HetMaterials* het = nullptr);
 
 }  // namespace gcmx

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 FACE_FORCE = {0: ["Sxx", "Sxy", "Sxz"], 1: ["Sxy", "Syy", "Syz"], 2: ["Sxz", "Syz", "Szz"]}
 
 
-def task(n, maxwell):
+def task(n, maxwell, layers=False, free=True):
     from gcm_amd import _gcm_host as H
     t = H.Task()
     t.dimensionality = 3
@@ -30,9 +30,13 @@ def task(n, maxwell):
     t.number_of_snaps = 10 ** 6
     t.add_body(0, [n, n, n], [0, 0, 0])
     t.set_default_material(4.0, 2.0, 1.0, tau0=50.0 if maxwell else 0.0)
+    if layers:  # a second material in the upper half along x (TestEngine.cpp:139-296's two layers)
+        t.add_material(("box", (n / 2 - 0.5, -1, -1), (2 * n, 2 * n, 2 * n)), 2.0, 1.0, 0.5,
+                       tau0=40.0 if maxwell else 0.0, number=1)
     t.add_initial_quantity(("sphere", n / 4, (n / 2, n / 2, n / 2)), "PRESSURE", 10.0)
     for d, qs in FACE_FORCE.items():  # free surface: zero traction on both faces of axis d
-        t.add_border_condition(0, d, ("infinite",), {q: (lambda time: 0.0) for q in qs})
+        if free:
+            t.add_border_condition(0, d, ("infinite",), {q: (lambda time: 0.0) for q in qs})
     if maxwell:
         t.add_ode(0, "MAXWELL_VISCOSITY")
     return t
@@ -44,9 +48,13 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--maxwell", action="store_true")
+    ap.add_argument("--layers", action="store_true",
+                    help="two materials (per-node material ids: the heterogeneous path)")
+    ap.add_argument("--free", action=argparse.BooleanOptionalAction, default=True,
+                    help="free surfaces on all faces (--no-free: ghosts stay zero)")
     a = ap.parse_args()
     from gcm_amd import _gcm_host as H
-    e = H.Engine(task(a.n, a.maxwell))
+    e = H.Engine(task(a.n, a.maxwell, a.layers, a.free))
     e.run_steps(a.warmup)
     e.sync()
     t0 = time.perf_counter()
@@ -54,10 +62,12 @@ def main():
     e.sync()
     dt = time.perf_counter() - t0
     print(json.dumps({
-        "metric": "Mnode-steps/s, cubic engine with free surfaces" + (" + Maxwell ODE" if a.maxwell else ""),
+        "metric": "Mnode-steps/s, cubic engine" + (" with free surfaces" if a.free else "") +
+                  (" + Maxwell ODE" if a.maxwell else "") + (", two materials" if a.layers else ""),
         "value": round(a.n ** 3 * a.steps / dt / 1e6, 1), "unit": "Mnode-steps/s",
         "ms_per_step": round(dt / a.steps * 1e3, 4), "n": a.n, "steps": a.steps,
-        "path": e.path(0), "dtype": "f64"}), flush=True)
+        "path": e.path(0), "last_path": e.last_path(0), "ode_fused": e.ode_fused(0),
+        "dtype": "f64"}), flush=True)
 
 
 if __name__ == "__main__":

@@ -248,3 +248,41 @@ def test_engine_partial_face_uses_node_lists(H):
     got = he.pde(0)
     want = oe.bodies[0].pde.reshape(got.shape)
     assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"
+
+
+@pytest.mark.parametrize("layout", ["random", "layers"])
+def test_step_faces_heterogeneous_one_pass(G, layout):
+    """Per-node materials (k_step_tx2<..., FACES, HET>) with whole-face conditions:
+    free surfaces, a time-dependent normal force on y+ and a velocity on x-; each
+    node's stages use its own material (random ids, or two layers along x) ==
+    the oracle's per-stage border fills and stages, inner nodes bitwise."""
+    from tests.helpers import random_materials
+    sizes = [8, 18, 64]
+    conds = [(0, 0, free(0)), (1, 0, free(1)), (1, 1, free(1, lambda t: 0.3 * math.sin(2 * t))),
+             (2, 0, free(2)), (0, -1, {"Vx": lambda t: 0.05})]
+    bcs = []
+    for axis, side, vals in conds:
+        area = ("infinite",) if side == 0 else face_area(3, sizes, axis, side)
+        bcs.append(O.BorderCondition(axis, area, vals))
+    mats = [O.Material(4.0, 2.0, 1.0), O.Material(1.0, 2.0, 0.8)]
+    t_ = O.Task(D=3, border_size=2, h=[1.0] * 3, cubics={0: (sizes, [0, 0, 0])}, courant=0.9,
+                default_material=mats[0], inhomogeneities=[(("infinite",), mats[1])], number_of_snaps=1,
+                border_conditions={0: bcs})
+    b = O.Engine(t_).bodies[0]
+    if layout == "random":
+        random_materials(b, seed=8)
+    else:
+        its = b.inner_indices()
+        b.mat_id[b.flat_index(its)] = np.where(its[:, 0] < sizes[0] // 2, 0, 1).astype(np.uint8)
+    random_state(b, seed=9, ghosts=False)
+    ctx = context_for(b)
+    tau = 0.9 / math.sqrt(3.0)  # Courant 0.9 on the faster material (floor(q) = 0)
+    t = 0.0
+    for step in range(3):
+        for s in range(3):
+            b.apply_border(s, t)
+            b.stage(s, tau)
+        ctx.step_faces(tau, faces_at(3, conds, t))
+        assert ctx.last_path == "fused"
+        assert_same_inner(ctx, b, f"faces HET {layout} step {step}")
+        t += tau

@@ -362,3 +362,36 @@ def test_full_size_512_step_matches_oracle(G):
     for s in range(3):
         b.stage(s, 0.9, threads)
     assert np.array_equal(b.inner_view(got), b.inner_view())
+
+
+@pytest.mark.parametrize("bs,sizes,layout", [(2, [6, 20, 64], "random"), (2, [7, 9, 128], "random"),
+                                             (1, [5, 12, 64], "random"), (2, [8, 16, 256], "layers"),
+                                             (2, [6, 24, 512], "layers")])
+def test_heterogeneous_one_pass_step_matches_oracle(G, bs, sizes, layout):
+    """Per-node materials on the one-pass step (k_step_tx2<..., HET>): every node's
+    three stages use its own material's tables (GridCharacteristicMethod::stage
+    takes each node's matrices), applied per wave through the materials present;
+    random ids put two materials in almost every lane pair (the X stage without
+    shared differences), layers (x < X/2 vs x >= X/2, the TestEngine two-layer
+    layout) keep waves uniform.  3 steps == the oracle's stages, bitwise."""
+    mats = ((4.0, 2.0, 1.0), (1.0, 2.0, 0.8), (2.5, 0.0, 3.0))
+    b = oracle_body(3, bs, sizes, materials=mats, courant=0.9)
+    if layout == "random":
+        random_materials(b, seed=5)
+    else:
+        its = b.inner_indices()
+        b.mat_id[b.flat_index(its)] = np.where(its[:, 0] < sizes[0] // 2, 0, 1).astype(np.uint8)
+    random_state(b, seed=6, ghosts=False)
+    ctx = context_for(b)
+    assert ctx.effective_path == "fused"
+    tau = 0.9 / np.sqrt((3.0 + 6.0) / 2.5)  # Courant 0.9 on the fastest material: floor(q) = 0
+    ctx.profile(True)
+    for step in range(3):
+        for s in range(3):
+            b.stage(s, tau)
+        ctx.step(tau)
+        assert ctx.last_path == "fused"
+        assert_same(ctx, b, f"HET {layout} step {step}")
+    k = ctx.profile_read()
+    assert "HET" in k["fused_xyz"]["kernel"], k
+    ctx.close()
