@@ -996,8 +996,14 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 		HIP_TRY(hipEventRecord(c->ev_bnd, c->stream));
 		HIP_TRY(hipStreamWaitEvent(c->bnd_stream, c->ev_bnd, 0));
 		join.bnd = true;
-		ok = ok && xyz("fused_xyz_boundary", 0, bs, c->stream, 16) &&
-		     xyz("fused_xyz_boundary", X - bs, X, c->bnd_stream, 16);
+		// boundary rows per block: 16 (GCMX_BOUNDARY_ROWS overrides it, tuning only)
+		static const int brows = [] {
+			const char* e = std::getenv("GCMX_BOUNDARY_ROWS");
+			const int v = e ? std::atoi(e) : 0;
+			return v > 0 ? v : 16;
+		}();
+		ok = ok && xyz("fused_xyz_boundary", 0, bs, c->stream, brows) &&
+		     xyz("fused_xyz_boundary", X - bs, X, c->bnd_stream, brows);
 		HIP_TRY(hipEventRecord(c->ev_bnd, c->bnd_stream));
 		HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
 		join.bnd = false;
