@@ -415,7 +415,8 @@ def main():
             "config": {"workload": f"3-D isotropic elastic CubicGrid {N}^3, borderSize 2, "
                                    f"Courant 0.9, tau 0.9, one full time step (3 stages)",
                        "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,
-                       "parallelism": f"x-slab{world}" if world > 1 else "single"},
+                       "parallelism": f"x-slab{world}" if world > 1 else "single",
+                       **({"rows_per_block": a.rows_per_block} if a.rows_per_block else {})},
             # NOT an HBM rate: the bytes three separate stage passes (SURVEY §8d, 432 B per
             # node-step) would move, over the measured step time; the one-pass step moves 144 B
             "equivalent_GBps_if_three_stage_passes": round(step_bytes * a.steps / el / 1e9, 1),

@@ -964,16 +964,44 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 	const int X = g.sizes[0], bs = c->bs;
 	const double plane_bytes = node_stage_bytes(c) * (double)g.sizes[1] * g.sizes[2];
 	const bool halo = has_halo(c);
-	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows) {
-		Timed t(c, name, plane_bytes * (x1 - x0), st);
+	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows, int xb0 = 0, int xb1 = 0) {
+		Timed t(c, name, plane_bytes * ((x1 - x0) + (xb1 - xb0)), st);
 		const HetMaterials het{c->het_d, c->mat_d};
 		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb, &t.kname,
-		                        c->iso_het ? &het : nullptr);
+		                        c->iso_het ? &het : nullptr, xb0, xb1);
 	};
 	const gcmx_schedule sched =
-	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_XSLAB : GCMX_SCHED_SINGLE) : c->sched;
+	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_BFIRST : GCMX_SCHED_SINGLE) : c->sched;
 	bool ok = true;
-	if (sched == GCMX_SCHED_XSLAB && X >= 4 * bs) {
+	// boundary rows per block: 16 beside the interior (XSLAB), 4 alone on the
+	// GPU (BFIRST: 2 x 128 blocks for a 512^2 face); GCMX_BOUNDARY_ROWS
+	// overrides both (tuning only)
+	static const int brows_env = [] {
+		const char* e = std::getenv("GCMX_BOUNDARY_ROWS");
+		return e ? std::atoi(e) : 0;
+	}();
+	if (sched == GCMX_SCHED_BFIRST && X >= 4 * bs) {
+		// Boundary-first schedule, one stream: the 2 x bs boundary planes (both
+		// sides in ONE launch of thin blocks) wait for the halo and run alone on
+		// the GPU, the exchange of their NEW planes is posted at once, and the
+		// interior planes [bs, X-bs) follow, covering the exchange.  Interior
+		// blocks are never resident when the boundary blocks are dispatched, and
+		// no cross-stream wait sits on the compute path, so nothing delays the
+		// critical path boundary -> exchange -> next step's boundary.
+		if (halo) {
+			s = halo_ensure(c);
+			if (s) return s;
+		}
+		const int brows = brows_env > 0 ? brows_env : 4;
+		ok = xyz("fused_xyz_boundary", 0, bs, c->stream, brows, X - bs, X);
+		if (ok && halo) {
+			std::swap(c->cur, c->nxt);  // E_{n+1}: exchange the new boundary planes
+			s = halo_post(c);
+			std::swap(c->cur, c->nxt);
+			if (s) return s;
+		}
+		ok = ok && xyz("fused_xyz", bs, X - bs, c->stream, c->rows_per_block);
+	} else if (sched == GCMX_SCHED_XSLAB && X >= 4 * bs) {
 		// X-slab schedule.  The interior planes [bs, X-bs) read no ghost plane:
 		// they start at once on the low-priority inner stream, ordered only
 		// after the previous step (ev_fork), not after the halo.  The boundary
@@ -996,12 +1024,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 		HIP_TRY(hipEventRecord(c->ev_bnd, c->stream));
 		HIP_TRY(hipStreamWaitEvent(c->bnd_stream, c->ev_bnd, 0));
 		join.bnd = true;
-		// boundary rows per block: 16 (GCMX_BOUNDARY_ROWS overrides it, tuning only)
-		static const int brows = [] {
-			const char* e = std::getenv("GCMX_BOUNDARY_ROWS");
-			const int v = e ? std::atoi(e) : 0;
-			return v > 0 ? v : 16;
-		}();
+		const int brows = brows_env > 0 ? brows_env : 16;
 		ok = ok && xyz("fused_xyz_boundary", 0, bs, c->stream, brows) &&
 		     xyz("fused_xyz_boundary", X - bs, X, c->bnd_stream, brows);
 		HIP_TRY(hipEventRecord(c->ev_bnd, c->bnd_stream));
@@ -1192,7 +1215,7 @@ extern "C" {
 
 gcmx_status gcmx_set_step_schedule(gcmx_ctx* c, gcmx_schedule sched, int rows_per_block) {
 	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");
-	if (sched < GCMX_SCHED_AUTO || sched > GCMX_SCHED_XSLAB)
+	if (sched < GCMX_SCHED_AUTO || sched > GCMX_SCHED_BFIRST)
 		return fail(GCMX_ERR_INVALID_ARG, "bad schedule");
 	if (rows_per_block < 0 || rows_per_block > 4096)
 		return fail(GCMX_ERR_INVALID_ARG, "rows_per_block must be 0 (automatic) .. 4096");

@@ -348,8 +348,8 @@ __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET>
 __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
     const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY_,
-    IsoAxis AZ_, int x0, int chunk, int nplanes, FaceBC fb, const IsoAxis* __restrict__ mtab,
-    const uint8_t* __restrict__ mat) {
+    IsoAxis AZ_, int x0, int chunk, int nplanes, int xb0, int nplanesb, FaceBC fb,
+    const IsoAxis* __restrict__ mtab, const uint8_t* __restrict__ mat) {
 	static_assert(!HET || (KF0 && UNI), "heterogeneous step: floor(q) = 0, Z == ZT, equal axes");
 	const IsoAxis& AY = UNI ? AX : AY_;
 	const IsoAxis& AZ = UNI ? AX : AZ_;
@@ -383,14 +383,18 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 
 	const int z = threadIdx.x;
 	const int Y = g.sizes[1], Z = g.sizes[2];
-	int x, yb;
-	{  // XCD-aware chunk-major block order (see k_fused_xyz) over plane pairs
-		const int npair = (nplanes + 1) / 2, T = (int)gridDim.x, b = (int)blockIdx.x;
+	int x, yb, xend;
+	{  // XCD-aware chunk-major block order (see k_fused_xyz) over the plane pairs of
+	   // range A [x0, x0 + nplanes), then range B [xb0, xb0 + nplanesb) (may be empty)
+		const int npa = (nplanes + 1) / 2, npair = npa + (nplanesb + 1) / 2;
+		const int T = (int)gridDim.x, b = (int)blockIdx.x;
 		const int p = (T % 8 == 0) ? (b % 8) * (T / 8) + b / 8 : b;
-		x = x0 + 2 * (p % npair);
+		const int q = p % npair;
+		x = q < npa ? x0 + 2 * q : xb0 + 2 * (q - npa);
+		xend = q < npa ? x0 + nplanes : xb0 + nplanesb;
 		yb = (p / npair) * chunk;
 	}
-	const bool two = x + 1 < x0 + nplanes;
+	const bool two = x + 1 < xend;
 	const int ye = min(yb + chunk, Y);
 	const bool live = UNI || z < Z;
 	const int zc = live ? z : Z - 1;
@@ -903,6 +907,33 @@ static const char* xyz_name() {
 	return s.c_str();
 }
 
+// Rows per block of k_step_tx2 (req > 0 forces a value): the longest chunk of
+// the form Y, 512, 256, ..., 16 whose launch still fills >= 90 % of the resident
+// block slots (`slots` = CUs x blocks per CU), so one round of blocks covers the
+// launch with the fewest 2*BS-row prologues (measured, DESIGN.md §3.1 / §5:
+// 512^3 512 rows 4.32 vs 256 rows 4.37 ms; a 60-plane slab interior 64 rows
+// 0.54 vs 32 rows 0.56 vs 16 rows 0.60 ms; 256^3 64 rows 0.590 vs 32 / 128 rows
+// 0.599 / 0.692 ms).
+static int tx2_chunk_for(int Y, int npair, int req, int slots) {
+	if (req > 0) return Y <= req ? Y : req;
+	for (int t = 1024; t >= 16; t /= 2) {
+		const int ch = Y < t ? Y : t;
+		if (10LL * npair * ((Y + ch - 1) / ch) >= 9LL * slots) return ch;
+	}
+	return Y < 16 ? Y : 16;
+}
+
+static int device_cus() {
+	static int n = [] {
+		int dev = 0, v = 0;
+		if (hipGetDevice(&dev) != hipSuccess ||
+		    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+			v = 256;
+		return v;
+	}();
+	return n;
+}
+
 // Rows per block (k_fused_xyz): GCMX_XYZ_CHUNK (128) while the launch still has >= 1024 blocks
 // (two rounds of the 512 resident blocks, 2 per CU); thinner slabs (multi-GPU
 // X slabs, the boundary planes) halve it, down to 16 rows, to keep every CU
@@ -917,25 +948,25 @@ static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK
 
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                         int x1, hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname,
-                         const HetMaterials* het) {
+                         int x1, int xb0, int xb1, hipStream_t st, int req_chunk, const FaceBC* fb,
+                         const char** kname, const HetMaterials* het) {
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
 	const bool uni = kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
 	if constexpr (BS <= 2 && ZT <= 512) {
 		if (GCMX_XYZ_TX2 || fb) {
-			const int npair = (x1 - x0 + 1) / 2;
-			// one block per CU: the longest blocks (<= 256 rows) that still give two
-			// rounds of the 256 resident blocks (512^3: 256 rows, 256^3: 64)
-			const int chunk = xyz_chunk_for(g.sizes[1], npair, req_chunk, 256, 512);
+			const int nb = xb1 > xb0 ? xb1 - xb0 : 0;
+			const int npair = (x1 - x0 + 1) / 2 + (nb + 1) / 2;
+			// resident blocks: 2 waves per SIMD (<= 256 VGPRs), i.e. 512 / ZT per CU
+			const int chunk = tx2_chunk_for(g.sizes[1], npair, req_chunk, device_cus() * (512 / ZT));
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair);
 			const FaceBC none{};
 			const FaceBC& f = fb ? *fb : none;
 			const IsoAxis* mt = het ? het->tab : nullptr;
 			const uint8_t* mi = het ? het->ids : nullptr;
 			auto go = [&](auto K, const char* name) {
-				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, f,
-				                   mt, mi);
+				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, xb0,
+				                   nb, f, mt, mi);
 				*kname = name;
 			};
 			if (het) {  // the caller checked Z == ZT, KF0 and equal axes per material
@@ -954,6 +985,11 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 			}
 			return;
 		}
+	}
+	if (xb1 > xb0) {  // k_fused_xyz has no second range: two launches
+		launch_xyz_t<BS, ZT>(in, out, g, a, x0, x1, 0, 0, st, req_chunk, fb, kname, het);
+		x0 = xb0;
+		x1 = xb1;
 	}
 	const int chunk = xyz_chunk_for(g.sizes[1], x1 - x0, req_chunk);
 	const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * (x1 - x0));
@@ -974,14 +1010,14 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 
 template <int BS>
 static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
-                          int x1, hipStream_t st, int ch, const FaceBC* fb, const char** kn,
-                          const HetMaterials* het) {
+                          int x1, int xb0, int xb1, hipStream_t st, int ch, const FaceBC* fb,
+                          const char** kn, const HetMaterials* het) {
 	const int Z = g.sizes[2];
-	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
-	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
-	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
-	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
-	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, st, ch, fb, kn, het);
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
 	return true;
 }
 
@@ -1005,17 +1041,18 @@ bool fused_faces_supported(const Geo& g) {
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk, const FaceBC* faces, const char** kname,
-                      const HetMaterials* het) {
+                      const HetMaterials* het, int xb0, int xb1) {
 	const char* dummy = nullptr;
 	const char** kn = kname ? kname : &dummy;
 	if (!fused_supported(g) || x1 <= x0) return false;
+	if (xb1 > xb0 && (xb0 < x1 || xb1 > g.sizes[0])) return false;  // range B after range A
 	if (het && !het_supported(g)) return false;
 	if (faces && faces->on && !fused_faces_supported(g)) return false;
 	if (faces && faces->ode_on && !(g.bs <= 2 && g.sizes[2] <= 512)) return false;  // k_fused_xyz has no epilogue
 	switch (g.bs) {
-	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, st, chunk, faces, kn, het);
-	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, st, chunk, faces, kn, het);
-	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, st, chunk, faces, kn, het);
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
 	default: return false;
 	}
 }

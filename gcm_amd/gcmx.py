@@ -25,7 +25,7 @@ STATUS_NAMES = {0: "GCMX_OK", 1: "GCMX_ERR_INVALID_ARG", 2: "GCMX_ERR_CFL", 3: "
                 7: "GCMX_ERR_COMM"}
 PATH_AUTO, PATH_GENERIC, PATH_SPLIT, PATH_FUSED = 0, 1, 2, 3
 PATH_NAMES = {0: "auto", 1: "generic", 2: "split", 3: "fused"}
-SCHED_AUTO, SCHED_SINGLE, SCHED_XSLAB = 0, 1, 2
+SCHED_AUTO, SCHED_SINGLE, SCHED_XSLAB, SCHED_BFIRST = 0, 1, 2, 3
 UNIQUE_ID_BYTES = 128
 MAX_BORDER_Q = 16
 QUANTITY_CODES = {"Vx": 2, "Vy": 3, "Vz": 4, "Sxx": 5, "Sxy": 6, "Sxz": 7, "Syy": 8, "Syz": 9,
@@ -252,7 +252,7 @@ class Context:
         _check(lib().gcmx_set_kernel_path(self._ptr, path))
 
     def set_schedule(self, sched: int, rows_per_block: int = 0):
-        """gcmx_set_step_schedule: SCHED_AUTO / SCHED_SINGLE / SCHED_XSLAB."""
+        """gcmx_set_step_schedule: SCHED_AUTO / SCHED_SINGLE / SCHED_XSLAB / SCHED_BFIRST."""
         _check(lib().gcmx_set_step_schedule(self._ptr, sched, rows_per_block))
 
     @property

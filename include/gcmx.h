@@ -63,11 +63,15 @@ typedef enum gcmx_path {
 
 /* How gcmx_step issues the fused pass (gcmx_set_step_schedule). */
 typedef enum gcmx_schedule {
-	GCMX_SCHED_AUTO = 0,   /* X-slab schedule when a halo exchange is configured   */
+	GCMX_SCHED_AUTO = 0,   /* boundary-first schedule when a halo exchange is
+	                          configured, else one launch                        */
 	GCMX_SCHED_SINGLE = 1, /* halo (if any) first, then one launch over all planes */
-	GCMX_SCHED_XSLAB = 2   /* interior planes on a low-priority stream beside the
+	GCMX_SCHED_XSLAB = 2,  /* interior planes on a low-priority stream beside the
 	                          boundary planes, the next halo posted before the
 	                          interior joins; needs X >= 4*bs     */
+	GCMX_SCHED_BFIRST = 3  /* boundary planes first (thin blocks, alone on the
+	                          GPU), the next halo posted, then the interior on
+	                          the same stream; needs X >= 4*bs    */
 } gcmx_schedule;
 
 /* ---- library ------------------------------------------------------------ */

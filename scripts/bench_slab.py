@@ -25,16 +25,17 @@ from gcm_amd import gcmx  # noqa: E402
 from gcm_amd.host import isotropic_elastic_matrices  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--sched", default="xslab", choices=["single", "xslab"])
+ap.add_argument("--sched", default="xslab", choices=["single", "xslab", "bfirst"])
 ap.add_argument("--rows", type=int, default=0)
 ap.add_argument("--ranks", default="1,2,4,8")
 ap.add_argument("--n", type=int, default=512)
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--no-check", action="store_true")
+ap.add_argument("--reps", type=int, default=5, help="timed repetitions of --steps steps (median)")
 args = ap.parse_args()
 U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
 N, STEPS = args.n, args.steps
-SCHED = gcmx.SCHED_XSLAB if args.sched == "xslab" else gcmx.SCHED_SINGLE
+SCHED = {"xslab": gcmx.SCHED_XSLAB, "bfirst": gcmx.SCHED_BFIRST}.get(args.sched, gcmx.SCHED_SINGLE)
 
 
 def make(X, path=gcmx.PATH_AUTO, x0=0):
@@ -56,7 +57,8 @@ if not args.no_check:
         c.close()
     bad = int(np.sum(outs["fused"] != outs["generic"]))
     print(json.dumps({"check": "slab 64x512x512 fused vs generic, 2 steps", "mismatches": bad,
-                      "sched": args.sched, "rows": args.rows}), flush=True)
+                      "sched": args.sched, "rows": args.rows,
+                      "boundary_rows": os.environ.get("GCMX_BOUNDARY_ROWS", "default")}), flush=True)
     if bad:
         sys.exit(1)
 
@@ -66,11 +68,14 @@ for ranks in [int(r) for r in args.ranks.split(",")]:
     for _ in range(3):
         c.step(0.9)
     c.sync()
-    t0 = time.perf_counter()
-    for _ in range(STEPS):
-        c.step(0.9)
-    c.sync()
-    el = time.perf_counter() - t0
+    reps = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        for _ in range(STEPS):
+            c.step(0.9)
+        c.sync()
+        reps.append(time.perf_counter() - t0)
+    el = sorted(reps)[len(reps) // 2]
     c.profile(True)
     c.profile_reset()
     for _ in range(STEPS):
@@ -81,9 +86,13 @@ for ranks in [int(r) for r in args.ranks.split(",")]:
     c.close()
     ms = el / STEPS * 1e3
     rate = X * N * N * STEPS / el / 1e6
+    kern = {n: round(v["total_ms"] / max(1, v["launches"]), 4) for n, v in k.items()}
+    ksum = sum(v["total_ms"] for v in k.values()) / STEPS
     print(json.dumps({"ranks": ranks, "slab": [X, N, N], "ms_per_step": round(ms, 4),
+                      "rep_ms_per_step": [round(r / STEPS * 1e3, 4) for r in reps],
+                      "kernel_ms_per_step": round(ksum, 4),
                       "Mnode_steps_per_gpu": round(rate, 1),
                       "projected_job_rate_no_comm": round(rate * ranks, 1),
-                      "kernels": {n: round(v["total_ms"] / max(1, v["launches"]), 4)
-                                  for n, v in k.items()},
-                      "sched": args.sched, "rows": args.rows}), flush=True)
+                      "kernels": kern,
+                      "sched": args.sched, "rows": args.rows,
+                      "boundary_rows": os.environ.get("GCMX_BOUNDARY_ROWS", "default")}), flush=True)

@@ -205,7 +205,7 @@ def test_adhesion_contact_two_contexts_bitwise(G):
     assert np.array_equal(ia, one.bodies[0].inner_view())
 
 
-@pytest.mark.parametrize("sched", ["single", "xslab"])
+@pytest.mark.parametrize("sched", ["single", "xslab", "bfirst"])
 def test_x_slabs_with_copy_halo_equal_single(G, sched):
     """Slab decomposition along X (the multi-GPU layout) on one device: two
     slabs whose X ghosts are refreshed from the neighbour before every step
@@ -221,7 +221,7 @@ def test_x_slabs_with_copy_halo_equal_single(G, sched):
     for r, (x0, X) in enumerate(((0, 17), (17, N - 17))):
         c = gcm_amd.Context(3, bs, [X, N, N], start=[x0, 0, 0])
         c.set_materials(U[None], U1[None], L[None]); c.fill_random([N, N, N], seed)
-        c.set_schedule(G.SCHED_XSLAB if sched == "xslab" else G.SCHED_SINGLE)
+        c.set_schedule({"xslab": G.SCHED_XSLAB, "bfirst": G.SCHED_BFIRST}.get(sched, G.SCHED_SINGLE))
         halves.append(c)
     a, b = halves
     from gcm_amd.gcmx import halo_exchange_group

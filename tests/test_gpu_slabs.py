@@ -94,14 +94,14 @@ def _run_threads(fns):
             raise e
 
 
-@pytest.mark.parametrize("sched", ["auto", "single", "xslab"])
+@pytest.mark.parametrize("sched", ["auto", "single", "xslab", "bfirst"])
 @pytest.mark.parametrize("xs", [[17, 23], [12, 9, 19]])
 def test_local_group_fused_equals_whole(G, sched, xs):
     """Ragged slabs on the fused path: the X-slab schedule (auto: a configured
     exchange selects it) with the in-step overlapped exchange, and the one-launch
     schedule with the exchange in front; 4 steps == one context, bitwise."""
     Y, Z, seed, steps = 40, 64, 0x5EED, 4
-    sc = {"auto": None, "single": G.SCHED_SINGLE, "xslab": G.SCHED_XSLAB}[sched]
+    sc = {"auto": None, "single": G.SCHED_SINGLE, "xslab": G.SCHED_XSLAB, "bfirst": G.SCHED_BFIRST}[sched]
     slabs = _group(G, xs, Y, Z, seed, sched=sc)
     whole = _whole(G, sum(xs), Y, Z, seed)
     G.local_group_steps(slabs, 0.9, steps)
@@ -200,12 +200,14 @@ def _oracle_steps(X, Y, Z, seed, steps):
 
 
 @pytest.mark.timeout(600)
-def test_local_group_two_64x512x512_slabs_match_oracle(G):
+@pytest.mark.parametrize("sched", ["xslab", "bfirst"])
+def test_local_group_two_64x512x512_slabs_match_oracle(G, sched):
     """Config 3's slab shape (512^3 over 8 GPUs = 64 x 512 x 512 per rank): two
-    such ranks in one group, 2 steps with the overlapped in-step exchange, ==
-    the oracle on the undivided 128 x 512 x 512 box, bitwise."""
+    such ranks in one group, 2 steps with the overlapped in-step exchange
+    (three-stream and boundary-first schedules), == the oracle on the undivided
+    128 x 512 x 512 box, bitwise."""
     X, Y, Z, seed, steps = 64, 512, 512, 0x5EED, 2
-    slabs = _group(G, [X, X], Y, Z, seed)
+    slabs = _group(G, [X, X], Y, Z, seed, sched={"xslab": G.SCHED_XSLAB, "bfirst": G.SCHED_BFIRST}[sched])
     G.local_group_steps(slabs, 0.9, steps)
     assert all(c.last_path == "fused" for c in slabs)
     got = _concat(slabs)
