@@ -139,6 +139,9 @@ struct gcmx_ctx {
 	double* halo_layer = nullptr;  // the layer the pending exchange fills
 	std::vector<int> halo_comps;
 	std::shared_ptr<LocalComm> lc;  // in-process slab group (gcmx_comm_init_local)
+	bool loop = false;              // loopback transport (gcmx_comm_init_loopback)
+	double loop_gbps = 0;           // emulated link rate per direction (0: no hold)
+	int loop_blocks = 0;            // blocks of the loopback copy kernel
 	int lrank = -1;
 	long long halo_gen = 0;        // posts made (in-process group)
 	// profiling
@@ -342,7 +345,7 @@ void compute_halo_comps(gcmx_ctx* c) {
 	}
 }
 
-bool has_halo(const gcmx_ctx* c) { return (c->comm || c->lc) && (c->left >= 0 || c->right >= 0); }
+bool has_halo(const gcmx_ctx* c) { return (c->comm || c->lc || c->loop) && (c->left >= 0 || c->right >= 0); }
 
 // The current layer changed: its ghost planes no longer hold the neighbours' planes.
 void touch_layer(gcmx_ctx* c) { c->halo_fresh = false; }
@@ -439,6 +442,78 @@ void local_abort(gcmx_ctx* c, const std::string& why) {
 	c->lc->cv.notify_all();
 }
 
+// Loopback transport (gcmx_comm_init_loopback): ONE slab exchanging with itself
+// periodically -- its right inner planes into its left ghost planes and its left
+// inner planes into its right ghost planes, the halo components only -- by a
+// few blocks on the comm stream (where RCCL's send/recv kernels run), each block
+// holding its CU slot until `min_ticks` of the 100 MHz real-time counter have
+// passed since it started: an xGMI transfer's duration and CU footprint on one
+// GPU, so one rank's step schedule can be timed with the exchange in flight.
+struct LoopPlan {
+	long long src[2 * kMaxM], dst[2 * kMaxM];  // element offsets of the planes, per (comp, side)
+	int n;                                     // (comp, side) pairs
+	long long half;                            // double2 elements per plane group (bs planes)
+};
+__global__ __launch_bounds__(256) void k_loop_halo(double* __restrict__ layer, LoopPlan p,
+                                                   unsigned long long min_ticks) {
+	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+	// per (comp, side): eight independent 16-byte loads in flight per lane, then
+	// their stores (32-bit indices: a group of bs planes is < 2^31 elements)
+	constexpr int U = 8;
+	const int stride = (int)(gridDim.x * blockDim.x), half = (int)p.half;
+	for (int k = 0; k < p.n; k++) {
+		const double2* __restrict__ src = reinterpret_cast<const double2*>(layer + p.src[k]);
+		double2* __restrict__ dst = reinterpret_cast<double2*>(layer + p.dst[k]);
+		for (int i0 = (int)(blockIdx.x * blockDim.x + threadIdx.x); i0 < half; i0 += U * stride) {
+			double2 v[U];
+#pragma unroll
+			for (int u = 0; u < U; u++)
+				if (i0 + u * stride < half) v[u] = src[i0 + u * stride];
+#pragma unroll
+			for (int u = 0; u < U; u++)
+				if (i0 + u * stride < half) dst[i0 + u * stride] = v[u];
+		}
+	}
+	if (threadIdx.x == 0) {
+		for (int it = 0; it < (1 << 24); it++) {  // bounded: ~4 s at most
+			if (__builtin_amdgcn_s_memrealtime() - t0 >= min_ticks) break;
+			__builtin_amdgcn_s_sleep(8);
+		}
+	}
+	__syncthreads();
+}
+
+gcmx_status loop_post(gcmx_ctx* c) {
+	const Geo& g = c->geo;
+	const int X = g.sizes[0], bs = c->bs;
+	LoopPlan p{};
+	const long long plane = (long long)bs * g.stride[0];
+	for (int comp : c->halo_comps) {
+		const long long base = (long long)comp * g.cs;
+		p.src[p.n] = base + (long long)(X - bs + bs) * g.stride[0];  // inner [X-bs, X)
+		p.dst[p.n++] = base;                                        // ghosts [-bs, 0)
+		p.src[p.n] = base + (long long)bs * g.stride[0];             // inner [0, bs)
+		p.dst[p.n++] = base + (long long)(X + bs) * g.stride[0];     // ghosts [X, X+bs)
+	}
+	p.half = plane / 2;
+	if (p.half >= (1LL << 31) - (1LL << 24)) return fail(GCMX_ERR_UNSUPPORTED, "loopback: planes too large");
+	const double bytes_dir = (double)c->halo_comps.size() * plane * sizeof(double);
+	const unsigned long long ticks =
+	    c->loop_gbps > 0 ? (unsigned long long)(bytes_dir / (c->loop_gbps * 1e9) * 1e8) : 0ull;
+	HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+	HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+	{
+		Timed t(c, "halo_loopback", 4.0 * bytes_dir, c->comm_stream);
+		hipLaunchKernelGGL(k_loop_halo, dim3(c->loop_blocks), dim3(256), 0, c->comm_stream, c->cur, p, ticks);
+		t.kname = "k_loop_halo";
+	}
+	HIP_TRY(hipGetLastError());
+	HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+	c->halo_pending = true;
+	c->halo_layer = c->cur;
+	return GCMX_OK;
+}
+
 // Post the X-ghost exchange of the current layer on the comm stream (ordered
 // after all work issued so far on the compute stream).  Completion is marked
 // by ev_halo (RCCL) or the group's events (in-process); consumers call halo_wait.
@@ -453,6 +528,7 @@ gcmx_status halo_post(gcmx_ctx* c) {
 		c->halo_layer = c->cur;
 		return GCMX_OK;
 	}
+	if (c->loop) return loop_post(c);
 	const Geo& g = c->geo;
 	const size_t n = (size_t)(c->bs * g.stride[0]);
 	const int X = g.sizes[0];
@@ -1431,6 +1507,27 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 	c->rank = rank;
 	c->left = left;
 	c->right = right;
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_comm_init_loopback(gcmx_ctx* c, double gbps_per_direction, int blocks) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (c->D < 2) return fail(GCMX_ERR_INVALID_ARG, "X-slab halo needs dim >= 2");
+	if (!(gbps_per_direction >= 0) || blocks < 1 || blocks > 1024)
+		return fail(GCMX_ERR_INVALID_ARG, "loopback: rate >= 0 GB/s and 1..1024 blocks expected");
+	if (c->comm || c->lc || c->loop) return fail(GCMX_ERR_STATE, "communicator already initialised");
+	if (c->geo.sizes[0] < c->bs) return fail(GCMX_ERR_INVALID_ARG, "loopback: slab thinner than borderSize");
+	if (c->geo.stride[0] % 2 != 0 || c->geo.cs % 2 != 0)
+		return fail(GCMX_ERR_UNSUPPORTED, "loopback: planes not 16-byte aligned");
+	if ((s = halo_wait(c)) != GCMX_OK) return s;
+	c->loop = true;
+	c->loop_gbps = gbps_per_direction;
+	c->loop_blocks = blocks;
+	c->nranks = 1;
+	c->rank = 0;
+	c->left = c->right = 0;  // itself, periodically
+	touch_layer(c);
 	return GCMX_OK;
 }
 

@@ -42,7 +42,7 @@ SYMBOLS = [
     "gcmx_copy_box",
     "gcmx_ode_maxwell", "gcmx_step_ode", "gcmx_last_ode_fused",
     "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
-    "gcmx_comm_init_local", "gcmx_local_group_steps",
+    "gcmx_comm_init_local", "gcmx_local_group_steps", "gcmx_comm_init_loopback",
     "gcmx_sync", "gcmx_stream",
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_profile_kernel",
     "gcmx_inner_nodes",
@@ -129,6 +129,7 @@ def lib() -> ctypes.CDLL:
     L.gcmx_halo_exchange.argtypes = [vp]
     L.gcmx_halo_exchange_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
     L.gcmx_comm_init_local.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.gcmx_comm_init_loopback.argtypes = [vp, ctypes.c_double, ctypes.c_int]
     L.gcmx_local_group_steps.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_double, ctypes.c_int]
     L.gcmx_sync.argtypes = [vp]
     L.gcmx_stream.argtypes = [vp]
@@ -323,6 +324,11 @@ class Context:
     def comm_init(self, unique_id: bytes, nranks: int, rank: int, left: int, right: int):
         buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)(*unique_id)
         _check(lib().gcmx_comm_init(self._ptr, buf, nranks, rank, left, right))
+
+    def comm_init_loopback(self, gbps_per_direction: float = 64.0, blocks: int = 8):
+        """gcmx_comm_init_loopback: x-periodic self-exchange through the RCCL
+        post / wait points, held for the bytes' time at the given link rate."""
+        _check(lib().gcmx_comm_init_loopback(self._ptr, gbps_per_direction, blocks))
 
     def halo_exchange(self):
         _check(lib().gcmx_halo_exchange(self._ptr))

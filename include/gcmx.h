@@ -240,6 +240,15 @@ gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n);
  * GCMX_LOCAL_WAIT_SECONDS); the
  * semantics are those of the (dead) MPI slab design, src/test/TestMPI.cpp:33-50. */
 gcmx_status gcmx_comm_init_local(gcmx_ctx* const* ctxs, int n);
+/* Loopback transport, for timing ONE rank's step on one GPU: the context's X
+ * slab exchanges with itself periodically (right inner planes -> left ghosts,
+ * left inner -> right ghosts, the components the X stage reads) through the same
+ * post / wait points as RCCL, by `blocks` 256-thread blocks of a copy kernel on
+ * the comm stream that hold their CU slots for the time the bytes of one
+ * direction take at `gbps_per_direction` (0: copy only) -- an xGMI transfer's
+ * duration and CU footprint.  The physics is x-periodic (tests compare it with
+ * gcmx_copy_box-filled periodic ghosts); bench only. */
+gcmx_status gcmx_comm_init_loopback(gcmx_ctx* ctx, double gbps_per_direction, int blocks);
 /* Drive an in-process group: one host thread per context, each calling
  * gcmx_step(ctxs[i], tau) `steps` times and then gcmx_sync.  The first failure
  * aborts the group and is returned (with its rank in gcmx_last_error). */
@@ -340,7 +349,11 @@ gcmx_status gsx_set_node_lanes(gsx_ctx* ctx, int lanes);
  * as ONE launch where the plan allows it (every inner foot that interpolates in
  * space-time with border nodes' new invariants waits, on the device, for exactly
  * those nodes): on = 1 (default) border + inner, 2 also the gradient groups in
- * the same launch, 0 separate launches.  Results are identical.
+ * the same launch, 0 separate launches, 3 (tuning only) mode 1 without the
+ * 4096-block cap on the fused grid.  Results are identical.  The one launch
+ * relies on workgroups being dispatched in id order (how the hardware behaves,
+ * not a HIP guarantee); every device-side wait is bounded and a timed-out wait
+ * is reported by gsx_sync / gsx_download / the engine's run_steps.
  * gsx_last_stage_fused reports whether the last gsx_stage ran as one launch. */
 gcmx_status gsx_set_stage_fusion(gsx_ctx* ctx, int on);
 gcmx_status gsx_last_stage_fused(const gsx_ctx* ctx, int* fused);

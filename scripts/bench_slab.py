@@ -2,15 +2,19 @@
 """Per-GPU time of one X slab of the 512^3 strong-scaling run, on ONE GPU.
 
 For each slab thickness X (512 / N for N = 1, 2, 4, 8) a [X, 512, 512] context
-runs the fused step; with --sched xslab it runs the multi-GPU step schedule
-(gcmx_set_step_schedule(GCMX_SCHED_XSLAB): interior planes on the low-priority
-stream, 16-row boundary blocks beside them) without a communicator, i.e.
-everything an N-rank run does per GPU except the RCCL transfers (which it
-overlaps).  --rows sets the interior's y rows per block (0: automatic).
-Also checks the slab step bitwise against the generic per-stage path on a
-[64, 512, 512] slab.  One JSON line per size on stdout.
+runs the fused step under a multi-GPU step schedule (gcmx_set_step_schedule):
+bfirst (default; what a rank runs: both boundary sides in one launch of thin
+blocks, then the interior on the same stream), xslab (interior on a
+low-priority stream beside 16-row boundary blocks) or single (one launch).
+With --loop-gbps R the slab also exchanges its halo -- with itself, through the
+loopback transport (gcmx_comm_init_loopback) at the RCCL post / wait points,
+each transfer holding a few CU slots for the time its bytes take at R GB/s per
+direction -- so the time is one rank's step with the exchange in flight;
+without it the transfers are not emulated.  --rows sets the interior's y rows
+per block (0: automatic).  Also checks the slab step bitwise against the
+generic per-stage path on a [64, 512, 512] slab.  One JSON line per size.
 
-    python scripts/bench_slab.py [--sched single|xslab] [--rows R] [--ranks 1,2,4,8]
+    python scripts/bench_slab.py [--sched bfirst|xslab|single] [--loop-gbps R] [--ranks 1,2,4,8]
 """
 import argparse
 import json
@@ -25,7 +29,12 @@ from gcm_amd import gcmx  # noqa: E402
 from gcm_amd.host import isotropic_elastic_matrices  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--sched", default="xslab", choices=["single", "xslab", "bfirst"])
+ap.add_argument("--sched", default="bfirst", choices=["single", "xslab", "bfirst"])
+ap.add_argument("--loop-gbps", type=float, default=-1.0,
+                help=">= 0: loopback transport (gcmx_comm_init_loopback): the slab exchanges "
+                     "with itself through the RCCL post/wait points, held for the bytes' time "
+                     "at this rate per direction (xGMI emulation); < 0: no exchange")
+ap.add_argument("--loop-blocks", type=int, default=8)
 ap.add_argument("--rows", type=int, default=0)
 ap.add_argument("--ranks", default="1,2,4,8")
 ap.add_argument("--n", type=int, default=512)
@@ -38,12 +47,14 @@ N, STEPS = args.n, args.steps
 SCHED = {"xslab": gcmx.SCHED_XSLAB, "bfirst": gcmx.SCHED_BFIRST}.get(args.sched, gcmx.SCHED_SINGLE)
 
 
-def make(X, path=gcmx.PATH_AUTO, x0=0):
+def make(X, path=gcmx.PATH_AUTO, x0=0, loop=False):
     c = gcm_amd.Context(3, 2, [X, N, N], start=[x0, 0, 0], device=0)
     c.set_materials(U[None], U1[None], L[None])
     c.set_path(path)
     c.set_schedule(SCHED, args.rows)
     c.fill_random([N, N, N], 0x5EED)
+    if loop and args.loop_gbps >= 0:
+        c.comm_init_loopback(args.loop_gbps, args.loop_blocks)
     return c
 
 
@@ -64,7 +75,7 @@ if not args.no_check:
 
 for ranks in [int(r) for r in args.ranks.split(",")]:
     X = N // ranks
-    c = make(X)
+    c = make(X, loop=True)
     for _ in range(3):
         c.step(0.9)
     c.sync()
@@ -92,7 +103,10 @@ for ranks in [int(r) for r in args.ranks.split(",")]:
                       "rep_ms_per_step": [round(r / STEPS * 1e3, 4) for r in reps],
                       "kernel_ms_per_step": round(ksum, 4),
                       "Mnode_steps_per_gpu": round(rate, 1),
-                      "projected_job_rate_no_comm": round(rate * ranks, 1),
+                      "projected_job_rate": round(rate * ranks, 1),
                       "kernels": kern,
                       "sched": args.sched, "rows": args.rows,
-                      "boundary_rows": os.environ.get("GCMX_BOUNDARY_ROWS", "default")}), flush=True)
+                      "boundary_rows": os.environ.get("GCMX_BOUNDARY_ROWS", "default"),
+                      "exchange": (f"loopback {args.loop_gbps} GB/s per direction, "
+                                   f"{args.loop_blocks} blocks" if args.loop_gbps >= 0 else
+                                   "none (transfers not emulated)")}), flush=True)

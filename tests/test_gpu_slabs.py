@@ -232,3 +232,28 @@ def test_local_group_eight_slabs_whole_512_match_oracle(G):
     want = _oracle_steps(N, N, N, seed, steps)
     for r in range(8):
         assert np.array_equal(got[r * X:(r + 1) * X], want[r * X:(r + 1) * X]), f"slab {r}"
+
+
+@pytest.mark.parametrize("sched", ["auto", "xslab", "single"])
+def test_loopback_exchange_is_periodic_halo(G, sched):
+    """The loopback transport (gcmx_comm_init_loopback: one slab exchanging with
+    itself through the RCCL post / wait points, held at an emulated link rate)
+    fills the x ghosts periodically: 3 fused steps == the per-stage path with
+    the same periodic ghosts written by gcmx_copy_box before each step,
+    bitwise."""
+    X, Y, Z, seed, steps = 18, 24, 64, 0x5EED, 3
+    a = _whole(G, X, Y, Z, seed)
+    if sched != "auto":
+        a.set_schedule({"xslab": G.SCHED_XSLAB, "single": G.SCHED_SINGLE}[sched])
+    a.comm_init_loopback(64.0, 4)
+    b = _whole(G, X, Y, Z, seed)
+    for _ in range(steps):
+        a.step(0.9)
+        b.copy_box([-2, 0, 0], [0, Y, Z], b, [X - 2, 0, 0])
+        b.copy_box([X, 0, 0], [X + 2, Y, Z], b, [0, 0, 0])
+        b.step(0.9)
+    a.sync()
+    assert a.last_path == "fused" and b.last_path == "split"
+    assert np.array_equal(_inner(a, a.download()), _inner(b, b.download()))
+    for c in (a, b):
+        c.close()
