@@ -1498,10 +1498,28 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 	if (c->comm || c->lc) return fail(GCMX_ERR_STATE, "communicator already initialised");
 	ncclUniqueId u;
 	std::memcpy(&u, id, sizeof(u));
-	ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+	// The exchange runs beside the interior kernel, which saturates HBM: a
+	// transfer with few blocks in flight is starved and stops hiding behind it
+	// (loopback measurement), so ask RCCL for at least
+	// GCMX_COMM_MIN_CTAS blocks (default 16; 0 leaves RCCL's own choice), at most
+	// GCMX_COMM_MAX_CTAS (default 32; RCCL rejects a minimum without a maximum).
+	static const int min_ctas = [] {
+		const char* e = std::getenv("GCMX_COMM_MIN_CTAS");
+		return e ? std::atoi(e) : 16;
+	}();
+	static const int max_ctas = [] {
+		const char* e = std::getenv("GCMX_COMM_MAX_CTAS");
+		return e ? std::atoi(e) : 32;
+	}();
+	ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+	if (min_ctas > 0) {
+		cfg.minCTAs = min_ctas;
+		cfg.maxCTAs = max_ctas > min_ctas ? max_ctas : min_ctas;
+	}
+	ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, u, rank, &cfg);
 	if (r != ncclSuccess) {
 		c->comm = nullptr;
-		return fail(GCMX_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+		return fail(GCMX_ERR_COMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
 	}
 	c->nranks = nranks;
 	c->rank = rank;

@@ -34,7 +34,7 @@ ap.add_argument("--loop-gbps", type=float, default=-1.0,
                 help=">= 0: loopback transport (gcmx_comm_init_loopback): the slab exchanges "
                      "with itself through the RCCL post/wait points, held for the bytes' time "
                      "at this rate per direction (xGMI emulation); < 0: no exchange")
-ap.add_argument("--loop-blocks", type=int, default=8)
+ap.add_argument("--loop-blocks", type=int, default=128)
 ap.add_argument("--rows", type=int, default=0)
 ap.add_argument("--ranks", default="1,2,4,8")
 ap.add_argument("--n", type=int, default=512)

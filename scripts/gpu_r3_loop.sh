@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r3/${TAG:-loop}
 mkdir -p $OUT
 set -o pipefail
-timeout -k 10 600 python -u -m pytest tests/test_gpu_slabs.py -m gpu -x -v -k "loopback or local_group_fused" \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_slabs.py -m gpu -x -v -k "loopback or local_group_fused or rccl" \
   --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || exit $rc

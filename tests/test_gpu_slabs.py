@@ -257,3 +257,21 @@ def test_loopback_exchange_is_periodic_halo(G, sched):
     assert np.array_equal(_inner(a, a.download()), _inner(b, b.download()))
     for c in (a, b):
         c.close()
+
+
+def test_rccl_single_rank_communicator(G):
+    """gcmx_comm_init on this box's RCCL (ncclCommInitRankConfig with the
+    minCTAs request): a one-rank communicator has no neighbours, so the step
+    runs without an exchange and equals a context without a communicator."""
+    import gcm_amd
+    X, Y, Z, seed = 16, 24, 64, 0x5EED
+    a = _whole(G, X, Y, Z, seed)
+    a.comm_init(gcm_amd.unique_id(), 1, 0, -1, -1)
+    b = _whole(G, X, Y, Z, seed)
+    for _ in range(2):
+        a.step(0.9)
+        b.step(0.9)
+    assert a.last_path == "fused"
+    assert np.array_equal(a.download(), b.download())
+    for c in (a, b):
+        c.close()
