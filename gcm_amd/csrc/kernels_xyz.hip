@@ -247,9 +247,6 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 #ifndef GCMX_TX2_BUF  // buffer loads/stores: block-uniform offsets in SGPRs (no VALU address math)
 #define GCMX_TX2_BUF 1
 #endif
-#ifndef GCMX_TX2_XFIRST  // X stage of the entering row between the Z-edge publish and the poll
-#define GCMX_TX2_XFIRST 0
-#endif
 #ifndef GCMX_TX2_PROBE_NOX
 #define GCMX_TX2_PROBE_NOX 0
 #endif
@@ -795,39 +792,6 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			}
 		}
 	};
-#if GCMX_TX2_XFIRST
-	// Row order: Y(y), publish the Z edges, X stage of the entering row (its two
-	// load pairs were issued one row ahead), issue the next row's pairs, then
-	// collect the neighbours' edges, Z stages and stores.  A whole X stage lies
-	// between a wave's publish and its poll, so the waves of a block rarely wait
-	// for each other; the pairs issued before the stores keep every vmcnt wait
-	// clear of the stores (loads and stores retire in order).
-	// GCMX_TX2_XFIRST == 2: only pair 0 is issued a row ahead (fewer live VGPRs
-	// across the Z stages); pair 1 is issued when the X stage starts.
-	XPre pre;
-	if constexpr (GCMX_TX2_XFIRST == 2) pair_load(P0{}, pre.a, clamp_row(yb + BS + 1));
-	else x_load_ahead(pre, clamp_row(yb + BS + 1));
-	auto row = [&](int y) {
-		double yv[2][9];
-		y_stage(y, yv);
-		TX2_T(0);
-		publish(y, yv);
-		TX2_T(1);
-		if constexpr (GCMX_TX2_XFIRST == 2) pair_load(P1{}, pre.b, clamp_row(y + BS + 1));
-		x_enter(y, pre);
-		TX2_T(5);
-		sched_fence();
-		if constexpr (GCMX_TX2_XFIRST == 2) pair_load(P0{}, pre.a, clamp_row(y + BS + 2));
-		else x_load_ahead(pre, clamp_row(y + BS + 2));
-		sched_fence();
-		TX2_T(6);
-		collect(y);
-		TX2_T(4);
-#pragma unroll
-		for (int t = 0; t < 2; t++) z_stage_store(t, y, yv);
-		TX2_T(3);
-	};
-#else
 	auto row = [&](int y) {
 		double yv[2][9];
 		XPre pre;
@@ -863,20 +827,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		x_enter(y, pre);
 		TX2_T(5);
 	};
-#endif
-#ifndef GCMX_TX2_ROWUNROLL  // unroll the row loop (fewer window-rotation moves)
-#define GCMX_TX2_ROWUNROLL 1
-#endif
-	if constexpr (GCMX_TX2_ROWUNROLL == 2) {
-		int y = yb;
-		for (; y + 1 < ye; y += 2) {
-			row(y);
-			row(y + 1);
-		}
-		if (y < ye) row(y);
-	} else {
-		for (int y = yb; y < ye; y++) row(y);
-	}
+	for (int y = yb; y < ye; y++) row(y);
 #if GCMX_TX2_DIAG
 	if ((threadIdx.x & 63) == 0) {
 		const int wv = threadIdx.x / 64;
