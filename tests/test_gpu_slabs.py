@@ -36,14 +36,14 @@ def _mats():
     return isotropic_elastic_matrices(3, 4, 2, 1)
 
 
-def _group(G, xs, Y, Z, seed, sched=None, path=None):
+def _group(G, xs, Y, Z, seed, sched=None, path=None, bs=2):
     """Contexts for X slabs of widths `xs` of an (sum(xs), Y, Z) grid, one group."""
     import gcm_amd
     U, U1, L = _mats()
     Xg = sum(xs)
     out, x0 = [], 0
     for X in xs:
-        c = gcm_amd.Context(3, 2, [X, Y, Z], start=[x0, 0, 0])
+        c = gcm_amd.Context(3, bs, [X, Y, Z], start=[x0, 0, 0])
         c.set_materials(U[None], U1[None], L[None])
         c.fill_random([Xg, Y, Z], seed)
         if sched is not None:
@@ -56,10 +56,10 @@ def _group(G, xs, Y, Z, seed, sched=None, path=None):
     return out
 
 
-def _whole(G, X, Y, Z, seed, path=None):
+def _whole(G, X, Y, Z, seed, path=None, bs=2):
     import gcm_amd
     U, U1, L = _mats()
-    c = gcm_amd.Context(3, 2, [X, Y, Z])
+    c = gcm_amd.Context(3, bs, [X, Y, Z])
     c.set_materials(U[None], U1[None], L[None])
     c.fill_random([X, Y, Z], seed)
     if path is not None:
@@ -71,8 +71,8 @@ def _inner(c, arr, bs=2):
     return arr.reshape(tuple(s + 2 * bs for s in c.sizes) + (9,))[bs:-bs, bs:-bs, bs:-bs]
 
 
-def _concat(slabs):
-    return np.concatenate([_inner(c, c.download()) for c in slabs], axis=0)
+def _concat(slabs, bs=2):
+    return np.concatenate([_inner(c, c.download(), bs) for c in slabs], axis=0)
 
 
 def _run_threads(fns):
@@ -274,4 +274,23 @@ def test_rccl_single_rank_communicator(G):
     assert a.last_path == "fused"
     assert np.array_equal(a.download(), b.download())
     for c in (a, b):
+        c.close()
+
+
+@pytest.mark.parametrize("sched", ["bfirst", "xslab"])
+@pytest.mark.parametrize("xs", [[4, 7, 5], [9, 6]])
+def test_local_group_border_size_one(G, sched, xs):
+    """borderSize 1: each boundary side is ONE plane, so the boundary-first
+    schedule's two-range launch covers two odd ranges (each pair's second plane
+    clamped and not stored); 3 steps == one context, bitwise."""
+    Y, Z, seed, steps, bs = 20, 64, 0x5EED, 3, 1
+    sc = {"xslab": G.SCHED_XSLAB, "bfirst": G.SCHED_BFIRST}[sched]
+    slabs = _group(G, xs, Y, Z, seed, sched=sc, bs=bs)
+    whole = _whole(G, sum(xs), Y, Z, seed, bs=bs)
+    G.local_group_steps(slabs, 0.9, steps)
+    for _ in range(steps):
+        whole.step(0.9)
+    assert all(c.last_path == "fused" for c in slabs)
+    assert np.array_equal(_concat(slabs, bs), _inner(whole, whole.download(), bs))
+    for c in slabs + [whole]:
         c.close()
