@@ -182,6 +182,18 @@ struct gsx_contact {
 
 namespace {
 
+// Global thread index with the blocks of each XCD made contiguous: workgroups
+// are dealt round-robin over the 8 XCDs (b % 8, MI355X_MICROARCH.md §Workgroup
+// dispatch), so XCD k gets blocks k, k+8, ...; renumbering them k*q + min(k, r)
+// + b/8 hands XCD k one contiguous range of nodes, whose neighbours / cell
+// vertices (spatially close in the vertex order) its own L2 then holds.  For
+// kernels whose blocks are independent only (not k_sx_stage_l8, whose waits
+// rely on block id order).
+__device__ __forceinline__ int xcd_gid() {
+	const int T = (int)gridDim.x, b = (int)blockIdx.x, q = T >> 3, r = T & 7, k = b & 7;
+	return (k * q + (k < r ? k : r) + (b >> 3)) * (int)blockDim.x + (int)threadIdx.x;
+}
+
 // out[c] = M(c,0) in[0] + sum_{j>=1} M(c,j) in[j]  (linal/operators.hpp:109-123).
 // AOS_OUT: the invariants of beforeStage are written node-major ([n][9]) because
 // the gradient and node kernels gather them per neighbour / per cell vertex.
@@ -189,7 +201,7 @@ template <bool AOS_OUT>
 __global__ __launch_bounds__(256) void k_sx_transform(const double* __restrict__ in,
                                                       double* __restrict__ out,
                                                       const double* __restrict__ Mx, int N) {
-	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	const int n = xcd_gid();
 	if (n >= N) return;
 	double v[kM];
 #pragma unroll
@@ -228,7 +240,7 @@ __global__ __launch_bounds__(256) void k_sx_gradient(const double* __restrict__ 
                                                      const double* __restrict__ wts,
                                                      const double* __restrict__ Mm,
                                                      const double* __restrict__ dets, int N) {
-	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	const int n = xcd_gid();
 	if (n >= N) return;
 	const int b0 = off[n], K = off[n + 1] - b0;
 	double wc[kG], r0[kG], r1[kG], r2[kG];
@@ -579,7 +591,7 @@ __global__ __launch_bounds__(64) void k_sx_border(
 	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
 	__shared__ SharedMats<3> sm;
 	stage_mats<3>(sm, {U, U1, Unext});
-	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	const int t = xcd_gid();
 	if (t >= count) return;
 	const int n = nodes[t];
 	double out[kM];
@@ -602,7 +614,7 @@ __global__ __launch_bounds__(256) void k_sx_inner(
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
     const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int N, int pos0, int P) {
-	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	const int t = xcd_gid();
 	if (t >= count) return;
 	const int n = nodes[t];
 	double out[kM];
@@ -723,7 +735,7 @@ __global__ __launch_bounds__(256) void k_sx_gradient_l8(const double* __restrict
                                                         const double* __restrict__ wts,
                                                         const double* __restrict__ Mm,
                                                         const double* __restrict__ dets, int N) {
-	gradient_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, w, grad, off, nbs, coords, wts, Mm, dets, N, nullptr);
+	gradient_l8<false>(xcd_gid(), w, grad, off, nbs, coords, wts, Mm, dets, N, nullptr);
 }
 
 // A border node's new invariants (wn) are complete once its flag holds this
@@ -1016,7 +1028,7 @@ __global__ __launch_bounds__(256) void k_sx_inner_l8(
     const double* __restrict__ coords, const double* __restrict__ w, const double* __restrict__ grad,
     const double* __restrict__ wn, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int N, int pos0, int P) {
-	inner_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
+	inner_l8<false>(xcd_gid(), nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
 	                U1, Unext, un, wnext, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr, 0});
 }
 
@@ -1240,7 +1252,7 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
     double* __restrict__ wn, const char* __restrict__ deferred, BorderDevArgs bp, const BorderArgs* __restrict__ argp,
     const double* __restrict__ U, const double* __restrict__ U1, const double* __restrict__ Unext,
     double* __restrict__ un, double* __restrict__ wnext, int stage, int N, int pos0, int P) {
-	border_l8<false>(blockIdx.x * blockDim.x + threadIdx.x, nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
+	border_l8<false>(xcd_gid(), nodes, count, fv, flam, fmeta, sh, coords, w, grad, wn,
 	                 deferred, bp, argp, U, U1, Unext, un, wnext, stage, N, pos0, P, StageWait{nullptr, nullptr, 0u, 0, nullptr, 0});
 }
 
@@ -1313,7 +1325,7 @@ __global__ __launch_bounds__(256) void k_sx_begin(double* u_, double* __restrict
                                                   const int2* __restrict__ nodeRec,
                                                   const double* __restrict__ Sm, int N, const BorderArgs* __restrict__ argp) {
 	const BorderArgs& args = *argp;  // static per plan: device memory, not kernel arguments
-	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	const int n = xcd_gid();
 	if (n >= N) return;
 	double u[kM];
 #pragma unroll
