@@ -265,7 +265,13 @@ def emulate_slabs(a):
         "per_rank_ms_per_step": round(ms / K, 4),
         "whole_grid_ms_per_step": round(msw, 4),
         "decomposition_overhead": round(ms / msw, 4),
-        "projected_speedup_if_exchange_hidden": round(K * msw / ms, 3),
+        # K ranks contending for ONE GPU (their boundary launches, interiors and
+        # copies interleaved on one chip): a pessimistic stand-in for K GPUs.  One
+        # rank's own step with the exchange in flight is scripts/bench_slab.py
+        # --loop-gbps (loopback transport), DESIGN.md §5.
+        "speedup_if_ranks_ran_this_fast_on_K_gpus": round(K * msw / ms, 3),
+        "note": "all K ranks share one GPU; per-rank step with the exchange in flight: "
+                "scripts/bench_slab.py --loop-gbps (DESIGN.md §5)",
         "kernels": {k: {"avg_ms": round(v["total_ms"] / max(1, v["launches"]), 4),
                         "launches_per_step": round(v["launches"] / (a.steps * max(1, a.reps)), 2),
                         "kernel": v["kernel"]} for k, v in kern.items()},

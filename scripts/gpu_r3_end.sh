@@ -24,6 +24,10 @@ for K in ${SLABS:-8 4 2}; do
     || { echo "emulate $K rc=$?"; tail $OUT/emulate_$K.err; exit 1; }
 done
 timeout -k 10 200 python scripts/bench_slab.py --ranks 8,4,2 --steps 30 > $OUT/slab.jsonl 2> $OUT/slab.err || { tail $OUT/slab.err; exit 1; }
+timeout -k 10 200 python scripts/bench_slab.py --ranks 8,4,2 --steps 30 --loop-gbps 64 --no-check > $OUT/slab_loop64.jsonl 2>> $OUT/slab.err || { tail $OUT/slab.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sx64 -o run -- \
+  python3 scripts/bench_simplex.py --workloads cube --n 64 --lanes 1 --steps 20 > $OUT/simplex64.jsonl 2> $OUT/simplex64.err \
+  || { echo "simplex64 rc=$?"; tail $OUT/simplex64.err; exit 1; }
 timeout -k 10 300 python scripts/bench_simplex.py --workloads cubetask,cube,fracture --n 16 --steps 200 \
   > $OUT/simplex16.jsonl 2> $OUT/simplex.err || { tail $OUT/simplex.err; exit 1; }
 if [ "${PROF:-1}" = 1 ]; then
@@ -40,10 +44,12 @@ for f in ("bench_512.json", "bench_256.json"):
           r.get("copy_ceiling", {}).get("GBps"), (d.get("cpu_baseline") or {}).get("value"))
 for f in sorted(glob.glob(f"{o}/emulate_*.json")):
     d = json.load(open(f))
-    print(f.split("/")[-1], d["ms_per_step"], d.get("per_rank_ms_per_step"), d.get("projected_speedup_if_exchange_hidden"))
-for l in open(f"{o}/slab.jsonl"):
-    d = json.loads(l)
-    print("slab", d["ranks"], d["ms_per_step"], d["kernels"])
+    print(f.split("/")[-1], d["ms_per_step"], d.get("per_rank_ms_per_step"), d.get("speedup_if_ranks_ran_this_fast_on_K_gpus"))
+for f in ("slab.jsonl", "slab_loop64.jsonl"):
+    for l in open(f"{o}/{f}"):
+        d = json.loads(l)
+        if "ranks" in d:
+            print(f, d["ranks"], d["ms_per_step"], d["kernels"])
 for l in open(f"{o}/simplex16.jsonl"):
     d = json.loads(l)
     print("simplex", {k: d[k] for k in d if k in ("workload", "ms_per_step", "value", "vertices")})
