@@ -1492,8 +1492,10 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
                            int rank, int left, int right) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
+	// A neighbour equal to this rank is accepted only in a one-rank communicator
+	// (the self-exchange that runs the RCCL transport on a one-GPU box, gcmx.h).
 	if (!id || nranks < 1 || rank < 0 || rank >= nranks || left >= nranks || right >= nranks ||
-	    left == rank || right == rank)
+	    (nranks > 1 && (left == rank || right == rank)))
 		return fail(GCMX_ERR_INVALID_ARG, "bad communicator arguments");
 	if (c->comm || c->lc) return fail(GCMX_ERR_STATE, "communicator already initialised");
 	ncclUniqueId u;

@@ -213,7 +213,12 @@ int         gcmx_last_ode_fused(gcmx_ctx* ctx);
 #define GCMX_UNIQUE_ID_BYTES 128
 gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]);
 /* left/right: ranks owning the slabs at lower/higher X, or -1 at a physical
- * boundary.  Collective over `nranks` processes (one context per process). */
+ * boundary.  Collective over `nranks` processes (one context per process).
+ * In a ONE-rank communicator left/right may be 0 (the rank itself): the same
+ * ncclSend/ncclRecv group then runs against itself, and RCCL matches a rank's
+ * sends to itself with its receives in posting order, so the left ghost planes
+ * receive the slab's first bs inner planes and the right ghost planes its last
+ * bs (the RCCL transport exercised on a one-GPU box; not periodic). */
 gcmx_status gcmx_comm_init(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES],
                            int nranks, int rank, int left, int right);
 /* Fill the X ghost layers of the current layer from the neighbours' boundary

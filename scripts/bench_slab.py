@@ -10,7 +10,10 @@ With --loop-gbps R the slab also exchanges its halo -- with itself, through the
 loopback transport (gcmx_comm_init_loopback) at the RCCL post / wait points,
 each transfer holding a few CU slots for the time its bytes take at R GB/s per
 direction -- so the time is one rank's step with the exchange in flight;
-without it the transfers are not emulated.  --rows sets the interior's y rows
+without it the transfers are not emulated.  With --rccl-self the slab is a
+one-rank RCCL communicator whose neighbours are itself (gcmx_comm_init, left =
+right = 0): the real ncclSend/ncclRecv group runs at every post point, its
+bytes moved by RCCL's own kernels on the same GPU.  --rows sets the interior's y rows
 per block (0: automatic).  Also checks the slab step bitwise against the
 generic per-stage path on a [64, 512, 512] slab.  One JSON line per size.
 
@@ -35,6 +38,8 @@ ap.add_argument("--loop-gbps", type=float, default=-1.0,
                      "with itself through the RCCL post/wait points, held for the bytes' time "
                      "at this rate per direction (xGMI emulation); < 0: no exchange")
 ap.add_argument("--loop-blocks", type=int, default=128)
+ap.add_argument("--rccl-self", action="store_true",
+                help="one-rank RCCL communicator exchanging with itself (real ncclSend/Recv)")
 ap.add_argument("--rows", type=int, default=0)
 ap.add_argument("--ranks", default="1,2,4,8")
 ap.add_argument("--n", type=int, default=512)
@@ -53,7 +58,9 @@ def make(X, path=gcmx.PATH_AUTO, x0=0, loop=False):
     c.set_path(path)
     c.set_schedule(SCHED, args.rows)
     c.fill_random([N, N, N], 0x5EED)
-    if loop and args.loop_gbps >= 0:
+    if loop and args.rccl_self:
+        c.comm_init(gcm_amd.unique_id(), 1, 0, 0, 0)
+    elif loop and args.loop_gbps >= 0:
         c.comm_init_loopback(args.loop_gbps, args.loop_blocks)
     return c
 
@@ -107,6 +114,7 @@ for ranks in [int(r) for r in args.ranks.split(",")]:
                       "kernels": kern,
                       "sched": args.sched, "rows": args.rows,
                       "boundary_rows": os.environ.get("GCMX_BOUNDARY_ROWS", "default"),
-                      "exchange": (f"loopback {args.loop_gbps} GB/s per direction, "
+                      "exchange": "RCCL self-exchange (one-rank communicator)" if args.rccl_self else
+                                  (f"loopback {args.loop_gbps} GB/s per direction, "
                                    f"{args.loop_blocks} blocks" if args.loop_gbps >= 0 else
-                                   "none (transfers not emulated)")}), flush=True)
+                                   "none (transfers not emulated)"))}), flush=True)

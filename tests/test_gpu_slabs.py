@@ -277,6 +277,46 @@ def test_rccl_single_rank_communicator(G):
         c.close()
 
 
+@pytest.mark.parametrize("sched", ["auto", "xslab", "single", "split"])
+def test_rccl_self_exchange(G, sched):
+    """The REAL RCCL exchange on one GPU: a one-rank communicator whose left and
+    right neighbours are itself (gcmx_comm_init(.., 1, 0, 0, 0)), so every post
+    point runs the ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd group and
+    the ev_halo ordering an N > 1 rank runs.  RCCL pairs a rank's sends to itself
+    with its receives in posting order: the left ghosts receive the first two
+    inner planes, the right ghosts the last two.  3 steps (the boundary-first,
+    X-slab and one-launch schedules, and the split path's per-stage exchange) ==
+    the per-stage path with those ghosts written by gcmx_copy_box, bitwise."""
+    import gcm_amd
+    X, Y, Z, seed, steps = 18, 24, 64, 0x5EED, 3
+    a = _whole(G, X, Y, Z, seed)
+    if sched == "split":
+        a.set_path(G.PATH_SPLIT)
+    elif sched != "auto":
+        a.set_schedule({"xslab": G.SCHED_XSLAB, "single": G.SCHED_SINGLE}[sched])
+    a.comm_init(gcm_amd.unique_id(), 1, 0, 0, 0)
+    b = _whole(G, X, Y, Z, seed)
+    for _ in range(steps):
+        a.step(0.9)
+        b.copy_box([-2, 0, 0], [0, Y, Z], b, [0, 0, 0])
+        b.copy_box([X, 0, 0], [X + 2, Y, Z], b, [X - 2, 0, 0])
+        b.step(0.9)
+    a.sync()
+    assert a.last_path == ("split" if sched == "split" else "fused") and b.last_path == "split"
+    assert np.array_equal(_inner(a, a.download()), _inner(b, b.download()))
+    for c in (a, b):
+        c.close()
+
+
+def test_rccl_self_neighbour_needs_one_rank(G):
+    """A neighbour equal to the rank itself is refused in a multi-rank communicator."""
+    import gcm_amd
+    a = _whole(G, 8, 16, 32, 1)
+    with pytest.raises(gcm_amd.GcmxError):
+        a.comm_init(gcm_amd.unique_id(), 2, 0, 0, 1)
+    a.close()
+
+
 @pytest.mark.parametrize("sched", ["bfirst", "xslab"])
 @pytest.mark.parametrize("xs", [[4, 7, 5], [9, 6]])
 def test_local_group_border_size_one(G, sched, xs):

@@ -66,6 +66,35 @@ __global__ __launch_bounds__(256) void k_flat_chunk(const d2* __restrict__ in, d
 	}
 }
 
+// the two halves of a copy alone: U 16-B loads in flight per lane (summed, one
+// store per lane that never fires for the zeroed input), or U non-temporal 16-B stores
+template <int U>
+__global__ __launch_bounds__(256) void k_read_u(const d2* __restrict__ in, d2* __restrict__ out, long long n2) {
+	const long long nth = (long long)gridDim.x * blockDim.x;
+	long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	d2 acc = {0.0, 0.0};
+	for (; i + (U - 1) * nth < n2; i += U * nth) {
+		d2 v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) v[u] = in[i + u * nth];
+#pragma unroll
+		for (int u = 0; u < U; u++) acc += v[u];
+	}
+	for (; i < n2; i += nth) acc += in[i];
+	if (acc.x == 1.0e300) out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+template <int U>
+__global__ __launch_bounds__(256) void k_write_u(d2* __restrict__ out, long long n2, double val) {
+	const long long nth = (long long)gridDim.x * blockDim.x;
+	long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	const d2 v = {val, val};
+	for (; i + (U - 1) * nth < n2; i += U * nth) {
+#pragma unroll
+		for (int u = 0; u < U; u++) __builtin_nontemporal_store(v, out + i + u * nth);
+	}
+	for (; i < n2; i += nth) out[i] = v;
+}
+
 __global__ __launch_bounds__(512) void k_layout(const double* __restrict__ in, double* __restrict__ out,
                                                 long long cs, int chunk) {
 	const int z = threadIdx.x;
@@ -127,6 +156,19 @@ int main() {
 		const long long per = (n2 + nb - 1) / nb;
 		float a = timeit([&] { hipLaunchKernelGGL((k_flat_chunk<4>), dim3(nb), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2, per); });
 		std::printf("chunked %6d blocks (U4, nt stores): %.0f GB/s\n", nb, rate(a));
+	}
+	// read-only and write-only passes over the same 9.66 GB each: if HBM overlapped
+	// a copy's reads and writes perfectly the copy would take max(t_r, t_w); a copy
+	// near t_r + t_w means the stack alternates between the two directions
+	auto half = [&](float ms) { return 72.0 * nodes / (ms * 1e6); };
+	for (int g : {2048, 8192, 16384}) {
+		float r4 = timeit([&] { hipLaunchKernelGGL((k_read_u<4>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		float r8 = timeit([&] { hipLaunchKernelGGL((k_read_u<8>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		float w4 = timeit([&] { hipLaunchKernelGGL((k_write_u<4>), dim3(g), dim3(256), 0, 0, (d2*)out, n2, 0.0); });
+		float c4 = timeit([&] { hipLaunchKernelGGL((k_flat_u<4, true, false>), dim3(g), dim3(256), 0, 0, (const d2*)in, (d2*)out, n2); });
+		std::printf("grid %6d: read-only U4 %.3f ms (%.0f GB/s)  U8 %.3f ms (%.0f GB/s)  write-only U4 %.3f ms (%.0f GB/s)  "
+		            "copy U4 %.3f ms (%.0f GB/s; read+write alone %.3f ms)\n",
+		            g, r4, half(r4), r8, half(r8), w4, half(w4), c4, rate(c4), (r4 < r8 ? r4 : r8) + w4);
 	}
 	if (std::getenv("COPY_ONLY")) return 0;
 	for (int chunk : {128, 32}) {
