@@ -1513,6 +1513,30 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 		const char* e = std::getenv("GCMX_COMM_MAX_CTAS");
 		return e ? std::atoi(e) : 32;
 	}();
+	// Channels per peer.  With RCCL's default, one step's exchange group (a
+	// send and a receive per halo component and neighbour) runs as SIX kernel
+	// launches: the first beside the interior, the other five after it, on the
+	// next step's critical path.  An explicit NCCL_NCHANNELS_PER_PEER makes it
+	// ONE launch of 2 x channels CTAs, which must find CUs the interior leaves
+	// free: the one-rank self-exchange on MI355X measured
+	// 64-plane slabs (16 CUs free) 0.70 -> 0.62-0.65 ms/step with 6-8 channels,
+	// 128-plane slabs (8 free) 1.17 -> 1.10 ms with 2-4 (1.28-1.30 with 6-8),
+	// 256-plane slabs (4 free) best with RCCL's default (2.46 ms; 4 channels
+	// 2.58).  So: 8 channels with >= 16 free CUs, 4 with >= 8, else RCCL's own.
+	// NCCL reads the variable once per process (the first communicator's slab
+	// decides) and never overrides a value the user set; GCMX_COMM_CHANNELS_PER_PEER
+	// forces a value (0 = RCCL's default).
+	if (!std::getenv("NCCL_NCHANNELS_PER_PEER")) {
+		int per_peer = 0;
+		if (const char* e = std::getenv("GCMX_COMM_CHANNELS_PER_PEER")) {
+			per_peer = std::atoi(e);
+		} else if (hipSetDevice(c->device) == hipSuccess) {
+			const int X = c->geo.sizes[0], bs = c->bs;
+			const int free_cus = X > 2 * bs ? step_free_cus(c->geo, bs, X - bs, c->rows_per_block) : -1;
+			per_peer = free_cus >= 16 ? 8 : free_cus >= 8 ? 4 : 0;
+		}
+		if (per_peer > 0) setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per_peer).c_str(), 0);
+	}
 	ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
 	if (min_ctas > 0) {
 		cfg.minCTAs = min_ctas;

@@ -980,6 +980,21 @@ extern "C" int gcmx_diag_tx2(unsigned long long* out) {  // 16 x 8 counters, the
 }
 #endif
 
+// CUs the one-pass step leaves free while it covers planes [x0, x1) in one
+// round (the slab interior of the boundary-first schedule); 0 when its blocks
+// fill every CU or it takes more than one round, -1 when k_step_tx2 does not run.
+int step_free_cus(const Geo& g, int x0, int x1, int req_chunk) {
+	const int Z = g.sizes[2];
+	if (!fused_supported(g) || g.bs > 2 || Z > 512 || x1 <= x0) return -1;
+	const int ZT = Z <= 64 ? 64 : Z <= 128 ? 128 : Z <= 256 ? 256 : 512;
+	const int per_cu = 512 / ZT, cus = device_cus();
+	const int npair = (x1 - x0 + 1) / 2;
+	const int chunk = tx2_chunk_for(g.sizes[1], npair, req_chunk, cus * per_cu);
+	const long long blocks = (long long)((g.sizes[1] + chunk - 1) / chunk) * npair;
+	const long long slots = (long long)cus * per_cu;
+	return blocks >= slots ? 0 : (int)((slots - blocks) / per_cu);
+}
+
 bool het_supported(const Geo& g) {
 	const int Z = g.sizes[2];
 	return fused_supported(g) && g.bs <= 2 && (Z == 64 || Z == 128 || Z == 256 || Z == 512);

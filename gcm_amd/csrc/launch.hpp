@@ -90,6 +90,7 @@ bool het_supported(const Geo& g);
 // `kname`: set to the launched instance's symbol (a static string).
 // [xb0, xb1): an optional second plane range (xb0 >= x1) covered by the same
 // launch (the X-slab boundary sides; two launches on the k_fused_xyz path).
+int step_free_cus(const Geo& g, int x0, int x1, int req_chunk);
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,
                       const char** kname = nullptr, const HetMaterials* het = nullptr, int xb0 = 0,

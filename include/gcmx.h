@@ -218,7 +218,14 @@ gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]);
  * ncclSend/ncclRecv group then runs against itself, and RCCL matches a rank's
  * sends to itself with its receives in posting order, so the left ghost planes
  * receive the slab's first bs inner planes and the right ghost planes its last
- * bs (the RCCL transport exercised on a one-GPU box; not periodic). */
+ * bs (the RCCL transport exercised on a one-GPU box; not periodic).
+ * Environment read at the first gcmx_comm_init of a process: GCMX_COMM_MIN_CTAS
+ * / GCMX_COMM_MAX_CTAS (ncclConfig_t minCTAs / maxCTAs, default 16 / 32) and
+ * GCMX_COMM_CHANNELS_PER_PEER (0 = RCCL's default), which sets
+ * NCCL_NCHANNELS_PER_PEER unless the user already set it; by default 8 when
+ * the slab's interior launch leaves >= 16 CUs free, 4 with >= 8, else RCCL's
+ * own (with RCCL's default the step's exchange group runs as six kernel
+ * launches instead of one). */
 gcmx_status gcmx_comm_init(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES],
                            int nranks, int rank, int left, int right);
 /* Fill the X ghost layers of the current layer from the neighbours' boundary

@@ -117,4 +117,4 @@ for ranks in [int(r) for r in args.ranks.split(",")]:
                       "exchange": "RCCL self-exchange (one-rank communicator)" if args.rccl_self else
                                   (f"loopback {args.loop_gbps} GB/s per direction, "
                                    f"{args.loop_blocks} blocks" if args.loop_gbps >= 0 else
-                                   "none (transfers not emulated)"))}), flush=True)
+                                   "none (transfers not emulated)")}), flush=True)
