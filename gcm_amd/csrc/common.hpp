@@ -21,6 +21,17 @@ constexpr int kRowAlign = 16;  // doubles (128 B)
 __host__ __device__ constexpr int pde_size(int D) { return D + D * (D + 1) / 2; }
 
 // Geometry of one context's device layers.
+// Position of block b of a 1-D grid of T blocks in an XCD-contiguous order:
+// blocks are dealt round-robin over the 8 XCDs (b % 8 share one,
+// MI355X_MICROARCH.md §Workgroup dispatch), so XCD k, which receives
+// ceil((T - k) / 8) blocks, gets the k-th contiguous run of positions.  Any T
+// (a grid of 252 blocks used to fall back to the identity order and scatter
+// neighbouring planes over the XCDs).
+__device__ __forceinline__ int xcd_order(int b, int T) {
+	const int q = T >> 3, r = T & 7, k = b & 7;
+	return k * q + (k < r ? k : r) + (b >> 3);
+}
+
 struct Geo {
 	int D, M, bs;
 	int sizes[3];          // inner nodes (1 for axes >= D)

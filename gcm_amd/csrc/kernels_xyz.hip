@@ -77,7 +77,7 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 	int x, yb;
 	{
 		const int nx = (int)nplanes, T = (int)gridDim.x, b = (int)blockIdx.x;
-		const int p = (T % 8 == 0) ? (b % 8) * (T / 8) + b / 8 : b;
+		const int p = xcd_order(b, T);
 		x = x0 + p % nx;
 		yb = (p / nx) * chunk;
 	}
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	   // range A [x0, x0 + nplanes), then range B [xb0, xb0 + nplanesb) (may be empty)
 		const int npa = (nplanes + 1) / 2, npair = npa + (nplanesb + 1) / 2;
 		const int T = (int)gridDim.x, b = (int)blockIdx.x;
-		const int p = (T % 8 == 0) ? (b % 8) * (T / 8) + b / 8 : b;
+		const int p = xcd_order(b, T);
 		const int q = p % npair;
 		x = q < npa ? x0 + 2 * q : xb0 + 2 * (q - npa);
 		xend = q < npa ? x0 + nplanes : xb0 + nplanesb;
