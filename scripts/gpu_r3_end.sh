@@ -25,6 +25,11 @@ for K in ${SLABS:-8 4 2}; do
 done
 timeout -k 10 200 python scripts/bench_slab.py --ranks 8,4,2 --steps 30 > $OUT/slab.jsonl 2> $OUT/slab.err || { tail $OUT/slab.err; exit 1; }
 timeout -k 10 200 python scripts/bench_slab.py --ranks 8,4,2 --steps 30 --loop-gbps 64 --no-check > $OUT/slab_loop64.jsonl 2>> $OUT/slab.err || { tail $OUT/slab.err; exit 1; }
+: > $OUT/slab_rccl_self.jsonl
+for r in 8 4 2; do  # one process per slab size: the first communicator fixes RCCL's channels per peer
+  timeout -k 10 200 python scripts/bench_slab.py --ranks $r --steps 30 --rccl-self --no-check >> $OUT/slab_rccl_self.jsonl 2>> $OUT/slab.err \
+    || { tail $OUT/slab.err; exit 1; }
+done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sx64 -o run -- \
   python3 scripts/bench_simplex.py --workloads cube --n 64 --lanes 1 --steps 20 > $OUT/simplex64.jsonl 2> $OUT/simplex64.err \
   || { echo "simplex64 rc=$?"; tail $OUT/simplex64.err; exit 1; }
@@ -45,8 +50,10 @@ for f in ("bench_512.json", "bench_256.json"):
 for f in sorted(glob.glob(f"{o}/emulate_*.json")):
     d = json.load(open(f))
     print(f.split("/")[-1], d["ms_per_step"], d.get("per_rank_ms_per_step"), d.get("speedup_if_ranks_ran_this_fast_on_K_gpus"))
-for f in ("slab.jsonl", "slab_loop64.jsonl"):
+for f in ("slab.jsonl", "slab_loop64.jsonl", "slab_rccl_self.jsonl"):
     for l in open(f"{o}/{f}"):
+        if not l.startswith("{"):
+            continue
         d = json.loads(l)
         if "ranks" in d:
             print(f, d["ranks"], d["ms_per_step"], d["kernels"])
