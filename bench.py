@@ -317,6 +317,7 @@ def main():
     if a.rows_per_block:
         ctx.set_schedule(gcmx.SCHED_AUTO, a.rows_per_block)
     ctx.fill_random([N, N, N], 0x5EED)
+    ctx_fp = ctx.fp_mode
     if world > 1:
         uid = gcm_amd.unique_id() if rank == 0 else None
         obj = [uid]
@@ -422,6 +423,11 @@ def main():
                                    f"Courant 0.9, tau 0.9, one full time step (3 stages)",
                        "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,
                        "parallelism": f"x-slab{world}" if world > 1 else "single",
+                       # the one-pass step's floating-point build (gcmx_set_fp_mode): "fma" =
+                       # multiply-adds contracted, the product default, held to the north
+                       # star's 1e-10 relative L2 of the reference (tests/test_gpu_fma.py);
+                       # "exact" = the reference's roundings, bitwise (GCMX_FP=exact)
+                       "fp": "exact" if ctx_fp == gcmx.FP_EXACT else "fma",
                        **({"rows_per_block": a.rows_per_block} if a.rows_per_block else {})},
             # NOT an HBM rate: the bytes three separate stage passes (SURVEY §8d, 432 B per
             # node-step) would move, over the measured step time; the one-pass step moves 144 B

@@ -5,10 +5,10 @@ gfx950 HIP kernels behind the C-ABI declared in ``include/gcmx.h``.  This packag
 holds the Python side of that boundary (``gcm_amd.gcmx``) and the host mirror of
 the reference's Engine / Task / factory surface (``gcm_amd.engine``).
 """
-from .gcmx import (Context, GcmxError, LIB_PATH, PATH_AUTO, PATH_FUSED, PATH_GENERIC,
+from .gcmx import (Context, FP_EXACT, FP_FMA, GcmxError, LIB_PATH, PATH_AUTO, PATH_FUSED, PATH_GENERIC,
                    PATH_SPLIT, SCHED_AUTO, SCHED_BFIRST, SCHED_SINGLE, SCHED_XSLAB, comm_init_local, lib,
                    local_group_steps, pde_size, unique_id)
 
-__all__ = ["Context", "GcmxError", "LIB_PATH", "PATH_AUTO", "PATH_FUSED", "PATH_GENERIC",
+__all__ = ["Context", "FP_EXACT", "FP_FMA", "GcmxError", "LIB_PATH", "PATH_AUTO", "PATH_FUSED", "PATH_GENERIC",
            "PATH_SPLIT", "SCHED_AUTO", "SCHED_BFIRST", "SCHED_SINGLE", "SCHED_XSLAB", "comm_init_local", "lib",
            "local_group_steps", "pde_size", "unique_id"]

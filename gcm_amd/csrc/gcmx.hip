@@ -131,6 +131,7 @@ struct gcmx_ctx {
 	gcmx_schedule sched = GCMX_SCHED_AUTO;
 	gcmx_path last_path = GCMX_PATH_AUTO;  // what the last step / stage ran
 	int rows_per_block = 0;        // fused kernel y rows per block (0 = automatic)
+	gcmx_fp_mode fp_mode = GCMX_FP_FMA;  // one-pass step build: contracted (default) or exact
 	// halo exchange
 	ncclComm_t comm = nullptr;
 	int nranks = 1, rank = 0, left = -1, right = -1;
@@ -734,6 +735,9 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 
 	auto* c = new gcmx_ctx();
 	c->device = device;
+	// GCMX_FP=exact makes the exact build every new context's default (tests
+	// that compare with the oracle bitwise); anything else keeps FMA.
+	if (const char* e = std::getenv("GCMX_FP")) c->fp_mode = std::strcmp(e, "exact") == 0 ? GCMX_FP_EXACT : GCMX_FP_FMA;
 	c->desc = *d;
 	c->D = d->dim;
 	c->M = pde_size(d->dim);
@@ -1043,8 +1047,9 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows, int xb0 = 0, int xb1 = 0) {
 		Timed t(c, name, plane_bytes * ((x1 - x0) + (xb1 - xb0)), st);
 		const HetMaterials het{c->het_d, c->mat_d};
-		return launch_fused_xyz(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb, &t.kname,
-		                        c->iso_het ? &het : nullptr, xb0, xb1);
+		auto launch = c->fp_mode == GCMX_FP_EXACT ? xyz_exact::launch_fused_xyz : xyz_fma::launch_fused_xyz;
+		return launch(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb, &t.kname, c->iso_het ? &het : nullptr,
+		              xb0, xb1);
 	};
 	const gcmx_schedule sched =
 	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_BFIRST : GCMX_SCHED_SINGLE) : c->sched;
@@ -1118,6 +1123,18 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 			if (s) return s;
 		}
 		ok = xyz("fused_xyz", 0, X, c->stream, c->rows_per_block);
+		// A slab too thin for the boundary / interior split (X < 4 bs) under the
+		// boundary-first or X-slab schedule still keeps their exchange protocol
+		// -- its new planes posted right after the step, one post per step --
+		// so that it pairs with neighbours that run the split (a group of 8-,
+		// 6- and 10-plane slabs otherwise waited forever for a post the thin
+		// slab never made).
+		if (ok && halo && (sched == GCMX_SCHED_BFIRST || sched == GCMX_SCHED_XSLAB)) {
+			std::swap(c->cur, c->nxt);
+			s = halo_post(c);
+			std::swap(c->cur, c->nxt);
+			if (s) return s;
+		}
 	}
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
 	HIP_TRY(hipGetLastError());
@@ -1288,6 +1305,20 @@ gcmx_status step_faces_impl(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 }  // namespace
 
 extern "C" {
+
+gcmx_status gcmx_set_fp_mode(gcmx_ctx* c, gcmx_fp_mode mode) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (mode != GCMX_FP_FMA && mode != GCMX_FP_EXACT) return fail(GCMX_ERR_INVALID_ARG, "unknown fp mode");
+	c->fp_mode = mode;
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_get_fp_mode(const gcmx_ctx* c, gcmx_fp_mode* mode) {
+	if (!c || !mode) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	*mode = c->fp_mode;
+	return GCMX_OK;
+}
 
 gcmx_status gcmx_set_step_schedule(gcmx_ctx* c, gcmx_schedule sched, int rows_per_block) {
 	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");

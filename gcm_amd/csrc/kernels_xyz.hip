@@ -9,6 +9,22 @@
 #include <type_traits>
 
 namespace gcmx {
+// This file is compiled twice (Makefile): as the exact build (xyz_exact,
+// -ffp-contract=off: the reference's separate multiply and add roundings,
+// bitwise equal to the oracle) and as the FMA build (xyz_fma, -DGCMX_FMA=1
+// -ffp-contract=fast: multiply-adds contracted, within the north-star fp64
+// tolerance of the reference).  gcmx_set_fp_mode selects one.
+#ifndef GCMX_FMA
+#define GCMX_FMA 0
+#endif
+#if GCMX_FMA
+#define GCMX_XYZ_NS xyz_fma
+#define GCMX_FP_TAG ", FMA"
+#else
+#define GCMX_XYZ_NS xyz_exact
+#define GCMX_FP_TAG ""
+#endif
+namespace GCMX_XYZ_NS {
 
 // ------------------------------------------------------------- fused xyz --
 
@@ -848,13 +864,13 @@ template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET>
 static const char* tx2_name() {
 	static const std::string s = "k_step_tx2<" + std::to_string(BS) + ", " + std::to_string(ZT) + ", " +
 	                             (KF0 ? "KF0" : "!KF0") + ", " + (UNI ? "UNI" : "!UNI") + ", " +
-	                             (FACES ? "FACES" : "!FACES") + (HET ? ", HET" : "") + ">";
+	                             (FACES ? "FACES" : "!FACES") + (HET ? ", HET" : "") + GCMX_FP_TAG + ">";
 	return s.c_str();
 }
 template <int BS, int ZT, bool KF0, bool UNI>
 static const char* xyz_name() {
 	static const std::string s = "k_fused_xyz<" + std::to_string(BS) + ", " + std::to_string(ZT) + ", " +
-	                             (KF0 ? "KF0" : "!KF0") + ", " + (UNI ? "UNI" : "!UNI") + ">";
+	                             (KF0 ? "KF0" : "!KF0") + ", " + (UNI ? "UNI" : "!UNI") + GCMX_FP_TAG + ">";
 	return s.c_str();
 }
 
@@ -972,38 +988,13 @@ static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const Iso
 	return true;
 }
 
-#if GCMX_TX2_DIAG
+#if GCMX_TX2_DIAG && !GCMX_FMA
 extern "C" int gcmx_diag_tx2(unsigned long long* out) {  // 16 x 8 counters, then reset
 	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tx2_diag), sizeof(g_tx2_diag)) != hipSuccess) return -1;
 	static const unsigned long long zero[16][8] = {};
 	return hipMemcpyToSymbol(HIP_SYMBOL(g_tx2_diag), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif
-
-// CUs the one-pass step leaves free while it covers planes [x0, x1) in one
-// round (the slab interior of the boundary-first schedule); 0 when its blocks
-// fill every CU or it takes more than one round, -1 when k_step_tx2 does not run.
-int step_free_cus(const Geo& g, int x0, int x1, int req_chunk) {
-	const int Z = g.sizes[2];
-	if (!fused_supported(g) || g.bs > 2 || Z > 512 || x1 <= x0) return -1;
-	const int ZT = Z <= 64 ? 64 : Z <= 128 ? 128 : Z <= 256 ? 256 : 512;
-	const int per_cu = 512 / ZT, cus = device_cus();
-	const int npair = (x1 - x0 + 1) / 2;
-	const int chunk = tx2_chunk_for(g.sizes[1], npair, req_chunk, cus * per_cu);
-	const long long blocks = (long long)((g.sizes[1] + chunk - 1) / chunk) * npair;
-	const long long slots = (long long)cus * per_cu;
-	return blocks >= slots ? 0 : (int)((slots - blocks) / per_cu);
-}
-
-bool het_supported(const Geo& g) {
-	const int Z = g.sizes[2];
-	return fused_supported(g) && g.bs <= 2 && (Z == 64 || Z == 128 || Z == 256 || Z == 512);
-}
-
-bool fused_faces_supported(const Geo& g) {
-	return fused_supported(g) && g.bs <= 2 && g.sizes[2] <= 512 && g.sizes[1] >= 2 * g.bs + 2 &&
-	       g.sizes[2] >= 2 * g.bs + 2;
-}
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk, const FaceBC* faces, const char** kname,
@@ -1022,5 +1013,35 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	default: return false;
 	}
 }
+
+}  // namespace GCMX_XYZ_NS
+
+#if !GCMX_FMA
+// CUs the one-pass step leaves free while it covers planes [x0, x1) in one
+// round (the slab interior of the boundary-first schedule); 0 when its blocks
+// fill every CU or it takes more than one round, -1 when k_step_tx2 does not run.
+int step_free_cus(const Geo& g, int x0, int x1, int req_chunk) {
+	const int Z = g.sizes[2];
+	if (!fused_supported(g) || g.bs > 2 || Z > 512 || x1 <= x0) return -1;
+	const int ZT = Z <= 64 ? 64 : Z <= 128 ? 128 : Z <= 256 ? 256 : 512;
+	const int per_cu = 512 / ZT, cus = GCMX_XYZ_NS::device_cus();
+	const int npair = (x1 - x0 + 1) / 2;
+	const int chunk = GCMX_XYZ_NS::tx2_chunk_for(g.sizes[1], npair, req_chunk, cus * per_cu);
+	const long long blocks = (long long)((g.sizes[1] + chunk - 1) / chunk) * npair;
+	const long long slots = (long long)cus * per_cu;
+	return blocks >= slots ? 0 : (int)((slots - blocks) / per_cu);
+}
+
+bool het_supported(const Geo& g) {
+	const int Z = g.sizes[2];
+	return fused_supported(g) && g.bs <= 2 && (Z == 64 || Z == 128 || Z == 256 || Z == 512);
+}
+
+bool fused_faces_supported(const Geo& g) {
+	return fused_supported(g) && g.bs <= 2 && g.sizes[2] <= 512 && g.sizes[1] >= 2 * g.bs + 2 &&
+	       g.sizes[2] >= 2 * g.bs + 2;
+}
+
+#endif
 
 }  // namespace gcmx

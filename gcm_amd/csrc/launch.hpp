@@ -91,9 +91,20 @@ bool het_supported(const Geo& g);
 // [xb0, xb1): an optional second plane range (xb0 >= x1) covered by the same
 // launch (the X-slab boundary sides; two launches on the k_fused_xyz path).
 int step_free_cus(const Geo& g, int x0, int x1, int req_chunk);
+// Two builds of the one-pass step kernels (kernels_xyz.hip): xyz_exact keeps the
+// reference's roundings (bitwise), xyz_fma contracts multiply-adds
+// (gcmx_set_fp_mode).
+namespace xyz_exact {
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,
                       const char** kname = nullptr, const HetMaterials* het = nullptr, int xb0 = 0,
                       int xb1 = 0);
+}
+namespace xyz_fma {
+bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
+                      int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,
+                      const char** kname = nullptr, const HetMaterials* het = nullptr, int xb0 = 0,
+                      int xb1 = 0);
+}
 
 }  // namespace gcmx

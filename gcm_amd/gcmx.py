@@ -26,6 +26,7 @@ STATUS_NAMES = {0: "GCMX_OK", 1: "GCMX_ERR_INVALID_ARG", 2: "GCMX_ERR_CFL", 3: "
 PATH_AUTO, PATH_GENERIC, PATH_SPLIT, PATH_FUSED = 0, 1, 2, 3
 PATH_NAMES = {0: "auto", 1: "generic", 2: "split", 3: "fused"}
 SCHED_AUTO, SCHED_SINGLE, SCHED_XSLAB, SCHED_BFIRST = 0, 1, 2, 3
+FP_FMA, FP_EXACT = 0, 1
 UNIQUE_ID_BYTES = 128
 MAX_BORDER_Q = 16
 QUANTITY_CODES = {"Vx": 2, "Vy": 3, "Vz": 4, "Sxx": 5, "Sxy": 6, "Sxz": 7, "Syy": 8, "Syz": 9,
@@ -36,7 +37,7 @@ SYMBOLS = [
     "gcmx_abi_version", "gcmx_last_error", "gcmx_pde_size", "gcmx_status_string",
     "gcmx_create", "gcmx_destroy", "gcmx_set_materials", "gcmx_set_material_ids",
     "gcmx_upload", "gcmx_download", "gcmx_fill_random", "gcmx_stage", "gcmx_step",
-    "gcmx_set_kernel_path", "gcmx_set_step_schedule", "gcmx_effective_path", "gcmx_last_step_path",
+    "gcmx_set_kernel_path", "gcmx_set_step_schedule", "gcmx_set_fp_mode", "gcmx_get_fp_mode", "gcmx_effective_path", "gcmx_last_step_path",
     "gcmx_border_fill",
     "gcmx_border_nodes_create", "gcmx_border_apply", "gcmx_border_nodes_destroy", "gcmx_step_faces",
     "gcmx_copy_box",
@@ -109,6 +110,8 @@ def lib() -> ctypes.CDLL:
     L.gcmx_step.argtypes = [vp, ctypes.c_double]
     L.gcmx_set_kernel_path.argtypes = [vp, ctypes.c_int]
     L.gcmx_set_step_schedule.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    L.gcmx_set_fp_mode.argtypes = [vp, ctypes.c_int]
+    L.gcmx_get_fp_mode.argtypes = [vp, ip]
     L.gcmx_effective_path.argtypes = [vp]
     L.gcmx_last_step_path.argtypes = [vp]
     L.gcmx_border_fill.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int,
@@ -255,6 +258,18 @@ class Context:
     def set_schedule(self, sched: int, rows_per_block: int = 0):
         """gcmx_set_step_schedule: SCHED_AUTO / SCHED_SINGLE / SCHED_XSLAB / SCHED_BFIRST."""
         _check(lib().gcmx_set_step_schedule(self._ptr, sched, rows_per_block))
+
+    @property
+    def fp_mode(self) -> int:
+        """gcmx_get_fp_mode: FP_FMA (default) or FP_EXACT."""
+        m = ctypes.c_int(0)
+        _check(lib().gcmx_get_fp_mode(self._ptr, ctypes.byref(m)))
+        return m.value
+
+    @fp_mode.setter
+    def fp_mode(self, mode: int):
+        """gcmx_set_fp_mode: the one-pass step's floating-point build."""
+        _check(lib().gcmx_set_fp_mode(self._ptr, mode))
 
     @property
     def effective_path(self) -> str:

@@ -61,6 +61,15 @@ typedef enum gcmx_path {
 	GCMX_PATH_FUSED = 3    /* the whole step in one pass (k_fused_xyz), 3-D only  */
 } gcmx_path;
 
+/* Floating-point build of the one-pass step (gcmx_set_fp_mode). */
+typedef enum gcmx_fp_mode {
+	GCMX_FP_FMA = 0,   /* multiply-adds contracted (default): within the north-star fp64
+	                      tolerance of the reference (relative L2 <= 1e-10; measured
+	                      ~1e-16 per step), 6-7 % faster at 512^3                    */
+	GCMX_FP_EXACT = 1  /* the reference's separate multiply and add roundings: bitwise
+	                      equal to the oracle / reference CPU path                  */
+} gcmx_fp_mode;
+
 /* How gcmx_step issues the fused pass (gcmx_set_step_schedule). */
 typedef enum gcmx_schedule {
 	GCMX_SCHED_AUTO = 0,   /* boundary-first schedule when a halo exchange is
@@ -127,6 +136,11 @@ gcmx_status gcmx_set_kernel_path(gcmx_ctx* ctx, gcmx_path path);
  * (0 = automatic).  Results do not depend on either (tests/test_gpu_parity.py);
  * only the overlap of the X-slab halo exchange with compute does. */
 gcmx_status gcmx_set_step_schedule(gcmx_ctx* ctx, gcmx_schedule sched, int rows_per_block);
+/* The one-pass step's floating-point build (k_step_tx2 / k_fused_xyz; the
+ * per-stage kernels always keep the reference's roundings).  Default FMA;
+ * environment GCMX_FP=exact makes EXACT the default of new contexts. */
+gcmx_status gcmx_set_fp_mode(gcmx_ctx* ctx, gcmx_fp_mode mode);
+gcmx_status gcmx_get_fp_mode(const gcmx_ctx* ctx, gcmx_fp_mode* mode);
 /* Which path gcmx_step would take now (after materials are set). */
 gcmx_path   gcmx_effective_path(gcmx_ctx* ctx);
 /* The path the last gcmx_step / gcmx_step_faces / gcmx_stage ran

@@ -4,6 +4,12 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# The suite compares the GPU with the oracle BITWISE, i.e. in the exact build of
+# the one-pass step (gcmx_set_fp_mode GCMX_FP_EXACT); every context a test
+# creates starts in it.  The product default (GCMX_FP_FMA, multiply-adds
+# contracted) is tested against the north-star tolerance in test_gpu_fma.py,
+# which sets the mode per context.
+os.environ["GCMX_FP"] = "exact"
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 

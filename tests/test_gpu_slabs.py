@@ -95,7 +95,7 @@ def _run_threads(fns):
 
 
 @pytest.mark.parametrize("sched", ["auto", "single", "xslab", "bfirst"])
-@pytest.mark.parametrize("xs", [[17, 23], [12, 9, 19]])
+@pytest.mark.parametrize("xs", [[17, 23], [12, 9, 19], [8, 6, 10], [9, 6, 7]])
 def test_local_group_fused_equals_whole(G, sched, xs):
     """Ragged slabs on the fused path: the X-slab schedule (auto: a configured
     exchange selects it) with the in-step overlapped exchange, and the one-launch

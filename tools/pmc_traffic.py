@@ -27,6 +27,8 @@ def readable(rocprof_name):
     a = [x.strip() for x in m.group(2).split(",")]
     flags = ["KF0", "UNI", "FACES"]
     out = a[:2] + [(f if v == "true" else "!" + f) for f, v in zip(flags, a[2:])]
+    if "xyz_fma::" in rocprof_name:  # the contracted build (gcmx_set_fp_mode), as the library names it
+        out.append("FMA")
     return f"{m.group(1)}<{', '.join(out)}>"
 
 
