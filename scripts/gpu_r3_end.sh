@@ -35,6 +35,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/s
   || { echo "simplex64 rc=$?"; tail $OUT/simplex64.err; exit 1; }
 timeout -k 10 300 python scripts/bench_simplex.py --workloads cubetask,cube,fracture --n 16 --steps 200 \
   > $OUT/simplex16.jsonl 2> $OUT/simplex.err || { tail $OUT/simplex.err; exit 1; }
+timeout -k 10 300 python scripts/fma_report.py > $OUT/fma_report.jsonl 2> $OUT/fma_report.err || { tail $OUT/fma_report.err; exit 1; }
+cat $OUT/fma_report.jsonl
 if [ "${PROF:-1}" = 1 ]; then
   TAG=r3${TAG:-end} bash scripts/gpu_profile.sh > $OUT/profile.log 2>&1 || { tail $OUT/profile.log; exit 1; }
   tail -3 $OUT/profile.log
