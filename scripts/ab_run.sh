@@ -7,7 +7,7 @@ for rep in 1 2; do
 for d in gcm_amd/lib/tune/*/; do
   name=$(basename "$d")
   if [ $rep = 1 ]; then
-    GCMX_LIB="$d/libgcmx.so" timeout -k 10 120 python scripts/ab_check.py > gpurun_out/ab/$name.check 2>&1
+    GCMX_FP=exact GCMX_LIB="$d/libgcmx.so" timeout -k 10 120 python scripts/ab_check.py > gpurun_out/ab/$name.check 2>&1
     rc=$?; echo "$name: $(tail -1 gpurun_out/ab/$name.check)"
     [ $rc -le 1 ] || exit $rc
   fi
