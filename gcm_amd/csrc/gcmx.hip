@@ -1554,13 +1554,21 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 	// 128-plane slabs (8 free) 1.17 -> 1.10 ms with 2-4 (1.28-1.30 with 6-8),
 	// 256-plane slabs (4 free) best with RCCL's default (2.46 ms; 4 channels
 	// 2.58).  So: 8 channels with >= 16 free CUs, 4 with >= 8, else RCCL's own.
-	// NCCL reads the variable once per process (the first communicator's slab
-	// decides) and never overrides a value the user set; GCMX_COMM_CHANNELS_PER_PEER
-	// forces a value (0 = RCCL's default).
+	// Both ends of a p2p connection must use the same count, so with several
+	// ranks the choice may depend only on what every rank knows alike: the
+	// rank count (nranks >= 8 -> 8, >= 4 -> 4, else RCCL's own -- the same
+	// choices for the 512^3 decompositions into 8, 4 and 2 even slabs, whose
+	// interiors leave 16, 8 and 4 CUs free); a one-rank communicator (the
+	// self-exchange) applies the free-CU rule to its own slab.  NCCL reads the
+	// variable once per process (the first communicator decides) and never
+	// overrides a value the user set; GCMX_COMM_CHANNELS_PER_PEER forces a
+	// value (0 = RCCL's default) and must then be equal on every rank.
 	if (!std::getenv("NCCL_NCHANNELS_PER_PEER")) {
 		int per_peer = 0;
 		if (const char* e = std::getenv("GCMX_COMM_CHANNELS_PER_PEER")) {
 			per_peer = std::atoi(e);
+		} else if (nranks > 1) {
+			per_peer = nranks >= 8 ? 8 : nranks >= 4 ? 4 : 0;
 		} else if (hipSetDevice(c->device) == hipSuccess) {
 			const int X = c->geo.sizes[0], bs = c->bs;
 			const int free_cus = X > 2 * bs ? step_free_cus(c->geo, bs, X - bs, c->rows_per_block) : -1;
