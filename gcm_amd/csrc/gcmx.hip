@@ -1496,7 +1496,12 @@ gcmx_status gcmx_copy_box(gcmx_ctx* dst, const int dmin[3], const int dmax[3], g
 		    smin[d] + ext[d] > src->geo.sizes[d] + src->bs)
 			return fail(GCMX_ERR_INVALID_ARG, "box outside the grid");
 	}
-	dst->ghosts_touched = true;
+	// A 3-D box inside the x ghost planes ([-bs, 0) or [X, X + bs): a contact
+	// along x, ContactCopier for stage 0) fills exactly what the one-pass step
+	// reads as x ghosts, like the X-slab halo, so the fused path stays
+	// admissible; any other ghost write selects the per-stage path.
+	const bool x_ghosts_only = D == 3 && (dmax[0] <= 0 || dmin[0] >= dst->geo.sizes[0]);
+	if (!x_ghosts_only) dst->ghosts_touched = true;
 	if ((s = halo_wait(dst)) != GCMX_OK || (s = halo_wait(src)) != GCMX_OK) return s;
 	// order the copy after the source's pending work
 	HIP_TRY(hipEventRecord(src->ev_ready, src->stream));

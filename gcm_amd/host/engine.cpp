@@ -513,10 +513,12 @@ void Engine<D>::createGridsAndContacts(const Task& task) {
 // Engine.cpp:90-121
 template <int D>
 void Engine<D>::nextTimeStep() {
-	bool plain = true, faces = true;
+	bool plain = true, faces = true, xcontacts = D == 3;
 	for (const Body& b : bodies) {
 		plain = plain && b.border->empty() && b.contacts.empty();
 		faces = faces && b.border->uniformFaces() && b.contacts.empty();
+		xcontacts = xcontacts && b.border->empty();
+		for (const auto& contact : b.contacts) xcontacts = xcontacts && contact.direction == 0;
 	}
 	// A body whose only ODE is MaxwellViscosityOde hands it to the library with
 	// the step (gcmx_step_ode): the same results as the stages followed by the ODE
@@ -524,9 +526,19 @@ void Engine<D>::nextTimeStep() {
 	auto oneMaxwell = [](const Body& b) {
 		return b.odes.size() == 1 && dynamic_cast<const HipMaxwellViscosityOde<D>*>(b.odes[0].get()) != nullptr;
 	};
-	if (plain) {
+	if (plain || xcontacts) {
 		// No border or contact work between the stages: one gcmx_step per body
-		// (identical results; lets the library use its fused kernels).
+		// (identical results; lets the library use its fused kernels).  3-D
+		// bodies whose contacts all lie along x: every ContactCopier of the step
+		// runs before stage 0 and reads the neighbours' layer E_n
+		// (Engine.cpp:99-107), and only stage 0 reads x ghosts, so all copies go
+		// first, then one gcmx_step per body (the x-ghost copy keeps the
+		// one-pass step admissible, gcmx_copy_box).
+		if (!plain)
+			for (Body& body : bodies)
+				for (auto& contact : body.contacts)
+					contact.copier->apply(dynamic_cast<HipMesh<D>&>(*body.mesh),
+					                      dynamic_cast<const HipMesh<D>&>(*getBody(contact.neighborId).mesh));
 		for (Body& b : bodies) {
 			HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(*b.mesh);
 			if (oneMaxwell(b)) {

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 FACE_FORCE = {0: ["Sxx", "Sxy", "Sxz"], 1: ["Sxy", "Syy", "Syz"], 2: ["Sxz", "Syz", "Szz"]}
 
 
-def task(n, maxwell, layers=False, free=True):
+def task(n, maxwell, layers=False, free=True, xbodies=1):
     from gcm_amd import _gcm_host as H
     t = H.Task()
     t.dimensionality = 3
@@ -28,7 +28,12 @@ def task(n, maxwell, layers=False, free=True):
     t.h = [1.0, 1.0, 1.0]
     t.courant = 0.9
     t.number_of_snaps = 10 ** 6
-    t.add_body(0, [n, n, n], [0, 0, 0])
+    if xbodies > 1:  # the domain as bodies stacked along x: contacts along x (engine: one pass)
+        w = n // xbodies
+        for k in range(xbodies):
+            t.add_body(k, [w, n, n], [k * w, 0, 0])
+    else:
+        t.add_body(0, [n, n, n], [0, 0, 0])
     t.set_default_material(4.0, 2.0, 1.0, tau0=50.0 if maxwell else 0.0)
     if layers:  # a second material in the upper half along x (TestEngine.cpp:139-296's two layers)
         t.add_material(("box", (n / 2 - 0.5, -1, -1), (2 * n, 2 * n, 2 * n)), 2.0, 1.0, 0.5,
@@ -50,23 +55,32 @@ def main():
     ap.add_argument("--maxwell", action="store_true")
     ap.add_argument("--layers", action="store_true",
                     help="two materials (per-node material ids: the heterogeneous path)")
+    ap.add_argument("--xbodies", type=int, default=1,
+                    help="split the domain into this many bodies along x (contacts along x)")
     ap.add_argument("--free", action=argparse.BooleanOptionalAction, default=True,
                     help="free surfaces on all faces (--no-free: ghosts stay zero)")
     a = ap.parse_args()
     from gcm_amd import _gcm_host as H
-    e = H.Engine(task(a.n, a.maxwell, a.layers, a.free))
+    e = H.Engine(task(a.n, a.maxwell, a.layers, a.free and a.xbodies == 1, a.xbodies))
+    free = a.free and a.xbodies == 1
+    nb = max(1, a.xbodies)
+
+    def sync_all():
+        for b in range(nb):
+            e.sync(b)
     e.run_steps(a.warmup)
-    e.sync()
+    sync_all()
     t0 = time.perf_counter()
     e.run_steps(a.steps)
-    e.sync()
+    sync_all()
     dt = time.perf_counter() - t0
     print(json.dumps({
-        "metric": "Mnode-steps/s, cubic engine" + (" with free surfaces" if a.free else "") +
-                  (" + Maxwell ODE" if a.maxwell else "") + (", two materials" if a.layers else ""),
+        "metric": "Mnode-steps/s, cubic engine" + (" with free surfaces" if free else "") +
+                  (" + Maxwell ODE" if a.maxwell else "") + (", two materials" if a.layers else "") +
+                  (f", {nb} bodies along x with contacts" if nb > 1 else ""),
         "value": round(a.n ** 3 * a.steps / dt / 1e6, 1), "unit": "Mnode-steps/s",
         "ms_per_step": round(dt / a.steps * 1e3, 4), "n": a.n, "steps": a.steps,
-        "path": e.path(0), "last_path": e.last_path(0), "ode_fused": e.ode_fused(0),
+        "path": e.path(0), "last_path": [e.last_path(b) for b in range(nb)], "ode_fused": e.ode_fused(0),
         "dtype": "f64"}), flush=True)
 
 

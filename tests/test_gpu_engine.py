@@ -103,6 +103,34 @@ def test_engine_adhesion_contact(H):
     assert_bodies_equal(oe, two, adhesion(True))
 
 
+def xcontact(two):
+    """Two 3-D bodies stacked along x (a contact along the stage-0 axis) or one."""
+    X, Y, Z = 12, 20, 64
+    cubics = {0: ([X, Y, Z], [0, 0, 0]), 1: ([X, Y, Z], [X, 0, 0])} if two else {0: ([2 * X, Y, Z], [0, 0, 0])}
+    return spec(3, 2, [1, 1, 1], cubics, 0.9, (4, 2, 1), snaps=6,
+                quantities=[(("sphere", 6.0, (X - 1.5, Y / 2, Z / 2)), "PRESSURE", 10.0)])
+
+
+def test_engine_contact_along_x_one_pass(H):
+    """3-D bodies whose contacts all lie along x: the engine copies every
+    contact's ghost planes first (they read the neighbours' E_n, Engine.cpp:99-107)
+    and then runs one gcmx_step per body -- the one-pass kernel, since an
+    x-ghost copy keeps it admissible.  Two bodies == one body and == the
+    oracle, bitwise (ghosts included)."""
+    two = H.Engine(host_task(xcontact(True)))
+    two.run()
+    assert two.last_path(0) == "fused" and two.last_path(1) == "fused"
+    one = H.Engine(host_task(xcontact(False)))
+    one.run()
+    a0, a1, aa = inner(two.pde(0), 2, 3), inner(two.pde(1), 2, 3), inner(one.pde(0), 2, 3)
+    assert np.any(aa != 0)
+    assert np.array_equal(aa[:12], a0) and np.array_equal(aa[12:], a1)
+    oe = O.Engine(oracle_task(xcontact(True)))
+    oe.run()
+    assert oe.steps_done == two.steps
+    assert_bodies_equal(oe, two, xcontact(True))
+
+
 def test_engine_run_statement(H):
     """Engine.runStatement (TestEngine.cpp:91-136): bs 5, Courant 4.5, exact translation."""
     s = spec(2, 5, [7.0 / 19, 3.0 / 39], {0: ([20, 40], [0, 0])}, 4.5, (4, 2, 0.5), snaps=9,
