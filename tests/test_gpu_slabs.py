@@ -246,7 +246,7 @@ def test_loopback_exchange_is_periodic_halo(G, sched):
     if sched != "auto":
         a.set_schedule({"xslab": G.SCHED_XSLAB, "single": G.SCHED_SINGLE}[sched])
     a.comm_init_loopback(64.0, 4)
-    b = _whole(G, X, Y, Z, seed)
+    b = _whole(G, X, Y, Z, seed, path=G.PATH_SPLIT)  # an independent path: per-stage kernels
     for _ in range(steps):
         a.step(0.9)
         b.copy_box([-2, 0, 0], [0, Y, Z], b, [X - 2, 0, 0])
@@ -267,7 +267,7 @@ def test_rccl_single_rank_communicator(G):
     X, Y, Z, seed = 16, 24, 64, 0x5EED
     a = _whole(G, X, Y, Z, seed)
     a.comm_init(gcm_amd.unique_id(), 1, 0, -1, -1)
-    b = _whole(G, X, Y, Z, seed)
+    b = _whole(G, X, Y, Z, seed, path=G.PATH_SPLIT)  # an independent path: per-stage kernels
     for _ in range(2):
         a.step(0.9)
         b.step(0.9)
@@ -295,7 +295,7 @@ def test_rccl_self_exchange(G, sched):
     elif sched != "auto":
         a.set_schedule({"xslab": G.SCHED_XSLAB, "single": G.SCHED_SINGLE}[sched])
     a.comm_init(gcm_amd.unique_id(), 1, 0, 0, 0)
-    b = _whole(G, X, Y, Z, seed)
+    b = _whole(G, X, Y, Z, seed, path=G.PATH_SPLIT)  # an independent path: per-stage kernels
     for _ in range(steps):
         a.step(0.9)
         b.copy_box([-2, 0, 0], [0, Y, Z], b, [0, 0, 0])
