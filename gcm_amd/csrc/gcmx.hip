@@ -1553,31 +1553,35 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 	// send and a receive per halo component and neighbour) runs as SIX kernel
 	// launches: the first beside the interior, the other five after it, on the
 	// next step's critical path.  An explicit NCCL_NCHANNELS_PER_PEER makes it
-	// ONE launch of 2 x channels CTAs, which must find CUs the interior leaves
-	// free: the one-rank self-exchange on MI355X measured
-	// 64-plane slabs (16 CUs free) 0.70 -> 0.62-0.65 ms/step with 6-8 channels,
-	// 128-plane slabs (8 free) 1.17 -> 1.10 ms with 2-4 (1.28-1.30 with 6-8),
-	// 256-plane slabs (4 free) best with RCCL's default (2.46 ms; 4 channels
-	// 2.58).  So: 8 channels with >= 16 free CUs, 4 with >= 8, else RCCL's own.
-	// Both ends of a p2p connection must use the same count, so with several
-	// ranks the choice may depend only on what every rank knows alike: the
-	// rank count (nranks >= 8 -> 8, >= 4 -> 4, else RCCL's own -- the same
-	// choices for the 512^3 decompositions into 8, 4 and 2 even slabs, whose
-	// interiors leave 16, 8 and 4 CUs free); a one-rank communicator (the
-	// self-exchange) applies the free-CU rule to its own slab.  NCCL reads the
-	// variable once per process (the first communicator decides) and never
-	// overrides a value the user set; GCMX_COMM_CHANNELS_PER_PEER forces a
+	// ONE launch, whose CTAs must find CUs the interior leaves free (an interior
+	// block holds a whole CU), else they crawl until interior blocks retire.
+	// The one-rank self-exchange on MI355X ran 2 CTAs per
+	// channel: 64-plane slabs (16 CUs free) 0.70 -> 0.62-0.65 ms/step with 4-8
+	// channels, 128-plane slabs (8 free) 1.17 -> 1.10 with 2-4 (1.28-1.30 with
+	// 6-8), 256-plane slabs (4 free) best with RCCL's default.  A rank with two
+	// distinct peers may need up to twice the CTAs, so the count is sized for
+	// that: free CUs / 4 channels, i.e. 4 with >= 16 free CUs, 2 with >= 8,
+	// else RCCL's own.  Both ends of a p2p connection must use the same count,
+	// so with several ranks the free CUs are taken from the rank count, which
+	// every rank knows alike (the 512^3 decompositions into >= 8 / >= 4 / 2
+	// even slabs leave 16 / 8 / 4 CUs free); a one-rank communicator (the
+	// self-exchange) uses its own slab's interior launch (step_free_cus).  NCCL
+	// reads the variable once per process (the first communicator decides) and
+	// never overrides a value the user set; GCMX_COMM_CHANNELS_PER_PEER forces a
 	// value (0 = RCCL's default) and must then be equal on every rank.
 	if (!std::getenv("NCCL_NCHANNELS_PER_PEER")) {
 		int per_peer = 0;
 		if (const char* e = std::getenv("GCMX_COMM_CHANNELS_PER_PEER")) {
 			per_peer = std::atoi(e);
-		} else if (nranks > 1) {
-			per_peer = nranks >= 8 ? 8 : nranks >= 4 ? 4 : 0;
-		} else if (hipSetDevice(c->device) == hipSuccess) {
-			const int X = c->geo.sizes[0], bs = c->bs;
-			const int free_cus = X > 2 * bs ? step_free_cus(c->geo, bs, X - bs, c->rows_per_block) : -1;
-			per_peer = free_cus >= 16 ? 8 : free_cus >= 8 ? 4 : 0;
+		} else {
+			int free_cus = -1;
+			if (nranks > 1) {
+				free_cus = nranks >= 8 ? 16 : nranks >= 4 ? 8 : 4;
+			} else if (hipSetDevice(c->device) == hipSuccess) {
+				const int X = c->geo.sizes[0], bs = c->bs;
+				free_cus = X > 2 * bs ? step_free_cus(c->geo, bs, X - bs, c->rows_per_block) : -1;
+			}
+			per_peer = free_cus >= 16 ? 4 : free_cus >= 8 ? 2 : 0;
 		}
 		if (per_peer > 0) setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per_peer).c_str(), 0);
 	}

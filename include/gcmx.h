@@ -236,10 +236,10 @@ gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]);
  * Environment read at the first gcmx_comm_init of a process: GCMX_COMM_MIN_CTAS
  * / GCMX_COMM_MAX_CTAS (ncclConfig_t minCTAs / maxCTAs, default 16 / 32) and
  * GCMX_COMM_CHANNELS_PER_PEER (0 = RCCL's default), which sets
- * NCCL_NCHANNELS_PER_PEER unless the user already set it; by default 8 for
- * >= 8 ranks, 4 for >= 4, else RCCL's own (a value every rank derives alike:
+ * NCCL_NCHANNELS_PER_PEER unless the user already set it; by default 4 for
+ * >= 8 ranks, 2 for >= 4, else RCCL's own (a value every rank derives alike:
  * both ends of a p2p connection must agree), and for a one-rank communicator
- * 8 / 4 / RCCL's own when the slab's interior launch leaves >= 16 / >= 8 / fewer
+ * 4 / 2 / RCCL's own when the slab's interior launch leaves >= 16 / >= 8 / fewer
  * CUs free (with RCCL's default the step's exchange group runs as six kernel
  * launches instead of one). */
 gcmx_status gcmx_comm_init(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES],
