@@ -46,6 +46,11 @@ def parse():
                    help="skip the flat-copy measurement reported beside the roofline")
     p.add_argument("--no-profile", action="store_true",
                    help="no hipEvent bracketing of the launches in the timed repetitions")
+    p.add_argument("--prealloc-gb", type=float, default=0.0,
+                   help="measurement only: hold a device buffer of this size (torch) while the "
+                        "layers are allocated (shifts their placement in HBM)")
+    p.add_argument("--no-clock-probe", action="store_true",
+                   help="no co-resident clock-sampling wave during the timed repetitions")
     p.add_argument("--emulate-slabs", type=int, default=0, metavar="K",
                    help="one GPU: split the grid into K X-slab contexts of one in-process group "
                         "(gcmx_comm_init_local: the X-slab step schedule with its overlapped "
@@ -150,6 +155,37 @@ def pmc_traffic(n, ranks, bucket, symbol):
     return k.get("hbm_bytes_per_launch"), f"{rec.get('source')} (same build, sha256 match)"
 
 
+def layer_placement(ctx) -> dict:
+    """Where the two time layers live (gcmx_layer_info): device addresses and
+    their residues modulo the page / fragment sizes that could matter for HBM
+    channel interleaving and translation (4 KiB, 64 KiB, 2 MiB, 1 GiB)."""
+    li = ctx.layer_info()
+    a, b = li["a"], li["b"]
+    mods = {"4K": 1 << 12, "64K": 1 << 16, "2M": 1 << 21, "1G": 1 << 30}
+    return {"a": hex(a), "b": hex(b), "b_minus_a": b - a, "layer_bytes": li["layer_bytes"],
+            "one_allocation": li["one_allocation"],
+            "a_mod": {k: a % m for k, m in mods.items()},
+            "b_mod": {k: b % m for k, m in mods.items()},
+            "b_minus_a_mod": {k: (b - a) % m for k, m in mods.items()}}
+
+
+def clock_summary(samples) -> dict:
+    """Shader clock from the probe's (100 MHz ticks, cycles) samples: per
+    interval Δcycles / Δticks × 100 MHz; median and 10/90 % over the intervals."""
+    import numpy as np
+    if len(samples) < 3:
+        return {"samples": int(len(samples))}
+    s = samples.astype(np.float64)
+    dt = np.diff(s[:, 0])
+    dc = np.diff(s[:, 1])
+    ok = dt > 0
+    mhz = dc[ok] / dt[ok] * 100.0
+    return {"samples": int(len(samples)), "span_ms": round(float((s[-1, 0] - s[0, 0]) / 1e5), 1),
+            "mhz_median": round(float(np.median(mhz)), 1),
+            "mhz_p10": round(float(np.percentile(mhz, 10)), 1),
+            "mhz_p90": round(float(np.percentile(mhz, 90)), 1)}
+
+
 def multi_gpu_parity(dist, world, rank, device, U, U1, L):
     """N > 1 self-check of the RCCL X-slab path (halo exchange overlapped with the
     interior X stage): 3 steps on a 12*N x 40 x 64 grid split into N slabs must
@@ -165,7 +201,7 @@ def multi_gpu_parity(dist, world, rank, device, U, U1, L):
     obj = [gcm_amd.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     c.comm_init(obj[0], world, rank, rank - 1 if rank > 0 else -1,
-                rank + 1 if rank < world - 1 else -1)
+                rank + 1 if rank < world - 1 else -1, global_x=Xg)
     for _ in range(3):
         c.step(0.9)
     mine = c.download().reshape(Xs + 2 * bs, Y + 2 * bs, Z + 2 * bs, 9)[bs:-bs, bs:-bs, bs:-bs]
@@ -311,7 +347,11 @@ def main():
     tau = 0.9 * 1.0 / 1.0  # Courant * h / max|lambda| (Engine.cpp:124-140)
 
     t_setup = time.perf_counter()
+    hold = None
+    if a.prealloc_gb > 0:  # measurement only: shifts the layers' placement
+        hold = torch.empty(int(a.prealloc_gb * (1 << 30)), dtype=torch.uint8, device=f"cuda:{device}")
     ctx = gcm_amd.Context(3, 2, [X, N, N], start=[x0, 0, 0], device=device)
+    placement = layer_placement(ctx)
     ctx.set_materials(U[None], U1[None], L[None])
     ctx.set_path(paths[a.path])
     if a.rows_per_block:
@@ -323,7 +363,7 @@ def main():
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         ctx.comm_init(obj[0], world, rank, rank - 1 if rank > 0 else -1,
-                      rank + 1 if rank < world - 1 else -1)
+                      rank + 1 if rank < world - 1 else -1, global_x=N)
     ctx.sync()
     parity = None
     if world > 1:
@@ -336,9 +376,16 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    tw = time.perf_counter()
     for _ in range(a.warmup):
         ctx.step(tau)
     ctx.sync()
+    warm_ms = (time.perf_counter() - tw) / max(1, a.warmup) * 1e3
+    # one co-resident wave samples the shader clock over the timed repetitions
+    clock = None
+    if not a.no_clock_probe:
+        span = min(20.0, max(0.2, 1.15 * a.reps * a.steps * warm_ms * 1e-3 + 0.05))
+        ctx.clock_probe_start(span, max(50.0, span * 1e6 / 4000))
 
     # K timed steps, repeated `reps` times (median reported).  When profiling,
     # every launch in these same repetitions is bracketed by hipEvents on the
@@ -362,6 +409,8 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = float(tt.item())
         rep_s.append(el)
+    if not a.no_clock_probe:
+        clock = clock_summary(ctx.clock_probe_read())
     kernels = {}
     if not a.no_profile:
         kernels = ctx.profile_read()
@@ -423,6 +472,7 @@ def main():
                                    f"Courant 0.9, tau 0.9, one full time step (3 stages)",
                        "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,
                        "parallelism": f"x-slab{world}" if world > 1 else "single",
+                       **({"rccl_channels_per_peer": ctx.comm_channels_per_peer} if world > 1 else {}),
                        # the one-pass step's floating-point build (gcmx_set_fp_mode): "fma" =
                        # multiply-adds contracted, the product default, held to the north
                        # star's 1e-10 relative L2 of the reference (tests/test_gpu_fma.py);
@@ -435,6 +485,17 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "multi_gpu_parity": parity,
+            # what distinguishes one process's run from another's on the same box
+            # (VERDICT r3 item 1): the layers' placement, the clock under load,
+            # the allocation order
+            "process_state": {"layers": placement, "clock": clock,
+                              "alloc_order": (f"torch buffer {a.prealloc_gb} GiB, " if hold is not None else "")
+                                             + ("layers A+gap+B in one allocation" if placement["one_allocation"]
+                                                else "layer A, layer B, tables"),
+                              "env": {k: os.environ[k] for k in ("GCMX_LAYER_GAP", "GCMX_STREAM_PRIO", "GCMX_FP")
+                                      if k in os.environ},
+                              "under_profiler": bool(os.environ.get("ROCPROF_OUTPUT_PATH") or
+                                                     "rocprof" in os.environ.get("LD_PRELOAD", ""))},
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -41,6 +41,7 @@ struct Geo {
 	long long n_inner;
 	int lead;              // padding in front of the first ghost of a row
 	long long row;         // padded length of the fastest axis
+	int gx0;               // global x index of local plane 0 (CubicGrid::start[0])
 };
 
 // Per (material, axis) table: the matrices plus everything the stage derives

@@ -112,10 +112,18 @@ struct gcmx_ctx {
 	size_t layer_elems = 0;      // M * cs
 	double* cur = nullptr;
 	double* nxt = nullptr;
+	double* layer_a = nullptr;   // the two layers as allocated (cur / nxt swap every step)
+	double* layer_b = nullptr;
+	void* layers_block = nullptr;  // both layers in one allocation (GCMX_LAYER_GAP), else null
+	// clock sampler (gcmx_clock_probe_*): its own stream and sample buffer
+	hipStream_t probe_stream = nullptr;
+	unsigned long long* probe_d = nullptr;
+	int probe_cap = 0;
 	// materials
 	int n_mat = 0;
 	std::vector<double> U, U1, L;  // [mat][D][M*M], [mat][D][M]
 	uint8_t* mat_d = nullptr;      // inner nodes, linear inner order; null = homogeneous
+	int max_mat_id = -1;           // largest id in mat_d (set_materials must cover it)
 	AxisTable* tabs_d = nullptr;   // [mat][D]
 	double tabs_tau = NAN;
 	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso structure)
@@ -134,6 +142,10 @@ struct gcmx_ctx {
 	gcmx_fp_mode fp_mode = GCMX_FP_FMA;  // one-pass step build: contracted (default) or exact
 	// halo exchange
 	ncclComm_t comm = nullptr;
+	bool comm_dead = false;         // the communicator failed and was aborted: every exchange fails
+	bool comm_stall = false;        // tests only (gcmx_comm_test_stall): post sends, never receives
+	double comm_timeout_s = 60.0;   // bound of every host wait on RCCL work
+	int channels_per_peer = -1;     // NCCL_NCHANNELS_PER_PEER in effect (0: RCCL's default)
 	int nranks = 1, rank = 0, left = -1, right = -1;
 	bool halo_pending = false;     // an exchange is in flight on comm_stream (ev_halo)
 	bool halo_fresh = false;       // the current layer's ghost planes hold its neighbours' planes
@@ -346,7 +358,78 @@ void compute_halo_comps(gcmx_ctx* c) {
 	}
 }
 
-bool has_halo(const gcmx_ctx* c) { return (c->comm || c->lc || c->loop) && (c->left >= 0 || c->right >= 0); }
+bool has_halo(const gcmx_ctx* c) {
+	return (c->comm || c->comm_dead || c->lc || c->loop) && (c->left >= 0 || c->right >= 0);
+}
+
+// Bound of host waits on RCCL work: GCMX_COMM_TIMEOUT_SECONDS, default 60.
+double comm_timeout_seconds() {
+	const char* e = std::getenv("GCMX_COMM_TIMEOUT_SECONDS");
+	const double d = e ? std::atof(e) : 0.0;
+	return d > 0 ? d : 60.0;
+}
+
+// The communicator failed: abort it (RCCL's kernels waiting on a peer exit, so
+// the streams drain), keep the context unable to exchange, report GCMX_ERR_COMM.
+gcmx_status comm_fail(gcmx_ctx* c, const std::string& msg) {
+	if (c->comm) (void)ncclCommAbort(c->comm);
+	c->comm = nullptr;
+	c->comm_dead = true;
+	c->halo_pending = false;
+	c->halo_fresh = false;
+	return fail(GCMX_ERR_COMM, msg);
+}
+
+// Non-blocking communicator: wait (bounded) until its last call has completed
+// its host part (ncclCommGetAsyncError leaves ncclInProgress).
+gcmx_status comm_settle(gcmx_ctx* c, const char* what) {
+	const auto t0 = std::chrono::steady_clock::now();
+	for (long it = 0;; it++) {
+		ncclResult_t st = ncclSuccess;
+		const ncclResult_t r = ncclCommGetAsyncError(c->comm, &st);
+		if (r != ncclSuccess) return comm_fail(c, std::string(what) + ": ncclCommGetAsyncError: " + ncclGetErrorString(r));
+		if (st == ncclSuccess) return GCMX_OK;
+		if (st != ncclInProgress) return comm_fail(c, std::string(what) + ": " + ncclGetErrorString(st));
+		const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+		if (el > c->comm_timeout_s)
+			return comm_fail(c, std::string(what) + ": no progress within " + std::to_string(c->comm_timeout_s) +
+			                        " s (a peer missing or dead?); communicator aborted");
+		if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+	}
+}
+
+// Host wait for a stream.  With an RCCL communicator the stream may depend on a
+// peer (the exchange, or a compute stream waiting for it), so the wait polls
+// under the communicator's timeout and its async error; a stalled exchange
+// aborts the communicator (its kernels then exit and the stream drains) and
+// returns GCMX_ERR_COMM instead of hanging.
+gcmx_status wait_stream(gcmx_ctx* c, hipStream_t st, const char* what) {
+	if (!c->comm) {
+		HIP_TRY(hipStreamSynchronize(st));
+		return GCMX_OK;
+	}
+	const auto t0 = std::chrono::steady_clock::now();
+	for (long it = 0;; it++) {
+		const hipError_t q = hipStreamQuery(st);
+		if (q == hipSuccess) return GCMX_OK;
+		if (q != hipErrorNotReady) return fail(GCMX_ERR_HIP, std::string(what) + ": " + hipGetErrorString(q));
+		ncclResult_t as = ncclSuccess;
+		if (ncclCommGetAsyncError(c->comm, &as) == ncclSuccess && as != ncclSuccess && as != ncclInProgress) {
+			gcmx_status s = comm_fail(c, std::string(what) + ": RCCL async error: " + ncclGetErrorString(as));
+			(void)hipStreamSynchronize(st);
+			return s;
+		}
+		const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+		if (el > c->comm_timeout_s) {
+			gcmx_status s = comm_fail(c, std::string(what) + ": the halo exchange did not complete within " +
+			                                 std::to_string(c->comm_timeout_s) +
+			                                 " s (a peer missing or dead?); communicator aborted");
+			(void)hipStreamSynchronize(st);  // the aborted RCCL kernels exit
+			return s;
+		}
+		if (it > 256) std::this_thread::sleep_for(std::chrono::microseconds(100));
+	}
+}
 
 // The current layer changed: its ghost planes no longer hold the neighbours' planes.
 void touch_layer(gcmx_ctx* c) { c->halo_fresh = false; }
@@ -530,6 +613,7 @@ gcmx_status halo_post(gcmx_ctx* c) {
 		return GCMX_OK;
 	}
 	if (c->loop) return loop_post(c);
+	if (c->comm_dead || !c->comm) return fail(GCMX_ERR_COMM, "the communicator failed earlier and was aborted");
 	const Geo& g = c->geo;
 	const size_t n = (size_t)(c->bs * g.stride[0]);
 	const int X = g.sizes[0];
@@ -545,19 +629,24 @@ gcmx_status halo_post(gcmx_ctx* c) {
 		if (r == ncclSuccess && c->left >= 0) {
 			what = "ncclSend/Recv left";
 			r = ncclSend(plane_ptr(c, c->cur, comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream);
-			if (r == ncclSuccess)
+			if ((r == ncclSuccess || r == ncclInProgress) && !c->comm_stall)
 				r = ncclRecv(plane_ptr(c, c->cur, comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream);
 		}
 		if (r == ncclSuccess && c->right >= 0) {
 			what = "ncclSend/Recv right";
 			r = ncclSend(plane_ptr(c, c->cur, comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream);
-			if (r == ncclSuccess)
+			if ((r == ncclSuccess || r == ncclInProgress) && !c->comm_stall)
 				r = ncclRecv(plane_ptr(c, c->cur, comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream);
 		}
 	}
 	const ncclResult_t re = ncclGroupEnd();
-	if (r != ncclSuccess) return fail(GCMX_ERR_COMM, what + ": " + ncclGetErrorString(r));
-	if (re != ncclSuccess) return fail(GCMX_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
+	if (r != ncclSuccess && r != ncclInProgress) return comm_fail(c, what + ": " + ncclGetErrorString(r));
+	if (re != ncclSuccess && re != ncclInProgress)
+		return comm_fail(c, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
+	// non-blocking communicator: the group's kernels are on comm_stream once its
+	// state leaves ncclInProgress; ev_halo must be recorded after them
+	gcmx_status se = comm_settle(c, "halo exchange group");
+	if (se) return se;
 	HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
 	c->halo_pending = true;
 	c->halo_layer = c->cur;
@@ -748,6 +837,7 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 	g.bs = c->bs;
 	const int D = c->D, bs = c->bs;
 	for (int i = 0; i < 3; i++) g.sizes[i] = (i < D) ? d->sizes[i] : 1;
+	g.gx0 = d->start[0];
 	// fastest axis: `lead` unused elements, bs ghosts, inner, bs ghosts, padding
 	const int last = D - 1;
 	g.lead = (int)round_up(bs, kRowAlign) - bs;
@@ -775,16 +865,34 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 	c->layer_elems = (size_t)c->M * (size_t)g.cs;
 
 	const size_t bytes = c->layer_elems * sizeof(double);
-	if (hipMalloc(&c->cur, bytes) != hipSuccess || hipMalloc(&c->nxt, bytes) != hipSuccess ||
-	    hipMalloc(&c->tabs_d, sizeof(AxisTable) * 255 * 3) != hipSuccess) {
+	// Layers: two allocations, or (GCMX_LAYER_GAP = bytes, measurement only) one
+	// allocation holding layer A, `gap` bytes (rounded to 256), then layer B.
+	long long gap = -1;
+	if (const char* e = std::getenv("GCMX_LAYER_GAP")) gap = round_up(std::max(0LL, std::atoll(e)), 256);
+	bool alloc_ok;
+	if (gap >= 0) {
+		alloc_ok = hipMalloc(&c->layers_block, 2 * bytes + (size_t)gap) == hipSuccess;
+		if (alloc_ok) {
+			c->cur = static_cast<double*>(c->layers_block);
+			c->nxt = reinterpret_cast<double*>(static_cast<char*>(c->layers_block) + bytes + (size_t)gap);
+		}
+	} else {
+		alloc_ok = hipMalloc(&c->cur, bytes) == hipSuccess && hipMalloc(&c->nxt, bytes) == hipSuccess;
+	}
+	c->layer_a = c->cur;
+	c->layer_b = c->nxt;
+	if (!alloc_ok || hipMalloc(&c->tabs_d, sizeof(AxisTable) * 255 * 3) != hipSuccess) {
 		gcmx_destroy(c);
 		return fail(GCMX_ERR_OOM, "device allocation failed");
 	}
 	// Main stream at the highest priority, the interior-plane stream at the
 	// lowest: the boundary planes of a slab step (and the halo they feed) are
 	// dispatched ahead of the interior blocks that run beside them.
+	// GCMX_STREAM_PRIO=normal (measurement only) gives every stream the default.
 	int prio_lo = 0, prio_hi = 0;
 	if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+	if (const char* e = std::getenv("GCMX_STREAM_PRIO"))
+		if (std::strcmp(e, "normal") == 0) prio_lo = prio_hi = 0;
 	if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
 	    hipStreamCreateWithPriority(&c->inner_stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
 	    hipStreamCreateWithPriority(&c->bnd_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
@@ -810,20 +918,50 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 void gcmx_destroy(gcmx_ctx* c) {
 	if (!c) return;
 	hipSetDevice(c->device);
+	if (c->comm) {  // bounded: a stalled exchange aborts the communicator
+		if (c->comm_stream) (void)wait_stream(c, c->comm_stream, "gcmx_destroy");
+		if (c->stream && c->comm) (void)wait_stream(c, c->stream, "gcmx_destroy");
+	}
 	if (c->stream) hipStreamSynchronize(c->stream);
 	if (c->comm_stream) hipStreamSynchronize(c->comm_stream);
 	if (c->inner_stream) hipStreamSynchronize(c->inner_stream);
 	if (c->bnd_stream) hipStreamSynchronize(c->bnd_stream);
 	drain_timings(c);
 	for (hipEvent_t ev : c->event_pool) hipEventDestroy(ev);
-	if (c->comm) ncclCommDestroy(c->comm);
+	if (c->probe_stream) hipStreamSynchronize(c->probe_stream);
+	if (c->comm) {  // non-blocking communicator: finalize (bounded), then destroy; abort on failure
+		ncclResult_t r = ncclCommFinalize(c->comm);
+		if (r == ncclSuccess || r == ncclInProgress) {
+			const std::string keep = g_last_error;
+			if (comm_settle(c, "ncclCommFinalize") == GCMX_OK) (void)ncclCommDestroy(c->comm);
+			g_last_error = keep;  // comm_settle aborted it on failure
+		} else {
+			(void)ncclCommAbort(c->comm);
+		}
+		c->comm = nullptr;
+	}
 	if (c->lc) {  // the group cannot exchange without this rank any more
 		local_abort(c, "a context of the group was destroyed");
 		std::lock_guard<std::mutex> lk(c->lc->mu);
-		c->lc->ctx[c->lrank] = nullptr;
+		LocalComm& L = *c->lc;
+		// A neighbour's comm stream may still copy into this rank's ghost planes or
+		// out of its inner planes (pairs (r-1, r) and (r, r+1), either issuer, both
+		// generation slots): wait for those copies before the layers are freed.
+		for (int t = 0; t < 2; t++)
+			for (int sd = 0; sd < 2; sd++)
+				for (int pr = c->lrank - 1; pr <= c->lrank; pr++)
+					if (pr >= 0 && pr < (int)L.done[t][sd].size() && L.done[t][sd][pr])
+						(void)hipEventSynchronize(L.done[t][sd][pr]);
+		L.ctx[c->lrank] = nullptr;
 	}
-	hipFree(c->cur);
-	hipFree(c->nxt);
+	if (c->layers_block) {
+		hipFree(c->layers_block);
+	} else {
+		hipFree(c->layer_a);
+		hipFree(c->layer_b);
+	}
+	hipFree(c->probe_d);
+	if (c->probe_stream) hipStreamDestroy(c->probe_stream);
 	hipFree(c->tabs_d);
 	hipFree(c->mat_d);
 	hipFree(c->nodes_d);
@@ -847,6 +985,10 @@ gcmx_status gcmx_set_materials(gcmx_ctx* c, int n_mat, const double* U, const do
 	if (s) return s;
 	if (n_mat < 1 || n_mat > 255 || !U || !U1 || !L)
 		return fail(GCMX_ERR_INVALID_ARG, "n_mat must be 1..255 with non-null tables");
+	// per-node ids set earlier index these tables (the device tables of the other
+	// entries would be uninitialised)
+	if (c->mat_d && c->max_mat_id >= n_mat)
+		return fail(GCMX_ERR_INVALID_ARG, "material ids set earlier exceed the new material count");
 	const int D = c->D, M = c->M;
 	const size_t nm = (size_t)n_mat * D * M * M, nl = (size_t)n_mat * D * M;
 	for (size_t i = 0; i < nm; i++)
@@ -870,7 +1012,9 @@ gcmx_status gcmx_set_material_ids(gcmx_ctx* c, const uint8_t* ids) {
 	if (!ids) {
 		hipFree(c->mat_d);
 		c->mat_d = nullptr;
+		c->max_mat_id = -1;
 	} else {
+		int mx = 0;
 		const Geo& g = c->geo;
 		std::vector<uint8_t> inner((size_t)g.n_inner);
 		long long i = 0;
@@ -887,9 +1031,11 @@ gcmx_status gcmx_set_material_ids(gcmx_ctx* c, const uint8_t* ids) {
 					if (c->n_mat > 0 && m >= c->n_mat)
 						return fail(GCMX_ERR_INVALID_ARG, "material id out of range");
 					inner[(size_t)i] = m;
+					mx = std::max(mx, (int)m);
 				}
 		if (!c->mat_d) HIP_TRY(hipMalloc(&c->mat_d, inner.size()));
 		HIP_TRY(hipMemcpy(c->mat_d, inner.data(), inner.size(), hipMemcpyHostToDevice));
+		c->max_mat_id = mx;
 	}
 	refresh_fast(c);
 	return GCMX_OK;
@@ -968,7 +1114,7 @@ gcmx_status gcmx_upload(gcmx_ctx* c, const double* aos) {
 		(void)g;
 		if (nz) c->ghosts_touched = true;
 	}
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	if ((s = wait_stream(c, c->stream, "gcmx_upload")) != GCMX_OK) return s;
 	HIP_TRY(hipMemcpy(c->cur, soa.data(), c->layer_elems * sizeof(double), hipMemcpyHostToDevice));
 	touch_layer(c);
 	return GCMX_OK;
@@ -981,7 +1127,7 @@ gcmx_status gcmx_download(gcmx_ctx* c, double* aos) {
 	if (s) return s;
 	if (!aos) return fail(GCMX_ERR_INVALID_ARG, "null host array");
 	std::vector<double> soa(c->layer_elems);
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	if ((s = wait_stream(c, c->stream, "gcmx_download")) != GCMX_OK) return s;
 	HIP_TRY(hipMemcpy(soa.data(), c->cur, c->layer_elems * sizeof(double), hipMemcpyDeviceToHost));
 	soa_to_aos(c, soa.data(), aos);
 	return GCMX_OK;
@@ -1034,7 +1180,14 @@ struct SlabJoin {
 
 // One fused step (k_step_tx2 / k_fused_xyz): the caller checked the path.
 // `fb`: y/z face conditions (x faces already filled in memory), or null.
-gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
+// `final`: the step's result is the new state (no separate ODE pass follows).
+// Only then may the boundary-first / X-slab schedules post the exchange of the
+// new boundary planes inside the step; otherwise the next step's halo_ensure
+// posts it after the ODE pass.  So every rank posts exactly once per step
+// whatever it decides locally (ODE folded or not, one-pass or per-stage path),
+// and the neighbours' posts pair up (a rank posting a second
+// generation after a non-folded ODE mismatched RCCL's send/recv counts).
+gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb, bool final) {
 	gcmx_status s = GCMX_OK;
 	// One pass per step (k_fused_xyz: cur -> nxt, then swap).  Ghost planes of
 	// `cur` must hold E_n; with the X-slab schedule the exchange of the NEW
@@ -1075,7 +1228,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 		}
 		const int brows = brows_env > 0 ? brows_env : 4;
 		ok = xyz("fused_xyz_boundary", 0, bs, c->stream, brows, X - bs, X);
-		if (ok && halo) {
+		if (ok && halo && final) {
 			std::swap(c->cur, c->nxt);  // E_{n+1}: exchange the new boundary planes
 			s = halo_post(c);
 			std::swap(c->cur, c->nxt);
@@ -1111,7 +1264,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 		HIP_TRY(hipEventRecord(c->ev_bnd, c->bnd_stream));
 		HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));
 		join.bnd = false;
-		if (ok && halo) {
+		if (ok && halo && final) {
 			std::swap(c->cur, c->nxt);  // E_{n+1} exchanges the new layer
 			s = halo_post(c);
 			std::swap(c->cur, c->nxt);
@@ -1129,7 +1282,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb) {
 		// so that it pairs with neighbours that run the split (a group of 8-,
 		// 6- and 10-plane slabs otherwise waited forever for a post the thin
 		// slab never made).
-		if (ok && halo && (sched == GCMX_SCHED_BFIRST || sched == GCMX_SCHED_XSLAB)) {
+		if (ok && halo && final && (sched == GCMX_SCHED_BFIRST || sched == GCMX_SCHED_XSLAB)) {
 			std::swap(c->cur, c->nxt);
 			s = halo_post(c);
 			std::swap(c->cur, c->nxt);
@@ -1186,12 +1339,12 @@ gcmx_status step_impl(gcmx_ctx* c, double tau, const StepOde& ode) {
 		FaceBC fb{};
 		fb.ode_on = 1;
 		fb.ode = ode.f[0];
-		s = fused_step(c, &fb);
+		s = fused_step(c, &fb, true);
 		if (s) return s;
 		c->last_ode_fused = true;
 		return GCMX_OK;
 	}
-	s = fused_step(c, nullptr);
+	s = fused_step(c, nullptr, !ode.on);
 	if (s) return s;
 	return ode.on ? ode_apply(c, ode.f) : GCMX_OK;
 }
@@ -1285,7 +1438,7 @@ gcmx_status step_faces_impl(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 			fb.ode_on = 1;
 			fb.ode = ode.f[0];
 		}
-		s = fused_step(c, (fb.on || fold) ? &fb : nullptr);
+		s = fused_step(c, (fb.on || fold) ? &fb : nullptr, !(ode.on && !fold));
 		if (s) return s;
 		c->last_ode_fused = fold;
 		return (ode.on && !fold) ? ode_apply(c, ode.f) : GCMX_OK;
@@ -1524,8 +1677,31 @@ gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]) {
 	return GCMX_OK;
 }
 
-gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], int nranks,
-                           int rank, int left, int right) {
+// Channels per peer the automatic rule picks for an X slab of `X` planes on a
+// grid of Y x Z rows (see gcmx_comm_init_opts).  With RCCL's default, one
+// step's exchange group (a send and a receive per halo component and
+// neighbour) runs as SIX kernel launches: the first beside the interior, the
+// other five after it, on the next step's critical path.  An explicit
+// NCCL_NCHANNELS_PER_PEER makes it ONE launch, whose CTAs must find CUs the
+// interior leaves free (an interior block holds a whole CU), else they crawl
+// until interior blocks retire.  The one-rank self-exchange on MI355X
+//  ran 2 CTAs per channel: 64-plane slabs (16 CUs free) 0.70 ->
+// 0.62-0.65 ms/step with 4-8 channels, 128-plane slabs (8 free) 1.17 -> 1.10
+// with 2-4 (1.28-1.30 with 6-8), 256-plane slabs (4 free) best with RCCL's
+// default.  A rank with two distinct peers may need up to twice the CTAs, so
+// the count is sized for that: free CUs / 4, i.e. 4 with >= 16 free CUs, 2 with
+// >= 8, else RCCL's own (0).
+static int channels_for_slab(const Geo& g0, int X, int rows_per_block) {
+	Geo g = g0;
+	g.sizes[0] = X;
+	g.gx0 = 0;
+	const int bs = g.bs;
+	const int free_cus = X > 2 * bs ? step_free_cus(g, bs, X - bs, rows_per_block) : -1;
+	return free_cus >= 16 ? 4 : free_cus >= 8 ? 2 : 0;
+}
+
+gcmx_status gcmx_comm_init_opts(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], int nranks, int rank,
+                                int left, int right, const gcmx_comm_options* opt) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
 	// A neighbour equal to this rank is accepted only in a one-rank communicator
@@ -1533,72 +1709,80 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 	if (!id || nranks < 1 || rank < 0 || rank >= nranks || left >= nranks || right >= nranks ||
 	    (nranks > 1 && (left == rank || right == rank)))
 		return fail(GCMX_ERR_INVALID_ARG, "bad communicator arguments");
-	if (c->comm || c->lc) return fail(GCMX_ERR_STATE, "communicator already initialised");
+	if (c->comm || c->lc || c->comm_dead) return fail(GCMX_ERR_STATE, "communicator already initialised");
+	gcmx_comm_options o;
+	if (opt) {
+		o = *opt;
+	} else {
+		o.global_x = 0;
+		o.channels_per_peer = -1;
+		o.min_ctas = -1;
+		o.max_ctas = -1;
+		o.timeout_s = 0;
+	}
+	if (o.global_x < 0 || o.channels_per_peer < -1 || o.channels_per_peer > 64)
+		return fail(GCMX_ERR_INVALID_ARG, "bad communicator options");
 	ncclUniqueId u;
 	std::memcpy(&u, id, sizeof(u));
 	// The exchange runs beside the interior kernel, which saturates HBM: a
 	// transfer with few blocks in flight is starved and stops hiding behind it
-	// (loopback measurement), so ask RCCL for at least
-	// GCMX_COMM_MIN_CTAS blocks (default 16; 0 leaves RCCL's own choice), at most
-	// GCMX_COMM_MAX_CTAS (default 32; RCCL rejects a minimum without a maximum).
-	static const int min_ctas = [] {
-		const char* e = std::getenv("GCMX_COMM_MIN_CTAS");
-		return e ? std::atoi(e) : 16;
-	}();
-	static const int max_ctas = [] {
-		const char* e = std::getenv("GCMX_COMM_MAX_CTAS");
-		return e ? std::atoi(e) : 32;
-	}();
-	// Channels per peer.  With RCCL's default, one step's exchange group (a
-	// send and a receive per halo component and neighbour) runs as SIX kernel
-	// launches: the first beside the interior, the other five after it, on the
-	// next step's critical path.  An explicit NCCL_NCHANNELS_PER_PEER makes it
-	// ONE launch, whose CTAs must find CUs the interior leaves free (an interior
-	// block holds a whole CU), else they crawl until interior blocks retire.
-	// The one-rank self-exchange on MI355X ran 2 CTAs per
-	// channel: 64-plane slabs (16 CUs free) 0.70 -> 0.62-0.65 ms/step with 4-8
-	// channels, 128-plane slabs (8 free) 1.17 -> 1.10 with 2-4 (1.28-1.30 with
-	// 6-8), 256-plane slabs (4 free) best with RCCL's default.  A rank with two
-	// distinct peers may need up to twice the CTAs, so the count is sized for
-	// that: free CUs / 4 channels, i.e. 4 with >= 16 free CUs, 2 with >= 8,
-	// else RCCL's own.  Both ends of a p2p connection must use the same count,
-	// so with several ranks the free CUs are taken from the rank count, which
-	// every rank knows alike (the 512^3 decompositions into >= 8 / >= 4 / 2
-	// even slabs leave 16 / 8 / 4 CUs free); a one-rank communicator (the
-	// self-exchange) uses its own slab's interior launch (step_free_cus).  NCCL
-	// reads the variable once per process (the first communicator decides) and
-	// never overrides a value the user set; GCMX_COMM_CHANNELS_PER_PEER forces a
-	// value (0 = RCCL's default) and must then be equal on every rank.
-	if (!std::getenv("NCCL_NCHANNELS_PER_PEER")) {
-		int per_peer = 0;
-		if (const char* e = std::getenv("GCMX_COMM_CHANNELS_PER_PEER")) {
-			per_peer = std::atoi(e);
-		} else {
-			int free_cus = -1;
-			if (nranks > 1) {
-				free_cus = nranks >= 8 ? 16 : nranks >= 4 ? 8 : 4;
-			} else if (hipSetDevice(c->device) == hipSuccess) {
-				const int X = c->geo.sizes[0], bs = c->bs;
-				free_cus = X > 2 * bs ? step_free_cus(c->geo, bs, X - bs, c->rows_per_block) : -1;
-			}
-			per_peer = free_cus >= 16 ? 4 : free_cus >= 8 ? 2 : 0;
-		}
-		if (per_peer > 0) setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per_peer).c_str(), 0);
+	// (loopback measurement), so ask RCCL for at least 16 blocks
+	// (min_ctas; 0 leaves RCCL's own choice), at most 32 (RCCL rejects a minimum
+	// without a maximum).
+	const int min_ctas = o.min_ctas >= 0 ? o.min_ctas : 16;
+	const int max_ctas = o.max_ctas >= 0 ? o.max_ctas : 32;
+	// Channels per peer: both ends of a p2p connection must use the same count,
+	// so the automatic rule uses only inputs every rank holds alike -- the global
+	// X extent, the rank count, Y, Z, borderSize and the library's block rule --
+	// applied to the THINNEST slab of an even split (floor(global_x / nranks)
+	// planes); a one-rank communicator (the self-exchange) uses its own slab.
+	// Without global_x the rule cannot be rank-consistent: RCCL's default.  The
+	// value reaches RCCL through NCCL_NCHANNELS_PER_PEER, which RCCL reads once
+	// per process (the first communicator decides), unless the user set it.
+	int per_peer = o.channels_per_peer;
+	if (per_peer < 0) {
+		if (nranks == 1) per_peer = channels_for_slab(c->geo, c->geo.sizes[0], c->rows_per_block);
+		else if (o.global_x > 0) per_peer = channels_for_slab(c->geo, o.global_x / nranks, c->rows_per_block);
+		else per_peer = 0;
 	}
+	c->channels_per_peer = per_peer;
+	if (per_peer > 0 && !std::getenv("NCCL_NCHANNELS_PER_PEER"))
+		setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per_peer).c_str(), 0);
+	if (const char* e = std::getenv("NCCL_NCHANNELS_PER_PEER")) c->channels_per_peer = std::atoi(e);
+	c->comm_timeout_s = o.timeout_s > 0 ? o.timeout_s : comm_timeout_seconds();
+	// Non-blocking communicator: every RCCL call returns at once and its state is
+	// polled (comm_settle) under the timeout, so a dead or missing peer surfaces
+	// as GCMX_ERR_COMM (after ncclCommAbort) instead of a hang.
 	ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+	cfg.blocking = 0;
 	if (min_ctas > 0) {
 		cfg.minCTAs = min_ctas;
 		cfg.maxCTAs = max_ctas > min_ctas ? max_ctas : min_ctas;
 	}
 	ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, u, rank, &cfg);
-	if (r != ncclSuccess) {
+	if (r != ncclSuccess && r != ncclInProgress) {
+		if (c->comm) (void)ncclCommAbort(c->comm);
 		c->comm = nullptr;
 		return fail(GCMX_ERR_COMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
 	}
+	if ((s = comm_settle(c, "ncclCommInitRankConfig")) != GCMX_OK) return s;
 	c->nranks = nranks;
 	c->rank = rank;
 	c->left = left;
 	c->right = right;
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], int nranks,
+                           int rank, int left, int right) {
+	return gcmx_comm_init_opts(c, id, nranks, rank, left, right, nullptr);
+}
+
+int gcmx_comm_channels_per_peer(const gcmx_ctx* c) { return c ? c->channels_per_peer : -1; }
+
+gcmx_status gcmx_comm_test_stall(gcmx_ctx* c, int on) {
+	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");
+	c->comm_stall = on != 0;
 	return GCMX_OK;
 }
 
@@ -1769,10 +1953,15 @@ gcmx_status gcmx_sync(gcmx_ctx* c) {
 		s = halo_wait(c);
 		if (s) return s;
 	}
-	HIP_TRY(hipStreamSynchronize(c->comm_stream));
-	HIP_TRY(hipStreamSynchronize(c->inner_stream));
-	HIP_TRY(hipStreamSynchronize(c->bnd_stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	// RCCL: bounded waits (wait_stream) -- a peer that never posts fails the
+	// call with GCMX_ERR_COMM instead of hanging it
+	if ((s = wait_stream(c, c->comm_stream, "gcmx_sync")) != GCMX_OK ||
+	    (s = wait_stream(c, c->inner_stream, "gcmx_sync")) != GCMX_OK ||
+	    (s = wait_stream(c, c->bnd_stream, "gcmx_sync")) != GCMX_OK ||
+	    (s = wait_stream(c, c->stream, "gcmx_sync")) != GCMX_OK) {
+		drain_timings(c);
+		return s;
+	}
 	if (c->halo_pending) {  // the comm stream has drained
 		c->halo_pending = false;
 		c->halo_fresh = c->halo_layer == c->cur;
@@ -1877,6 +2066,83 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 	std::sort(ms.begin(), ms.end());
 	*ms_out = ms[ms.size() / 2] * (float)((double)bytes / (double)(2 * half));  // per `bytes`
 	return GCMX_OK;
+}
+
+gcmx_status gcmx_layer_info(gcmx_ctx* c, uint64_t out[4]) {
+	if (!c || !out) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	out[0] = (uint64_t)(uintptr_t)c->layer_a;
+	out[1] = (uint64_t)(uintptr_t)c->layer_b;
+	out[2] = (uint64_t)(c->layer_elems * sizeof(double));
+	out[3] = c->layers_block ? 1 : 0;
+	return GCMX_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// Clock sampler: ONE wave (lane 0 works) that records (s_memrealtime, s_memtime)
+// pairs every `period` ticks of the 100 MHz real-time counter for `span` ticks,
+// sleeping in between.  Launched on its own stream before a timed region, it
+// shares a CU with whatever runs (it holds 64 threads, no LDS, few VGPRs), so
+// Δmemtime / Δrealtime × 100 MHz is the shader clock the chip holds under that
+// load (MI355X_MICROARCH.md §DVFS give-back, item 6).  out[0] = samples taken.
+__global__ __launch_bounds__(64) void k_clock_probe(unsigned long long* __restrict__ out, int cap,
+                                                    unsigned long long period, unsigned long long span) {
+	if (threadIdx.x != 0) return;
+	const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+	unsigned long long next = r0;
+	int n = 0;
+	for (int it = 0; it < (1 << 24) && n < cap; it++) {  // bounded: span ends it first
+		const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+		if (r - r0 > span) break;
+		if (r >= next) {
+			const unsigned long long t = __builtin_amdgcn_s_memtime();
+			out[1 + 2 * n] = r;
+			out[2 + 2 * n] = t;
+			n++;
+			next = r + period;
+		}
+		__builtin_amdgcn_s_sleep(32);
+	}
+	out[0] = (unsigned long long)n;
+}
+}  // namespace
+
+extern "C" {
+
+gcmx_status gcmx_clock_probe_start(gcmx_ctx* c, double seconds, double period_us) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!(seconds > 0 && seconds <= 30) || !(period_us >= 10))
+		return fail(GCMX_ERR_INVALID_ARG, "clock probe: 0 < seconds <= 30, period >= 10 us");
+	const int cap = (int)std::min(65536.0, seconds * 1e6 / period_us + 2);
+	if (!c->probe_stream) HIP_TRY(hipStreamCreateWithFlags(&c->probe_stream, hipStreamNonBlocking));
+	HIP_TRY(hipStreamSynchronize(c->probe_stream));
+	if (cap > c->probe_cap) {
+		hipFree(c->probe_d);
+		c->probe_d = nullptr;
+		c->probe_cap = 0;
+		HIP_TRY(hipMalloc(&c->probe_d, (1 + 2 * (size_t)cap) * sizeof(unsigned long long)));
+		c->probe_cap = cap;
+	}
+	HIP_TRY(hipMemsetAsync(c->probe_d, 0, sizeof(unsigned long long), c->probe_stream));
+	hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, c->probe_stream, c->probe_d, cap,
+	                   (unsigned long long)(period_us * 100.0), (unsigned long long)(seconds * 1e8));
+	HIP_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
+int gcmx_clock_probe_read(gcmx_ctx* c, uint64_t* samples, int cap) {
+	if (!c || !c->probe_stream || !c->probe_d) return -1;
+	if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->probe_stream) != hipSuccess) return -1;
+	unsigned long long n = 0;
+	if (hipMemcpy(&n, c->probe_d, sizeof(n), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+	const int m = (int)std::min<unsigned long long>(n, (unsigned long long)std::max(cap, 0));
+	if (m > 0 && samples &&
+	    hipMemcpy(samples, c->probe_d + 1, 2 * (size_t)m * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
+	        hipSuccess)
+		return -1;
+	return (int)n;
 }
 
 }  // extern "C"

@@ -396,17 +396,26 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 
 	const int z = threadIdx.x;
 	const int Y = g.sizes[1], Z = g.sizes[2];
-	int x, yb, xend;
+	int x, yb, xbeg, xend;
 	{  // XCD-aware chunk-major block order (see k_fused_xyz) over the plane pairs of
-	   // range A [x0, x0 + nplanes), then range B [xb0, xb0 + nplanesb) (may be empty)
-		const int npa = (nplanes + 1) / 2, npair = npa + (nplanesb + 1) / 2;
+	   // range A [x0, x0 + nplanes), then range B [xb0, xb0 + nplanesb) (may be empty).
+	   // Pairs are GLOBAL: (2k, 2k+1) in the global x index g.gx0 + x, so a range
+	   // starting at an odd global plane begins with a pair whose first node is not
+	   // ours.  The two nodes of a pair run different (contracted, in the FMA build)
+	   // operation sequences, so global pairing keeps every node's sequence, and with
+	   // it every bit, independent of how the grid is cut into slabs or bodies.
+		const int pa = (g.gx0 + x0) & 1, pb = (g.gx0 + xb0) & 1;
+		const int npa = (nplanes + pa + 1) / 2;
+		const int npair = npa + (nplanesb > 0 ? (nplanesb + pb + 1) / 2 : 0);
 		const int T = (int)gridDim.x, b = (int)blockIdx.x;
 		const int p = xcd_order(b, T);
 		const int q = p % npair;
-		x = q < npa ? x0 + 2 * q : xb0 + 2 * (q - npa);
+		x = q < npa ? x0 - pa + 2 * q : xb0 - pb + 2 * (q - npa);
+		xbeg = q < npa ? x0 : xb0;
 		xend = q < npa ? x0 + nplanes : xb0 + nplanesb;
 		yb = (p / npair) * chunk;
 	}
+	const bool one = x >= xbeg;  // node x is ours (else only x + 1 is)
 	const bool two = x + 1 < xend;
 	const int ye = min(yb + chunk, Y);
 	const bool live = UNI || z < Z;
@@ -427,7 +436,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #if GCMX_TX2_PROBE_NOX  // timing probe only (wrong results): x-neighbour loads re-read the own planes
 		k = k < BS ? BS : (k > BS + 1 ? BS + 1 : k);
 #endif
-		const int d = (k == WX - 1 && !two) ? 2 * BS : k;
+		// planes outside the valid range (x - BS when x is not ours, x + 1 + BS when
+		// x + 1 is not ours) are read by the discarded node only: clamp them
+		const int d = (k == WX - 1 && !two) ? 2 * BS : (k == 0 && !one) ? 1 : k;
 		return ld_b(src, j, opaque_u32(lv + (pxm + (unsigned)d * stx + (unsigned)r * sty) * 8u));
 	};
 	auto stz = [&](int c, int t, int y, double v) {
@@ -438,7 +449,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const Planes src(in, g.cs);
 	const PlanesW out_p(outl, g.cs);
 	auto ldx = [&](int j, int k, int r) {
-		const int d = (k == WX - 1 && !two) ? BS : k - BS;
+		const int d = (k == WX - 1 && !two) ? BS : (k == 0 && !one) ? 1 - BS : k - BS;
 		return src.ld(j, base + (unsigned)r * sty + (unsigned)d * stx);
 	};
 	auto stz = [&](int c, int t, int y, double v) { out_p.st_nt(c, plane + (unsigned)y * sty + zo + (unsigned)t * stx, v); };
@@ -562,7 +573,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// material of node (x + t, r) (HET; rows outside [0, Y) take row Y-1's: their
 	// X results come from zero ghost rows or are replaced by a face's mirror)
 	auto mat_of = [&](int t, int r) -> unsigned {
-		const int xx = (t == 1 && !two) ? x : x + t;
+		const int xx = (t == 1 && !two) ? x : (t == 0 && !one) ? x + 1 : x + t;
 		const int rr_ = r < Y ? r : Y - 1;
 		return mat[((size_t)xx * Y + rr_) * Z + z];
 	};
@@ -782,7 +793,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll
 			for (int c = 3; c < 9; c++) zv[c] = zv[c] * fb.ode;
 		}
-		if (t == 0 || two) {
+		if (t == 0 ? one : two) {
 #pragma unroll
 			for (int c = 0; c < 9; c++) stz(c, t, y, live ? zv[c] : 0.0);
 		}
@@ -923,7 +934,10 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 	if constexpr (BS <= 2 && ZT <= 512) {
 		if (GCMX_XYZ_TX2 || fb) {
 			const int nb = xb1 > xb0 ? xb1 - xb0 : 0;
-			const int npair = (x1 - x0 + 1) / 2 + (nb + 1) / 2;
+			// global pairs (k_step_tx2): a range starting at an odd global plane
+			// begins with a half pair
+			const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2 +
+			                  (nb > 0 ? (nb + ((g.gx0 + xb0) & 1) + 1) / 2 : 0);
 			// resident blocks: 2 waves per SIMD (<= 256 VGPRs), i.e. 512 / ZT per CU
 			const int chunk = tx2_chunk_for(g.sizes[1], npair, req_chunk, device_cus() * (512 / ZT));
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair);
@@ -1025,7 +1039,7 @@ int step_free_cus(const Geo& g, int x0, int x1, int req_chunk) {
 	if (!fused_supported(g) || g.bs > 2 || Z > 512 || x1 <= x0) return -1;
 	const int ZT = Z <= 64 ? 64 : Z <= 128 ? 128 : Z <= 256 ? 256 : 512;
 	const int per_cu = 512 / ZT, cus = GCMX_XYZ_NS::device_cus();
-	const int npair = (x1 - x0 + 1) / 2;
+	const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2;
 	const int chunk = GCMX_XYZ_NS::tx2_chunk_for(g.sizes[1], npair, req_chunk, cus * per_cu);
 	const long long blocks = (long long)((g.sizes[1] + chunk - 1) / chunk) * npair;
 	const long long slots = (long long)cus * per_cu;

@@ -42,12 +42,14 @@ SYMBOLS = [
     "gcmx_border_nodes_create", "gcmx_border_apply", "gcmx_border_nodes_destroy", "gcmx_step_faces",
     "gcmx_copy_box",
     "gcmx_ode_maxwell", "gcmx_step_ode", "gcmx_last_ode_fused",
-    "gcmx_comm_unique_id", "gcmx_comm_init", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
+    "gcmx_comm_unique_id", "gcmx_comm_init_opts", "gcmx_comm_init", "gcmx_comm_channels_per_peer",
+    "gcmx_comm_test_stall", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_comm_init_local", "gcmx_local_group_steps", "gcmx_comm_init_loopback",
     "gcmx_sync", "gcmx_stream",
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_profile_kernel",
     "gcmx_inner_nodes",
-    "gcmx_all_nodes", "gcmx_device_bytes", "gcmx_copy_ceiling",
+    "gcmx_all_nodes", "gcmx_device_bytes", "gcmx_copy_ceiling", "gcmx_layer_info",
+    "gcmx_clock_probe_start", "gcmx_clock_probe_read",
     "gsx_create", "gsx_destroy", "gsx_set_matrices", "gsx_set_gradient_plan",
     "gsx_set_stage_plan", "gsx_set_border_plan", "gsx_set_border_values",
     "gsx_plain_correction", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
@@ -68,6 +70,12 @@ class Face(ctypes.Structure):
     _fields_ = [("enabled", ctypes.c_int), ("n_quantities", ctypes.c_int),
                 ("quantities", ctypes.c_int * MAX_BORDER_Q),
                 ("values", ctypes.c_double * MAX_BORDER_Q)]
+
+
+class CommOptions(ctypes.Structure):
+    """gcmx_comm_options."""
+    _fields_ = [("global_x", ctypes.c_int), ("channels_per_peer", ctypes.c_int),
+                ("min_ctas", ctypes.c_int), ("max_ctas", ctypes.c_int), ("timeout_s", ctypes.c_double)]
 
 
 class GridDesc(ctypes.Structure):
@@ -129,6 +137,11 @@ def lib() -> ctypes.CDLL:
     L.gcmx_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
     L.gcmx_comm_init.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int]
+    L.gcmx_comm_init_opts.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.POINTER(CommOptions)]
+    L.gcmx_comm_channels_per_peer.argtypes = [vp]
+    L.gcmx_comm_channels_per_peer.restype = ctypes.c_int
+    L.gcmx_comm_test_stall.argtypes = [vp, ctypes.c_int]
     L.gcmx_halo_exchange.argtypes = [vp]
     L.gcmx_halo_exchange_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
     L.gcmx_comm_init_local.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
@@ -152,6 +165,11 @@ def lib() -> ctypes.CDLL:
     L.gcmx_device_bytes.restype = ctypes.c_size_t
     L.gcmx_copy_ceiling.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
     L.gcmx_copy_ceiling.restype = ctypes.c_int
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    L.gcmx_layer_info.argtypes = [vp, u64p]
+    L.gcmx_clock_probe_start.argtypes = [vp, ctypes.c_double, ctypes.c_double]
+    L.gcmx_clock_probe_read.argtypes = [vp, u64p, ctypes.c_int]
+    L.gcmx_clock_probe_read.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -336,9 +354,25 @@ class Context:
         t0 = np.ascontiguousarray(tau0, dtype=np.float64).reshape(-1)
         _check(lib().gcmx_ode_maxwell(self._ptr, tau, _dp(t0), t0.shape[0]))
 
-    def comm_init(self, unique_id: bytes, nranks: int, rank: int, left: int, right: int):
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int, left: int, right: int,
+                  global_x: Optional[int] = None, channels_per_peer: int = -1, timeout_s: float = 0.0):
+        """gcmx_comm_init / gcmx_comm_init_opts (non-blocking RCCL communicator;
+        global_x = the whole grid's X extent, equal on every rank, for the
+        rank-consistent automatic channels-per-peer rule)."""
         buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)(*unique_id)
-        _check(lib().gcmx_comm_init(self._ptr, buf, nranks, rank, left, right))
+        if global_x is None and channels_per_peer == -1 and timeout_s == 0:
+            _check(lib().gcmx_comm_init(self._ptr, buf, nranks, rank, left, right))
+            return
+        o = CommOptions(int(global_x or 0), int(channels_per_peer), -1, -1, float(timeout_s))
+        _check(lib().gcmx_comm_init_opts(self._ptr, buf, nranks, rank, left, right, ctypes.byref(o)))
+
+    @property
+    def comm_channels_per_peer(self) -> int:
+        return lib().gcmx_comm_channels_per_peer(self._ptr)
+
+    def comm_test_stall(self, on: bool = True):
+        """Tests only: exchange groups post sends but never receives."""
+        _check(lib().gcmx_comm_test_stall(self._ptr, 1 if on else 0))
 
     def comm_init_loopback(self, gbps_per_direction: float = 64.0, blocks: int = 8):
         """gcmx_comm_init_loopback: x-periodic self-exchange through the RCCL
@@ -354,6 +388,25 @@ class Context:
         ms = ctypes.c_float(0.0)
         _check(lib().gcmx_copy_ceiling(self._ptr, int(nbytes), int(reps), ctypes.byref(ms)))
         return float(ms.value)
+
+    def layer_info(self) -> dict:
+        """gcmx_layer_info: the two time layers' device addresses (measurement)."""
+        out = (ctypes.c_uint64 * 4)()
+        _check(lib().gcmx_layer_info(self._ptr, out))
+        return {"a": int(out[0]), "b": int(out[1]), "layer_bytes": int(out[2]),
+                "one_allocation": bool(out[3])}
+
+    def clock_probe_start(self, seconds: float, period_us: float = 200.0):
+        """gcmx_clock_probe_start: one co-resident wave samples the shader clock."""
+        _check(lib().gcmx_clock_probe_start(self._ptr, float(seconds), float(period_us)))
+
+    def clock_probe_read(self, cap: int = 65536) -> np.ndarray:
+        """(n, 2) array of (100 MHz ticks, shader cycles) samples."""
+        buf = np.zeros(2 * cap, dtype=np.uint64)
+        n = lib().gcmx_clock_probe_read(self._ptr, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap)
+        if n < 0:
+            raise GcmxError(3, "clock probe read failed")
+        return buf[:2 * min(n, cap)].reshape(-1, 2)
 
     def sync(self):
         _check(lib().gcmx_sync(self._ptr))

@@ -233,17 +233,46 @@ gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]);
  * sends to itself with its receives in posting order, so the left ghost planes
  * receive the slab's first bs inner planes and the right ghost planes its last
  * bs (the RCCL transport exercised on a one-GPU box; not periodic).
- * Environment read at the first gcmx_comm_init of a process: GCMX_COMM_MIN_CTAS
- * / GCMX_COMM_MAX_CTAS (ncclConfig_t minCTAs / maxCTAs, default 16 / 32) and
- * GCMX_COMM_CHANNELS_PER_PEER (0 = RCCL's default), which sets
- * NCCL_NCHANNELS_PER_PEER unless the user already set it; by default 4 for
- * >= 8 ranks, 2 for >= 4, else RCCL's own (a value every rank derives alike:
- * both ends of a p2p connection must agree), and for a one-rank communicator
- * 4 / 2 / RCCL's own when the slab's interior launch leaves >= 16 / >= 8 / fewer
- * CUs free (with RCCL's default the step's exchange group runs as six kernel
- * launches instead of one). */
+ *
+ * The communicator is NON-BLOCKING (ncclConfig_t blocking = 0): every host wait
+ * on RCCL work -- its initialisation, the enqueue of each exchange group,
+ * gcmx_sync / gcmx_download / gcmx_upload / gcmx_destroy on a stream the
+ * exchange feeds -- polls ncclCommGetAsyncError under a timeout; a failure or a
+ * timeout (a peer that never posts, a dead peer) aborts the communicator
+ * (ncclCommAbort: RCCL's waiting kernels exit) and returns GCMX_ERR_COMM, and
+ * every later exchange of the context fails with GCMX_ERR_COMM.  Replaces the
+ * blocking MPI_Sendrecv_replace of the dead MPI design (src/test/TestMPI.cpp:33-50). */
+typedef struct gcmx_comm_options {
+	int    global_x;          /* inner nodes of the WHOLE grid along X, equal on every rank
+	                             (0: unknown)                                              */
+	int    channels_per_peer; /* -1: automatic, 0: RCCL's default, > 0: explicit (must be
+	                             equal on every rank: both ends of a p2p connection use it) */
+	int    min_ctas, max_ctas;/* ncclConfig_t minCTAs / maxCTAs; -1: 16 / 32, 0: RCCL's own */
+	double timeout_s;         /* bound of host waits on RCCL work; <= 0: the environment's
+	                             GCMX_COMM_TIMEOUT_SECONDS, default 60                       */
+} gcmx_comm_options;
+/* Automatic channels per peer: from inputs every rank holds alike (global_x,
+ * nranks, Y, Z, borderSize, the one-pass step's block rule) -- the CUs the
+ * interior launch of the thinnest slab of an even split, floor(global_x /
+ * nranks) planes, leaves free: >= 16 -> 4 channels, >= 8 -> 2, else RCCL's
+ * default; a one-rank communicator uses its own slab; without
+ * global_x, RCCL's default.  The value reaches RCCL as NCCL_NCHANNELS_PER_PEER,
+ * set in the process environment before the communicator is created unless the
+ * user set it (RCCL reads it once per process: the first communicator decides).
+ * opt == NULL: every field automatic / default (global_x unknown). */
+gcmx_status gcmx_comm_init_opts(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES],
+                                int nranks, int rank, int left, int right,
+                                const gcmx_comm_options* opt);
+/* = gcmx_comm_init_opts(..., NULL). */
 gcmx_status gcmx_comm_init(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES],
                            int nranks, int rank, int left, int right);
+/* The channels per peer in effect for this context's communicator (0: RCCL's
+ * default), -1 without one. */
+int         gcmx_comm_channels_per_peer(const gcmx_ctx* ctx);
+/* Tests only: with on != 0 the context's exchange groups post their sends but
+ * never their receives (a peer that never posts), so the exchange cannot
+ * complete: the next bounded wait must return GCMX_ERR_COMM. */
+gcmx_status gcmx_comm_test_stall(gcmx_ctx* ctx, int on);
 /* Fill the X ghost layers of the current layer from the neighbours' boundary
  * inner planes (only the components the X stage reads), on the comm stream.
  * gcmx_step/gcmx_stage(axis 0) on a comm-enabled context call it themselves. */
@@ -461,6 +490,19 @@ size_t      gcmx_device_bytes(gcmx_ctx* ctx);
  * after one warm copy; *ms_out = that copy's duration (HIP events on the
  * ctx stream).  Allocates and frees 2 x bytes / 2 on the context's device. */
 gcmx_status gcmx_copy_ceiling(gcmx_ctx* ctx, size_t bytes, int reps, float* ms_out);
+/* Measurement only: out[0], out[1] = device addresses of the two time layers as
+ * allocated (layer A holds the state after an even number of steps), out[2] =
+ * bytes per layer, out[3] = 1 when both live in one allocation (environment
+ * GCMX_LAYER_GAP = bytes between them at gcmx_create), else 0. */
+gcmx_status gcmx_layer_info(gcmx_ctx* ctx, uint64_t out[4]);
+/* Measurement only: the shader clock under load.  _start launches ONE wave on
+ * a stream of its own that records (s_memrealtime, s_memtime) pairs every
+ * `period_us` for `seconds` (it co-resides with the kernels that run meanwhile);
+ * _read waits for it and copies up to `cap` pairs into samples[2*i], [2*i+1]
+ * (100 MHz ticks, shader cycles); returns the number taken, -1 on error.
+ * Clock over an interval = Δcycles / Δticks × 100 MHz. */
+gcmx_status gcmx_clock_probe_start(gcmx_ctx* ctx, double seconds, double period_us);
+int         gcmx_clock_probe_read(gcmx_ctx* ctx, uint64_t* samples, int cap);
 
 #ifdef __cplusplus
 }

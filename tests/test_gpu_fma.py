@@ -165,15 +165,16 @@ def test_fma_anchor_pressure_sphere(G):
 
 
 @pytest.mark.parametrize("sched", ["bfirst", "xslab", "single"])
-@pytest.mark.parametrize("xs", [[8, 6, 10], [9, 6, 7]])
+@pytest.mark.parametrize("xs", [[8, 6, 10], [9, 6, 7], [7, 5, 9, 3], [5, 8, 3]])
 def test_fma_slab_group_equals_whole_bitwise(G, sched, xs):
     """The multi-GPU schedules in the FMA build (in-process group of X slabs,
     boundary-first / X-slab / one launch) within the tolerance of the oracle,
-    and bitwise equal to the undivided FMA step when every slab starts at an
-    even plane: k_step_tx2 computes x planes in pairs whose two nodes take
-    differently contracted instruction sequences, so a node computes the same
-    bits only in the same pair position (the exact build is bitwise for any
-    split; even slab widths are what bench.py's N > 1 decomposition uses)."""
+    and bitwise equal to the undivided FMA step for ANY split: k_step_tx2
+    computes x planes in pairs whose two nodes take differently contracted
+    instruction sequences, and the pairs are global ((2k, 2k+1) in the global
+    x index), so a slab starting at an odd plane begins with a half pair and
+    every node keeps its pair position (TestEngine.cpp:27-87 / TestMPI.cpp:146-150:
+    split == unsplit, bitwise)."""
     import gcm_amd
     from gcm_amd.host import isotropic_elastic_matrices
     Y, Z, seed = 20, 64, 0x5EED
@@ -200,10 +201,7 @@ def test_fma_slab_group_equals_whole_bitwise(G, sched, xs):
         w.step(0.9)
     inner = lambda c: c.download().reshape(tuple(s + 4 for s in c.sizes) + (9,))[2:-2, 2:-2, 2:-2]
     got = np.concatenate([inner(c) for c in slabs], axis=0)
-    if all(x % 2 == 0 for x in xs):
-        assert np.array_equal(got, inner(w))
-    else:
-        assert rel_l2(got, inner(w)) <= TOL
+    assert np.array_equal(got, inner(w)), rel_l2(got, inner(w))
     b = oracle_body(3, 2, [Xg, Y, Z])
     O.fill_random(b, [Xg, Y, Z], seed)
     for _ in range(steps):
@@ -236,3 +234,103 @@ def test_fma_full_size_512_within_tolerance_of_exact(G):
         c.close()
     r = rel_l2(outs[G.FP_FMA], outs[G.FP_EXACT])
     assert 0 < r <= TOL, r
+
+
+def _xbodies(widths):
+    """3-D bodies stacked along x with the given widths (contacts along the
+    stage-0 axis only: the engine's one-pass path), pressure sphere across them."""
+    from tests.taskspec import spec
+    Y, Z = 20, 64
+    cubics, x0 = {}, 0
+    for i, w in enumerate(widths):
+        cubics[i] = ([w, Y, Z], [x0, 0, 0])
+        x0 += w
+    return spec(3, 2, [1, 1, 1], cubics, 0.9, (4, 2, 1), snaps=6,
+                quantities=[(("sphere", 6.0, (widths[0] - 1.5, Y / 2, Z / 2)), "PRESSURE", 10.0)])
+
+
+@pytest.mark.parametrize("widths", [[12, 12], [7, 5, 12], [9, 8, 7]])
+def test_fma_engine_xbodies_equal_one_body(G, monkeypatch, widths):
+    """The FMA build through the C++ engine (GCMX_FP unset: the product default)
+    with bodies along x of ODD widths, i.e. bodies starting at odd global planes:
+    every body's one-pass step pairs planes globally, so the bodies together are
+    bitwise equal to one body (TestEngine.cpp:27-87's split == unsplit), and
+    within the tolerance of the oracle."""
+    from gcm_amd import _gcm_host as H
+    from tests.taskspec import host_task, oracle_task
+    monkeypatch.setenv("GCMX_FP", "fma")
+    split = H.Engine(host_task(_xbodies(widths)))
+    split.run()
+    assert all(split.last_path(i) == "fused" for i in range(len(widths)))
+    one = H.Engine(host_task(_xbodies([sum(widths)])))
+    one.run()
+    parts = [split.pde(i)[2:-2, 2:-2, 2:-2] for i in range(len(widths))]
+    whole = one.pde(0)[2:-2, 2:-2, 2:-2]
+    got = np.concatenate(parts, axis=0)
+    assert np.any(whole != 0)
+    assert np.array_equal(got, whole), rel_l2(got, whole)
+    oe = O.Engine(oracle_task(_xbodies(widths)))
+    oe.run()
+    want = np.concatenate([b.pde.reshape(split.pde(b.id).shape)[2:-2, 2:-2, 2:-2] for b in oe.bodies], axis=0)
+    assert rel_l2(got, want) <= TOL
+    # the exact build would match the oracle bitwise; the FMA one really ran
+    assert not np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("faces", [False, True])
+def test_fma_step_ode_fused_equals_step_then_ode(G, faces):
+    """gcmx_step_ode in the product default (FMA) build == gcmx_step /
+    gcmx_step_faces then gcmx_ode_maxwell, bitwise (the ODE folded into the
+    stores multiplies the same values the separate pass would), and within the
+    tolerance of the oracle's stages + MaxwellViscosityOde (Ode.hpp:28-37)."""
+    import math
+    q = G.QUANTITY_CODES
+    fc = [[(q["Sxx"], 0.0), (q["Sxy"], 0.0), (q["Sxz"], 0.0)], None,
+          [(q["Syy"], -0.3), (q["Syz"], 0.0)], [(q["Vy"], 0.1)],
+          [(q["Szz"], 0.0), (q["Sxz"], 0.0), (q["Syz"], 0.0)], None] if faces else None
+    b = oracle_body(3, 2, [6, 20, 32])
+    random_state(b, seed=11, ghosts=False)
+    a, c = fma_ctx(G, b), fma_ctx(G, b)
+    f = math.exp(-0.9 / 3.0)
+    for _ in range(3):
+        if faces:
+            a.step_faces(0.9, fc)
+        else:
+            a.step(0.9)
+        a.ode_maxwell(0.9, [3.0])
+        c.step_ode(0.9, [3.0], fc)
+        if not faces:
+            for s in range(3):
+                b.stage(s, 0.9)
+            iv = b.inner_view()
+            iv[..., 3:] = iv[..., 3:] * f
+    assert c.last_ode_fused and c.last_path == "fused"
+    assert np.array_equal(a.download(), c.download())
+    if not faces:
+        check(c, b, "FMA step_ode")
+    a.close(); c.close()
+
+
+@pytest.mark.parametrize("kind", ["rho", "E"])
+def test_fma_engine_two_layers(G, monkeypatch, kind):
+    """Engine.TwoLayersDifferentRho/E (TestEngine.cpp:139-296) through the C++
+    engine in the product default (FMA) build: per-node materials (the HET
+    one-pass step where it applies), within the tolerance of the oracle engine."""
+    from gcm_amd import _gcm_host as H
+    from tests.taskspec import host_task, oracle_task, spec
+    monkeypatch.setenv("GCMX_FP", "fma")
+    rho0, lam0, mu0 = 1, 2, 0.8
+    rho, lam, mu = (0.5, lam0, mu0) if kind == "rho" else (rho0, 0.5 * lam0, 0.5 * mu0)
+    s = spec(3, 2, [1, 1, 1], {0: ([16, 12, 64], [0, 0, 0])}, 0.9, (rho0, lam0, mu0), snaps=6,
+             inhomogeneities=[(("box", (-1, -1, 31.5), (100, 100, 100)), (rho, lam, mu))],
+             quantities=[(("sphere", 5.0, (8, 6, 20)), "PRESSURE", 10.0)])
+    he = H.Engine(host_task(s))
+    he.run()
+    assert he.last_path(0) == "fused"  # k_step_tx2<..., HET>
+    oe = O.Engine(oracle_task(s))
+    oe.run()
+    assert he.steps == oe.steps_done
+    got = he.pde(0)
+    want = oe.bodies[0].pde.reshape(got.shape)
+    r = rel_l2(got, want)
+    assert r <= TOL, r
