@@ -180,13 +180,14 @@ GSX_HD ContactCorrection contactCorrection(const double (&uA)[M], const double* 
 // and not vendored by the reference; this is the classic (pre-2.6) algorithm.
 constexpr int N6 = 6;
 
-GSX_HD void luDecomp6(double (&A)[N6][N6], int (&perm)[N6], int& signum) {
+template <int N>
+GSX_HD void luDecomp(double (&A)[N][N], int (&perm)[N], int& signum) {
 	signum = 1;
-	for (int i = 0; i < N6; i++) perm[i] = i;
-	for (int j = 0; j < N6 - 1; j++) {
+	for (int i = 0; i < N; i++) perm[i] = i;
+	for (int j = 0; j < N - 1; j++) {
 		double mx = std::fabs(A[j][j]);
 		int piv = j;
-		for (int i = j + 1; i < N6; i++) {
+		for (int i = j + 1; i < N; i++) {
 			const double aij = std::fabs(A[i][j]);
 			if (aij > mx) {
 				mx = aij;
@@ -194,7 +195,7 @@ GSX_HD void luDecomp6(double (&A)[N6][N6], int (&perm)[N6], int& signum) {
 			}
 		}
 		if (piv != j) {
-			for (int k = 0; k < N6; k++) {
+			for (int k = 0; k < N; k++) {
 				const double t = A[j][k];
 				A[j][k] = A[piv][k];
 				A[piv][k] = t;
@@ -206,33 +207,47 @@ GSX_HD void luDecomp6(double (&A)[N6][N6], int (&perm)[N6], int& signum) {
 		}
 		const double ajj = A[j][j];
 		if (ajj != 0.0) {
-			for (int i = j + 1; i < N6; i++) {
+			for (int i = j + 1; i < N; i++) {
 				const double aij = A[i][j] / ajj;
 				A[i][j] = aij;
-				for (int k = j + 1; k < N6; k++) A[i][k] = A[i][k] - aij * A[j][k];
+				for (int k = j + 1; k < N; k++) A[i][k] = A[i][k] - aij * A[j][k];
 			}
 		}
 	}
 }
-GSX_HD double luDet6(const double (&LU)[N6][N6], int signum) {
+template <int N>
+GSX_HD double luDet(const double (&LU)[N][N], int signum) {
 	double det = (double)signum;
-	for (int i = 0; i < N6; i++) det *= LU[i][i];
+	for (int i = 0; i < N; i++) det *= LU[i][i];
 	return det;
 }
-GSX_HD void luSolve6(const double (&LU)[N6][N6], const int (&perm)[N6], const double (&b)[N6],
-                     double (&x)[N6]) {
-	for (int i = 0; i < N6; i++) x[i] = b[perm[i]];  // gsl_permute_vector: x'_i = x_{p_i}
-	for (int i = 1; i < N6; i++) {                 // L, unit diagonal
+// gsl_linalg_LU_solve refuses a singular factorisation (a zero on U's
+// diagonal: "matrix is singular", GSL_EDOM); the callers check it first.
+template <int N>
+GSX_HD bool luSingular(const double (&LU)[N][N]) {
+	for (int i = 0; i < N; i++)
+		if (LU[i][i] == 0.0) return true;
+	return false;
+}
+template <int N>
+GSX_HD void luSolve(const double (&LU)[N][N], const int (&perm)[N], const double (&b)[N], double (&x)[N]) {
+	for (int i = 0; i < N; i++) x[i] = b[perm[i]];  // gsl_permute_vector: x'_i = x_{p_i}
+	for (int i = 1; i < N; i++) {                // L, unit diagonal
 		double t = x[i];
 		for (int j = 0; j < i; j++) t -= LU[i][j] * x[j];
 		x[i] = t;
 	}
-	x[N6 - 1] = x[N6 - 1] / LU[N6 - 1][N6 - 1];  // U
-	for (int i = N6 - 2; i >= 0; i--) {
+	x[N - 1] = x[N - 1] / LU[N - 1][N - 1];  // U
+	for (int i = N - 2; i >= 0; i--) {
 		double t = x[i];
-		for (int j = i + 1; j < N6; j++) t -= LU[i][j] * x[j];
+		for (int j = i + 1; j < N; j++) t -= LU[i][j] * x[j];
 		x[i] = t / LU[i][i];
 	}
+}
+GSX_HD void luDecomp6(double (&A)[N6][N6], int (&perm)[N6], int& signum) { luDecomp<N6>(A, perm, signum); }
+GSX_HD double luDet6(const double (&LU)[N6][N6], int signum) { return luDet<N6>(LU, signum); }
+GSX_HD void luSolve6(const double (&LU)[N6][N6], const int (&perm)[N6], const double (&b)[N6], double (&x)[N6]) {
+	luSolve<N6>(LU, perm, b, x);
 }
 
 /// The contact node that is a border with two conditions (ContactCorrector.hpp:

@@ -123,6 +123,7 @@ struct gsx_ctx {
 	int* ready = nullptr;
 	int epoch = 0;
 	unsigned gTarget = 0;
+	unsigned tickets = 0;  // work tickets k_sx_stage_l8 launches have handed out (device counter ready[N + 2])
 	int fuseMode = 1;  // gsx_set_stage_fusion: 0 never, 1 border + inner, 2 gradient + border + inner,
 	                   // 3 border + inner without the grid-size cap (tuning)
 	bool lastFused = false;  // the last gsx_stage ran as one launch
@@ -748,6 +749,8 @@ struct StageWait {
 	int epoch;
 	int* err;
 	int budget;         // polls before a wait gives up (gsx_set_wait_budget; < 0: every wait reports a timeout)
+	unsigned* ticket;   // work tickets handed out, monotonic (k_sx_stage_l8)
+	unsigned tbase;     // *ticket when this launch started
 };
 // Hand-offs inside k_sx_stage_l8 (cdna_hip_programming.md Guideline 16, the
 // write-through form): every handed-off byte (gradients, wn) is stored sc1 by its
@@ -816,6 +819,26 @@ __device__ __forceinline__ double grad_dot(const double* __restrict__ grad, int 
 	return dot;
 }
 
+// TetrahedronInterpolator::hybridInterpolate (TetrahedronInterpolator.hpp:93-104)
+// of a CELL foot: v = the four vertices' values, dots = each vertex's gradient
+// times (q - c_i) (grad_dot's order), lam = q's barycentrics (the host plan's,
+// linal::barycentricCoordinates).  The quadratic form (hpp:47-58), the min-max
+// limiter of the four values (linal::limiterMinMax), and the linear form (hpp:
+// 27-37) when the limiter changed the quadratic value.
+__device__ __forceinline__ double tet_linear(const double (&v)[4], const double (&lam)[4]) {
+	return lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
+}
+__device__ __forceinline__ double tet_hybrid(const double (&v)[4], const double (&dots)[4], const double (&lam)[4]) {
+	double term[4];
+#pragma unroll
+	for (int i = 0; i < 4; i++) term[i] = v[i] + dots[i] / 2.0;
+	const double quadratic = lam[0] * term[0] + lam[1] * term[1] + lam[2] * term[2] + lam[3] * term[3];
+	const double mn = std_min(std_min(std_min(v[0], v[1]), v[2]), v[3]);
+	const double mx = std_max(std_max(std_max(v[0], v[1]), v[2]), v[3]);
+	const double limited = std_min(std_max(quadratic, mn), mx);
+	return (quadratic == limited) ? quadratic : tet_linear(v, lam);
+}
+
 // interpolateValuesAround for one invariant k (0..5) of node n (node_invariants' body).
 // WAIT: the foot's new-invariant reads wait for the border nodes' flags first.
 template <bool WAIT = false>
@@ -844,7 +867,7 @@ __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const
 	const double lam[4] = {l.x, l.y, l.z, l.w};
 	const double q0 = coords[3 * (size_t)n + 0] + s0, q1 = coords[3 * (size_t)n + 1] + s1,
 	             q2 = coords[3 * (size_t)n + 2] + s2;
-	double v[4], term[4], dots[4], dd[4][3];
+	double v[4], dots[4], dd[4][3];
 	bool waits[4];
 	const double* wsrc[4];
 	int wnode[4];
@@ -882,17 +905,9 @@ __device__ __forceinline__ double foot_value(int n, int k, int pos, int P, const
 				v[i] = read_ready(wsrc[i]);
 			}
 	}
-#pragma unroll
-	for (int i = 0; i < 4; i++) term[i] = v[i] + dots[i] / 2.0;
-	if (kind == GSX_FOOT_CELL) {
-		const double quadratic = lam[0] * term[0] + lam[1] * term[1] + lam[2] * term[2] + lam[3] * term[3];
-		const double mn = std_min(std_min(std_min(v[0], v[1]), v[2]), v[3]);
-		const double mx = std_max(std_max(std_max(v[0], v[1]), v[2]), v[3]);
-		const double limited = std_min(std_max(quadratic, mn), mx);
-		return (quadratic == limited) ? quadratic
-		                              : lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
-	}
-	if (kind == GSX_FOOT_SPACETIME) return lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3];
+	if (kind == GSX_FOOT_CELL) return tet_hybrid(v, dots, lam);
+	// interpolateInSpaceTime (common.hpp:102-129): interpolateInOwner's linear form
+	if (kind == GSX_FOOT_SPACETIME) return tet_linear(v, lam);
 	return 0.0;
 }
 
@@ -1266,10 +1281,13 @@ __global__ __launch_bounds__(256) void k_sx_border_l8(
 // stage first) waits for exactly those nodes' flags.  Every wait is on blocks
 // with LOWER ids: inner groups wait on border and gradient blocks, border groups
 // (their CELL feet, mode 2) only on gradient blocks, gradient blocks never wait.
-// ASSUMPTION (how the hardware dispatches, not a HIP guarantee): workgroups of
-// one launch are dispatched in id order on each XCD, so every block a waiting
-// block depends on is resident or finished.  The launch is capped at
-// kFuseMaxBlocks (4096) blocks, and every wait is bounded (StageWait::budget).
+// No dispatch-order assumption: a block's work index is not blockIdx.x but a
+// TICKET it takes from a per-context counter when it starts (one atomic per
+// block).  Tickets are handed out in the order blocks start running, so the
+// lower-index work a block waits for belongs to blocks that already started --
+// resident or finished -- whatever order the hardware dispatches workgroups in,
+// and every wait can end.  Every wait stays bounded (StageWait::budget) as a
+// backstop; the grid is capped at kFuseMaxBlocks (4096) blocks for speed only.
 __global__ __launch_bounds__(256) void k_sx_stage_l8(
     const int* __restrict__ border, int nBorder, const int* __restrict__ inner, int nInner, int nbBlk,
     const int4* __restrict__ fv, const double4* __restrict__ flam, const int* __restrict__ fmeta, StageShift sh,
@@ -1280,7 +1298,10 @@ __global__ __launch_bounds__(256) void k_sx_stage_l8(
     double* __restrict__ gradw, const int* __restrict__ gOff, const int* __restrict__ gNb,
     const double* __restrict__ gW, const double* __restrict__ gM, const double* __restrict__ gDet) {
 	const int P = nBorder + nInner;
-	const int b = blockIdx.x;
+	__shared__ unsigned ticket;
+	if (threadIdx.x == 0) ticket = __hip_atomic_fetch_add(sw.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	__syncthreads();
+	const int b = (int)(ticket - sw.tbase);  // work index, in start order
 	if (b < ngBlk)
 		gradient_l8<true>(b * blockDim.x + threadIdx.x, w, gradw, gOff, gNb, coords, gW, gM, gDet, N, sw.gcount);
 	else if (b < ngBlk + nbBlk)
@@ -1559,8 +1580,10 @@ gcmx_status gsx_create(int device, int n_nodes, const double* coords, gsx_ctx** 
 		gsx_destroy(c);
 		return fail(GCMX_ERR_OOM, "simplex border-value allocation failed");
 	}
-	if (hipMalloc(&c->ready, (N + 2) * sizeof(int)) != hipSuccess ||
-	    hipMemset(c->ready, 0, (N + 2) * sizeof(int)) != hipSuccess) {
+	// [0, N) border flags, [N] finished-gradient-block counter, [N + 1] error word,
+	// [N + 2] work-ticket counter of k_sx_stage_l8
+	if (hipMalloc(&c->ready, (N + 3) * sizeof(int)) != hipSuccess ||
+	    hipMemset(c->ready, 0, (N + 3) * sizeof(int)) != hipSuccess) {
 		gsx_destroy(c);
 		return fail(GCMX_ERR_OOM, "simplex flag allocation failed");
 	}
@@ -1969,8 +1992,10 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 		const int ngBlk = withGrad ? (int)(((size_t)N * kL + kL8Block - 1) / kL8Block) : 0;
 		// the counter wraps like the target; both advance only with a launched grid
 		const unsigned target = c->gTarget + (unsigned)ngBlk;
-		const StageWait sw{c->ready, withGrad ? reinterpret_cast<unsigned*>(c->ready + N) : nullptr, target,
-		                   c->epoch + 1, c->ready + N + 1, c->waitBudget};
+		const StageWait sw{c->ready,      withGrad ? reinterpret_cast<unsigned*>(c->ready + N) : nullptr,
+		                   target,        c->epoch + 1,
+		                   c->ready + N + 1, c->waitBudget,
+		                   reinterpret_cast<unsigned*>(c->ready + N + 2), c->tickets};
 		if (!withGrad)
 			hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
 			                   c->stream, c->w, c->grad, c->gOff, c->gNb, c->coords, c->gW, c->gM, c->gDet, N);
@@ -1983,6 +2008,7 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 		                   c->grad, c->gOff, c->gNb, c->gW, c->gM, c->gDet);
 		SX_TRY(hipGetLastError());
 		c->gTarget = target;
+		c->tickets += (unsigned)(ngBlk + nbBlk + niBlk);
 		c->epoch++;
 		*fused = true;
 		return GCMX_OK;
@@ -2326,3 +2352,58 @@ gcmx_status gsx_set_wait_budget(gsx_ctx* c, int polls) {
 }
 
 }  // extern "C"
+
+// ---- tests only: the device interpolation functions on given inputs -----------
+namespace {
+// Per case i: out[2i] = tet_hybrid (a CELL foot), out[2i + 1] = tet_linear (a
+// SPACETIME foot / interpolateInOwner's value), with the gradient terms formed
+// exactly as grad_dot forms them from q - c_j.
+__global__ __launch_bounds__(64) void k_sx_test_interp(int n, const double* __restrict__ v,
+                                                      const double* __restrict__ g, const double* __restrict__ c,
+                                                      const double* __restrict__ q, const double* __restrict__ lam,
+                                                      double* __restrict__ out) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	double vv[4], dots[4], l[4];
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		vv[j] = v[4 * i + j];
+		l[j] = lam[4 * i + j];
+		double d[3];
+#pragma unroll
+		for (int r = 0; r < 3; r++) d[r] = q[3 * i + r] - c[(4 * i + j) * 3 + r];
+		const double* gj = g + (4 * i + j) * 3;
+		double dot = gj[0] * d[0];
+		dot += gj[1] * d[1];
+		dot += gj[2] * d[2];
+		dots[j] = dot;
+	}
+	out[2 * i] = tet_hybrid(vv, dots, l);
+	out[2 * i + 1] = tet_linear(vv, l);
+}
+}  // namespace
+
+extern "C" gcmx_status gsx_test_interpolate(int device, int n, const double* v, const double* g, const double* c,
+                                            const double* q, const double* lam, double* out) {
+	if (n < 1 || n > (1 << 20) || !v || !g || !c || !q || !lam || !out)
+		return fail(GCMX_ERR_INVALID_ARG, "gsx_test_interpolate: bad arguments");
+	SX_TRY(hipSetDevice(device));
+	const size_t sz[6] = {4 * (size_t)n, 12 * (size_t)n, 12 * (size_t)n, 3 * (size_t)n, 4 * (size_t)n, 2 * (size_t)n};
+	const double* src[5] = {v, g, c, q, lam};
+	double* d[6] = {};
+	gcmx_status st = GCMX_OK;
+	for (int k = 0; k < 6 && st == GCMX_OK; k++) {
+		if (hipMalloc(&d[k], sz[k] * sizeof(double)) != hipSuccess) st = fail(GCMX_ERR_OOM, "gsx_test_interpolate");
+		else if (k < 5 && hipMemcpy(d[k], src[k], sz[k] * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+			st = fail(GCMX_ERR_HIP, "gsx_test_interpolate: upload");
+	}
+	if (st == GCMX_OK) {
+		hipLaunchKernelGGL(k_sx_test_interp, dim3((n + 63) / 64), dim3(64), 0, 0, n, d[0], d[1], d[2], d[3], d[4], d[5]);
+		if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+		    hipMemcpy(out, d[5], sz[5] * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+			st = fail(GCMX_ERR_HIP, "gsx_test_interpolate: kernel");
+	}
+	for (double* p : d)
+		if (p) (void)hipFree(p);
+	return st;
+}

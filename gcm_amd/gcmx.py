@@ -56,6 +56,7 @@ SYMBOLS = [
     "gsx_stage_nodes", "gsx_stage_finish", "gsx_contact_create", "gsx_contact_destroy",
     "gsx_contact_plain", "gsx_contact_correct", "gsx_step", "gsx_set_node_lanes",
     "gsx_set_stage_fusion", "gsx_last_stage_fused", "gsx_stage_plan_info", "gsx_set_wait_budget",
+    "gsx_test_interpolate",
 ]
 
 
@@ -165,6 +166,7 @@ def lib() -> ctypes.CDLL:
     L.gcmx_device_bytes.restype = ctypes.c_size_t
     L.gcmx_copy_ceiling.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
     L.gcmx_copy_ceiling.restype = ctypes.c_int
+    L.gsx_test_interpolate.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, dp]
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.gcmx_layer_info.argtypes = [vp, u64p]
     L.gcmx_clock_probe_start.argtypes = [vp, ctypes.c_double, ctypes.c_double]
@@ -486,6 +488,20 @@ def local_group_steps(slabs: Sequence["Context"], tau: float, steps: int):
     thread per context, then gcmx_sync (gcmx_local_group_steps)."""
     arr = (ctypes.c_void_p * len(slabs))(*[c.ptr.value for c in slabs])
     _check(lib().gcmx_local_group_steps(arr, len(slabs), float(tau), int(steps)))
+
+
+def test_interpolate(v, g, c, q, lam, device: int = 0):
+    """gsx_test_interpolate (tests only): the simplex kernels' device interpolation
+    on given cases; returns (hybrid, linear) arrays."""
+    v = np.ascontiguousarray(v, dtype=np.float64).reshape(-1, 4)
+    n = v.shape[0]
+    g = np.ascontiguousarray(g, dtype=np.float64).reshape(n, 4, 3)
+    c = np.ascontiguousarray(c, dtype=np.float64).reshape(n, 4, 3)
+    q = np.ascontiguousarray(q, dtype=np.float64).reshape(n, 3)
+    lam = np.ascontiguousarray(lam, dtype=np.float64).reshape(n, 4)
+    out = np.zeros((n, 2), dtype=np.float64)
+    _check(lib().gsx_test_interpolate(device, n, _dp(v), _dp(g), _dp(c), _dp(q), _dp(lam), _dp(out)))
+    return out[:, 0].copy(), out[:, 1].copy()
 
 
 def unique_id() -> bytes:

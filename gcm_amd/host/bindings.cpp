@@ -5,8 +5,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <type_traits>
+
 #include "engine.hpp"
 #include "simplex.hpp"
+#include "../csrc/contact.hpp"
 
 namespace py = pybind11;
 using namespace gcm;
@@ -487,6 +490,68 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    },
 	    "The task's whole triangulation: (points, cells (0-based), grid id per cell, -1 = empty)",
 	    py::arg("task"));
+
+	m.def(
+	    "tet_barycentric",
+	    [](const Real3& a, const Real3& b, const Real3& c, const Real3& d, const Real3& q) {
+		    return simplex::barycentricCoordinates(a, b, c, d, q);
+	    },
+	    "linal::barycentricCoordinates of a tetrahedron (the stage plans' CELL-foot weights)");
+
+	m.def(
+	    "tet_owner_pick",
+	    [](const std::array<Real3, 6>& pts, const Real3& q) {
+		    Real3 p6[6];
+		    for (int i = 0; i < 6; i++) p6[i] = pts[i];
+		    int slot[4];
+		    real lam[4];
+		    simplex::interpolateInOwnerPick(p6, q, slot, lam);
+		    return py::make_tuple(std::array<int, 4>{slot[0], slot[1], slot[2], slot[3]},
+		                          std::array<real, 4>{lam[0], lam[1], lam[2], lam[3]});
+	    },
+	    "TetrahedronInterpolator::interpolateInOwner's choice as the stage plans make it: "
+	    "(point indices, barycentrics); raises when no tetrahedron holds q",
+	    py::arg("points"), py::arg("q"));
+
+	m.def(
+	    "gsl_lu",
+	    [](py::array_t<double, py::array::c_style | py::array::forcecast> A, py::object b) {
+		    // csrc/contact.hpp's restatement of gsl_linalg_LU_decomp / _det / _solve
+		    // (GslUtils.hpp:96-168), the code the contact-corrector kernels run
+		    if (A.ndim() != 2 || A.shape(0) != A.shape(1)) throw Exception("square matrix expected");
+		    const int n = (int)A.shape(0);
+		    auto run = [&](auto NC) -> py::object {
+			    constexpr int N = decltype(NC)::value;
+			    double LU[N][N], bb[N], x[N];
+			    int perm[N], signum;
+			    for (int i = 0; i < N; i++)
+				    for (int j = 0; j < N; j++) LU[i][j] = A.at(i, j);
+			    gsx::luDecomp<N>(LU, perm, signum);
+			    const double det = gsx::luDet<N>(LU, signum);
+			    if (b.is_none()) return py::float_(det);
+			    auto bv = b.cast<std::vector<double>>();
+			    if ((int)bv.size() != N) throw Exception("right-hand side of the wrong size");
+			    // gsl_linalg_LU_solve: "matrix is singular" (solveLinearSystem throws)
+			    if (gsx::luSingular<N>(LU)) throw Exception("gsl_linalg_LU_solve: matrix is singular");
+			    for (int i = 0; i < N; i++) bb[i] = bv[i];
+			    gsx::luSolve<N>(LU, perm, bb, x);
+			    return py::cast(std::vector<double>(x, x + N));
+		    };
+		    switch (n) {
+		    case 1: return run(std::integral_constant<int, 1>{});
+		    case 2: return run(std::integral_constant<int, 2>{});
+		    case 3: return run(std::integral_constant<int, 3>{});
+		    case 4: return run(std::integral_constant<int, 4>{});
+		    case 5: return run(std::integral_constant<int, 5>{});
+		    case 6: return run(std::integral_constant<int, 6>{});
+		    case 7: return run(std::integral_constant<int, 7>{});
+		    case 8: return run(std::integral_constant<int, 8>{});
+		    case 9: return run(std::integral_constant<int, 9>{});
+		    default: throw Exception("1..9 rows supported");
+		    }
+	    },
+	    "determinant (b None) or solution of A x = b through csrc/contact.hpp's GSL LU restatement",
+	    py::arg("A"), py::arg("b") = py::none());
 
 	m.def("simplex_plans", &simplexPlans,
 	      "GPU-free simplex set-up: mesh, time step, gradient and stage plans", py::arg("task"));

@@ -758,6 +758,33 @@ GradientPlan buildGradientPlan(const Grid& grid) {
 	return g;
 }
 
+std::array<real, 4> barycentricCoordinates(const Real3& a, const Real3& b, const Real3& c, const Real3& d,
+                                           const Real3& q) {
+	return barycentric(a, b, c, d, q);
+}
+
+void interpolateInOwnerPick(const Real3 (&pts)[6], const Real3& q, int (&slot)[4], real (&lam)[4]) {
+	// TetrahedronInterpolator::interpolateInOwner (hpp:113-155): the 15 tetrahedra
+	// in the reference's TRY_TETRAHEDRON order, the first non-degenerate one whose
+	// barycentrics pass isInterpolation (hpp:15-20)
+	static const int tries[15][4] = {{0, 1, 2, 3}, {0, 1, 2, 4}, {0, 1, 2, 5}, {0, 1, 3, 4}, {0, 1, 3, 5},
+	                                 {0, 1, 4, 5}, {0, 2, 3, 4}, {0, 2, 3, 5}, {0, 2, 4, 5}, {0, 3, 4, 5},
+	                                 {1, 2, 3, 4}, {1, 2, 3, 5}, {1, 2, 4, 5}, {1, 3, 4, 5}, {2, 3, 4, 5}};
+	for (const auto& tr : tries) {
+		if (volume(pts[tr[0]], pts[tr[1]], pts[tr[2]], pts[tr[3]]) == 0) continue;
+		const auto l = barycentric(pts[tr[0]], pts[tr[1]], pts[tr[2]], pts[tr[3]], q);
+		if (l[0] > -EQUALITY_TOLERANCE && l[1] > -EQUALITY_TOLERANCE && l[2] > -EQUALITY_TOLERANCE &&
+		    l[3] > -EQUALITY_TOLERANCE) {
+			for (int i = 0; i < 4; i++) {
+				slot[i] = tr[i];
+				lam[i] = l[i];
+			}
+			return;
+		}
+	}
+	throw Exception("Containing tetrahedron is not found");  // THROW_INVALID_ARG, hpp:153
+}
+
 StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[9], real tau) {
 	const auto& m = grid.mesh;
 	const int nv = m.nVertices();
@@ -800,26 +827,9 @@ StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[
 				const auto w = lls32(sub(r2, r1), sub(r3, r1), sub(rc, r1));
 				const Real3 pts[6] = {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {0, 1, 1}};
 				const Real3 qst = {w[0], w[1], 1 - length(sub(rc, r0)) / length(shift)};
-				// TetrahedronInterpolator::interpolateInOwner (hpp:113-155)
-				static const int tries[15][4] = {{0, 1, 2, 3}, {0, 1, 2, 4}, {0, 1, 2, 5}, {0, 1, 3, 4},
-				                                 {0, 1, 3, 5}, {0, 1, 4, 5}, {0, 2, 3, 4}, {0, 2, 3, 5},
-				                                 {0, 2, 4, 5}, {0, 3, 4, 5}, {1, 2, 3, 4}, {1, 2, 3, 5},
-				                                 {1, 2, 4, 5}, {1, 3, 4, 5}, {2, 3, 4, 5}};
-				bool ok = false;
-				for (const auto& tr : tries) {
-					if (volume(pts[tr[0]], pts[tr[1]], pts[tr[2]], pts[tr[3]]) == 0) continue;
-					const auto lam = barycentric(pts[tr[0]], pts[tr[1]], pts[tr[2]], pts[tr[3]], qst);
-					if (lam[0] > -EQUALITY_TOLERANCE && lam[1] > -EQUALITY_TOLERANCE &&
-					    lam[2] > -EQUALITY_TOLERANCE && lam[3] > -EQUALITY_TOLERANCE) {
-						for (int i = 0; i < 4; i++) {
-							f.slot[i] = tr[i];
-							f.lam[i] = lam[i];
-						}
-						ok = true;
-						break;
-					}
-				}
-				if (!ok) throw Exception("Containing tetrahedron is not found");
+				real lam[4];
+				interpolateInOwnerPick(pts, qst, f.slot, lam);  // throws when none contains qst
+				for (int i = 0; i < 4; i++) f.lam[i] = lam[i];
 				f.kind = GSX_FOOT_SPACETIME;
 				for (int i = 0; i < 3; i++) f.v[i] = t.v[i];
 			} else if (t.n == 2) {

@@ -177,6 +177,16 @@ GradientPlan buildGradientPlan(const Grid& grid);
 /// bookkeeping of contactAndBorderStage (:57-95).
 StagePlan buildStagePlan(const Grid& grid, const Real3& direction, const real L[9], real tau);
 
+/// linal::barycentricCoordinates of a tetrahedron (linal/geometry.hpp:142-151).
+std::array<real, 4> barycentricCoordinates(const Real3& a, const Real3& b, const Real3& c, const Real3& d,
+                                           const Real3& q);
+/// TetrahedronInterpolator::interpolateInOwner's choice (util/math/interpolation/
+/// TetrahedronInterpolator.hpp:113-155): the tetrahedron of the six points that
+/// holds q (its point indices) and q's barycentrics in it; throws when none does.
+/// The stage plan's space-time feet use it; the interpolated value is then
+/// lam[0] v[slot[0]] + ... + lam[3] v[slot[3]] (on the device).
+void interpolateInOwnerPick(const Real3 (&pts)[6], const Real3& q, int (&slot)[4], real (&lam)[4]);
+
 /// ElasticModel::borderMatrixFixedForce / borderMatrixFixedVelocity
 /// (rheology/models/ElasticModel.hpp:111-154), 3 x 9 row-major.
 std::array<real, 27> borderMatrix(BorderConditions::T type, const Real3& normal);

@@ -460,6 +460,14 @@ gcmx_status gsx_contact_correct(gsx_contact* c, int stage);
 gcmx_status gsx_step(gsx_ctx* const* bodies, int n_bodies, gsx_contact* const* contacts,
                      int n_contacts);
 gcmx_status gsx_sync(gsx_ctx* ctx);
+/* Tests only: the device interpolation the simplex stage kernels run, on given
+ * inputs.  Case i: v[4i..], g[(4i+j)*3..] (vertex j's gradient), c[(4i+j)*3..]
+ * (vertex j), q[3i..], lam[4i..] (q's barycentrics, as the host plan computes
+ * them); out[2i] = TetrahedronInterpolator::hybridInterpolate
+ * (TetrahedronInterpolator.hpp:93-104, a CELL foot), out[2i+1] = the linear
+ * form lam . v (hpp:27-37; interpolateInOwner's value, a SPACETIME foot). */
+gcmx_status gsx_test_interpolate(int device, int n, const double* v, const double* g, const double* c,
+                                 const double* q, const double* lam, double* out);
 
 /* ---- synchronisation and timing ------------------------------------------- */
 gcmx_status gcmx_sync(gcmx_ctx* ctx);

@@ -131,6 +131,120 @@ def barycentric4(a, b, c, d, q):  # geometry.hpp:142-151
     return (l[0], l[1], l[2], 1 - l[0] - l[1] - l[2])
 
 
+# ---- TetrahedronInterpolator / TriangleInterpolator (util/math/interpolation/
+# TetrahedronInterpolator.hpp, TriangleInterpolator.hpp) as standalone functions:
+# the reference's own known answers (src/test/sequence/TestInterpolator.cpp:
+# 129-282) pin them (tests/test_simplex_cpu.py); _interp below uses the same ones.
+_TET_TRIES = [(0, 1, 2, 3), (0, 1, 2, 4), (0, 1, 2, 5), (0, 1, 3, 4), (0, 1, 3, 5), (0, 1, 4, 5),
+              (0, 2, 3, 4), (0, 2, 3, 5), (0, 2, 4, 5), (0, 3, 4, 5), (1, 2, 3, 4), (1, 2, 3, 5),
+              (1, 2, 4, 5), (1, 3, 4, 5), (2, 3, 4, 5)]
+
+
+def _is_interpolation(lam):  # TetrahedronInterpolator.hpp:15-20 / TriangleInterpolator.hpp:15-19
+    return all(l > -EQUALITY_TOLERANCE for l in lam)
+
+
+def tet_weights(c, q):
+    """barycentricCoordinates + the isInterpolation assert (hpp:33-34)."""
+    lam = barycentric4(c[0], c[1], c[2], c[3], q)
+    if not _is_interpolation(lam):
+        raise ValueError("isInterpolation")  # assert_true throws gcm::Exception
+    return lam
+
+
+def tet_linear_lam(lam, v):  # hpp:35-38: lambda(0) * v0 + ... + lambda(3) * v3
+    return lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3]
+
+
+def tet_quadratic_lam(lam, c, v, g, q):  # hpp:54-58
+    t = [v[i] + _dot(g[i], _sub(q, c[i])) / 2.0 for i in range(4)]
+    return lam[0] * t[0] + lam[1] * t[1] + lam[2] * t[2] + lam[3] * t[3]
+
+
+def _limiter_min_max(u, vals):  # linal/functions.hpp:676-679: min(max(u, min(vals)), max(vals))
+    mn, mx = vals[0], vals[0]
+    for x in vals[1:]:
+        mn, mx = _std_min(mn, x), _std_max(mx, x)
+    return _std_min(_std_max(u, mn), mx)
+
+
+def tet_linear(c, v, q):  # TetrahedronInterpolator::interpolate, linear (hpp:27-38)
+    return tet_linear_lam(tet_weights(c, q), v)
+
+
+def tet_quadratic(c, v, g, q):  # TetrahedronInterpolator::interpolate, quadratic (hpp:47-58)
+    return tet_quadratic_lam(tet_weights(c, q), c, v, g, q)
+
+
+def tet_min_max(c, v, g, q):  # minMaxInterpolate (hpp:69-78)
+    return _limiter_min_max(tet_quadratic(c, v, g, q), v)
+
+
+def tet_hybrid_lam(lam, c, v, g, q):  # hybridInterpolate (hpp:93-104) with the weights given
+    quad = tet_quadratic_lam(lam, c, v, g, q)
+    return quad if quad == _limiter_min_max(quad, v) else tet_linear_lam(lam, v)
+
+
+def tet_hybrid(c, v, g, q):
+    return tet_hybrid_lam(tet_weights(c, q), c, v, g, q)
+
+
+def tet_owner_pick(c6, q):
+    """interpolateInOwner's choice (hpp:113-155): (point indices, barycentrics)."""
+    for tr in _TET_TRIES:
+        if _volume(*[c6[i] for i in tr]) != 0:
+            lam = barycentric4(*[c6[i] for i in tr], q)
+            if _is_interpolation(lam):
+                return tr, lam
+    raise ValueError("Containing tetrahedron is not found")
+
+
+def tet_interpolate_in_owner(c6, v6, q):
+    tr, lam = tet_owner_pick(c6, q)
+    return tet_linear_lam(lam, [v6[i] for i in tr])
+
+
+def tri_barycentric(a, b, c, q):  # geometry.hpp:108-116 (2-D): 2x2 Cramer (linearSystems.hpp:71-90)
+    T = [[a[0] - c[0], b[0] - c[0]], [a[1] - c[1], b[1] - c[1]]]
+    r = (q[0] - c[0], q[1] - c[1])
+    det = _det2(T[0][0], T[0][1], T[1][0], T[1][1])
+    if det == 0:
+        raise ValueError("SLE determinant is zero")
+    l0 = _det2(r[0], T[0][1], r[1], T[1][1]) / det
+    l1 = _det2(T[0][0], r[0], T[1][0], r[1]) / det
+    return (l0, l1, 1 - l0 - l1)
+
+
+def tri_weights(a, b, c, q):  # + the isInterpolation assert (TriangleInterpolator.hpp:32-33)
+    lam = tri_barycentric(a, b, c, q)
+    if not _is_interpolation(lam):
+        raise ValueError("isInterpolation")
+    return lam
+
+
+def tri_linear(c, v, q):  # TriangleInterpolator::interpolate, linear (hpp:26-36)
+    lam = tri_weights(c[0], c[1], c[2], q)
+    return lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2]
+
+
+def tri_quadratic(c, v, g, q):  # TriangleInterpolator::interpolate, quadratic (hpp:45-56)
+    lam = tri_weights(c[0], c[1], c[2], q)
+    t = [v[i] + (g[i][0] * (q[0] - c[i][0]) + g[i][1] * (q[1] - c[i][1])) / 2.0 for i in range(3)]
+    return lam[0] * t[0] + lam[1] * t[1] + lam[2] * t[2]
+
+
+def tri_min_max(c, v, g, q):  # TriangleInterpolator::minMaxInterpolate
+    return _limiter_min_max(tri_quadratic(c, v, g, q), v)
+
+
+def tri_interpolate_in_owner(c4, v4, q):  # TriangleInterpolator::interpolateInOwner (TRY_TRIANGLE order)
+    for tr in [(0, 1, 2), (0, 1, 3), (0, 2, 3), (1, 2, 3)]:
+        lam = tri_barycentric(*[c4[i] for i in tr], q)  # a zero determinant throws, as in the reference
+        if _is_interpolation(lam):
+            return lam[0] * v4[tr[0]] + lam[1] * v4[tr[1]] + lam[2] * v4[tr[2]]
+    raise ValueError("Containing triangle is not found")
+
+
 def _barycentric3(a, b, c, q):  # geometry.hpp:124-137
     l = _lls32(_sub(a, c), _sub(b, c), _sub(q, c))
     return (l[0], l[1], 1 - l[0] - l[1])
@@ -597,10 +711,6 @@ def _std_max(a, b):
 class Engine:
     """simplex::Engine<3> for one body (see module docstring)."""
 
-    TRIES = [(0, 1, 2, 3), (0, 1, 2, 4), (0, 1, 2, 5), (0, 1, 3, 4), (0, 1, 3, 5), (0, 1, 4, 5),
-             (0, 2, 3, 4), (0, 2, 3, 5), (0, 2, 4, 5), (0, 3, 4, 5), (1, 2, 3, 4), (1, 2, 3, 5),
-             (1, 2, 4, 5), (1, 3, 4, 5), (2, 3, 4, 5)]
-
     def __init__(self, coords, cells, U, U1, L, basis, courant, pde0, border_conditions=(),
                  grid=None, tau=None):
         """U, U1: [3][9][9]; L: [3][9]; basis: 3x3 (column s = stage s); pde0 [n][9];
@@ -734,21 +844,9 @@ class Engine:
         if kind == "cell":
             verts, q = foot[1], foot[2]
             c = [g.P[x] for x in verts]
-            lam = barycentric4(c[0], c[1], c[2], c[3], q)
-            if not all(l > -EQUALITY_TOLERANCE for l in lam):
-                raise ValueError("isInterpolation")
             v = [w[x][k] for x in verts]
-            terms = []
-            for i, x in enumerate(verts):
-                gr = (grads[x][0][k], grads[x][1][k], grads[x][2][k])
-                terms.append(v[i] + _dot(gr, _sub(q, c[i])) / 2.0)
-            quad = lam[0] * terms[0] + lam[1] * terms[1] + lam[2] * terms[2] + lam[3] * terms[3]
-            mn = _std_min(_std_min(_std_min(v[0], v[1]), v[2]), v[3])
-            mx = _std_max(_std_max(_std_max(v[0], v[1]), v[2]), v[3])
-            lim = _std_min(_std_max(quad, mn), mx)
-            if quad == lim:
-                return quad
-            return lam[0] * v[0] + lam[1] * v[1] + lam[2] * v[2] + lam[3] * v[3]
+            gr = [(grads[x][0][k], grads[x][1][k], grads[x][2][k]) for x in verts]
+            return tet_hybrid(c, v, gr, q)  # TetrahedronInterpolator::hybridInterpolate
         if kind == "st":  # common.hpp:102-129
             face, shift = foot[1], foot[2]
             r0 = g.P[it]
@@ -759,13 +857,7 @@ class Engine:
             vals = [w[face[0]][k], w[face[1]][k], w[face[2]][k],
                     wn[face[0]][k], wn[face[1]][k], wn[face[2]][k]]
             qst = (ww[0], ww[1], 1 - _length(_sub(rc, r0)) / _length(shift))
-            for tr in self.TRIES:  # TetrahedronInterpolator::interpolateInOwner
-                if _volume(*[pts[i] for i in tr]) != 0:
-                    lam = barycentric4(*[pts[i] for i in tr], qst)
-                    if all(l > -EQUALITY_TOLERANCE for l in lam):
-                        return lam[0] * vals[tr[0]] + lam[1] * vals[tr[1]] + \
-                            lam[2] * vals[tr[2]] + lam[3] * vals[tr[3]]
-            raise ValueError("Containing tetrahedron is not found")
+            return tet_interpolate_in_owner(pts, vals, qst)  # TetrahedronInterpolator::interpolateInOwner
         return 0.0
 
     def _mat_vec(self, M, x):  # linal/operators.hpp:109-123

@@ -230,6 +230,31 @@ def test_one_launch_stage_equals_two_launches(H, case, mode):
     assert np.abs(fused).max() > 0
 
 
+@pytest.mark.timeout(300)
+def test_one_launch_stage_above_block_cap_completes(H):
+    """k_sx_stage_l8 takes its work index from an atomic
+    ticket at block start instead of blockIdx.x, so a block waits only on work
+    that blocks already running took -- no assumption on the order the hardware
+    dispatches workgroups in.  Mode 3 lifts the 4096-block cap: a 53^3-vertex
+    cube (eight lanes per node: > 4 600 blocks of border and inner groups, with
+    space-time feet waiting on border nodes at Courant 2) completes without any
+    wait timing out (run_steps checks the error word) and equals the separate
+    launches bitwise."""
+    out = []
+    for fuse in (3, 0):
+        e = H.SimplexEngine(host_task(52, 2.0, 0.1, 7, border=FREE_BORDER))
+        e.set_node_lanes(8)
+        e.set_stage_fusion(fuse)
+        info = [e.stage_plan_info(0, s) for s in range(3)]
+        e.run_steps(2)
+        e.sync()
+        out.append((e.pde(), e.fused_stages))
+    (fused, n_fused), (split, n_split) = out
+    assert n_fused == 6 and n_split == 0
+    assert sum(w for _, w in info) > 0, info
+    assert np.array_equal(fused, split), f"{int((fused != split).sum())} values differ"
+
+
 def test_one_launch_stage_timeout_is_reported(H):
     """A device wait of the one-launch stage that gives up (forced here: a wait
     budget < 0 makes every wait report a timeout) must not hand stale results to
@@ -356,3 +381,54 @@ def test_cube_task_matches_oracle_across_the_load_switch(H):
         assert np.array_equal(got, want), f"step {done}: {int((got != want).sum())} values differ"
     assert e.fused_stages > 0
     assert np.abs(got).max() > 0
+
+
+def test_device_interpolation_known_answers():
+    """The simplex kernels' device interpolation (csrc/simplex.hip tet_hybrid /
+    tet_linear, what k_sx_inner / k_sx_border run per foot) on the reference's
+    own known-answer inputs (TestInterpolator.cpp:183-282), with the weights the
+    host plans compute: bitwise equal to the oracle's hybridInterpolate and
+    linear form; exact for a linear f (TetrahedronInterpolator.linear, within
+    EQUALITY_TOLERANCE * |f(q)|) and for a quadratic f wherever the hybrid limiter
+    kept the quadratic value (TetrahedronInterpolator.quadratic); interpolateInOwner's
+    answer 1 (:247-257) and the quadraticMinMax input's hybrid value 1.5 (:274-282)."""
+    from gcm_amd import _gcm_host as H
+    from gcm_amd import gcmx as G
+    from oracle import simplex as S
+    from tests.test_simplex_cpu import _f3, _g3, _q3, tet_known_answer_cases
+    cases = tet_known_answer_cases(1000, seed=183)
+    C = np.array([c for c, _ in cases], dtype=np.float64)
+    Q = np.array([q for _, q in cases], dtype=np.float64)
+    lam = np.array([H.tet_barycentric(*[list(x) for x in c], list(q)) for c, q in cases])
+    for fn, gr, name in ((_f3, lambda x: (5.0, 8.0, -4.0), "linear"), (_q3, _g3, "quadratic")):
+        V = np.array([[fn(x) for x in c] for c, _ in cases], dtype=np.float64)
+        Gr = np.array([[gr(x) for x in c] for c, _ in cases], dtype=np.float64)
+        hyb, lin = G.test_interpolate(V, Gr, C, Q, lam)
+        want_h = [S.tet_hybrid_lam(tuple(l), c, list(v), [tuple(g) for g in gg], q)
+                  for l, (c, q), v, gg in zip(lam, cases, V, Gr)]
+        want_l = [S.tet_linear_lam(tuple(l), list(v)) for l, v in zip(lam, V)]
+        assert np.array_equal(hyb, np.array(want_h)), name
+        assert np.array_equal(lin, np.array(want_l)), name
+        exact = np.array([fn(q) for _, q in cases])
+        tol = S.EQUALITY_TOLERANCE * np.abs(exact)
+        if name == "linear":
+            assert np.all(np.abs(lin - exact) <= tol) and np.all(np.abs(hyb - exact) <= tol)
+        else:
+            quad = np.array([S.tet_quadratic_lam(tuple(l), c, list(v), [tuple(g) for g in gg], q)
+                             for l, (c, q), v, gg in zip(lam, cases, V, Gr)])
+            kept = hyb == quad
+            assert kept.sum() > 100
+            assert np.all(np.abs(hyb[kept] - exact[kept]) <= tol[kept])
+    # interpolateInOwner (space-time foot): owner weights from the host pick, value 1
+    c6 = [[0, 0, 0], [0, 1, 0], [1, 0, 0], [0, 0, 1], [0, 1, 1], [1, 0, 1]]
+    v6 = [1.0, 1.0, 1.0, 1.0, 1e100, 1e100]
+    slots, lw = H.tet_owner_pick([list(map(float, p)) for p in c6], [0.1, 0.1, 0.1])
+    v4 = np.array([[v6[s] for s in slots]])
+    _, lin = G.test_interpolate(v4, np.zeros((1, 4, 3)), np.zeros((1, 4, 3)), np.zeros((1, 3)), np.array([lw]))
+    assert lin[0] == 1.0
+    # quadraticMinMax's input through the hybrid form: the limiter fires, linear value 1.5
+    c = [(0, 0, 1), (0, 1, 0), (1, 0, 0), (-1, -1, -1)]
+    lq = H.tet_barycentric(*[list(map(float, x)) for x in c], [0.0, 0.0, 0.0])
+    hyb, _ = G.test_interpolate(np.array([[1.0, 1, 1, 3]]), np.array([[(0, 0, 2), (0, 2, 0), (2, 0, 0), (-2, -2, -2)]],
+                                dtype=np.float64), np.array([c], dtype=np.float64), np.zeros((1, 3)), np.array([lq]))
+    assert hyb[0] == 1.5 == S.tet_hybrid(c, [1, 1, 1, 3], [(0, 0, 2), (0, 2, 0), (2, 0, 0), (-2, -2, -2)], (0, 0, 0))

@@ -446,3 +446,181 @@ def test_cube_task_plans_match_oracle(H):
         for i, (it, ci, nrm) in enumerate(e.corrected):
             outers = tuple(e.outers[s].get(it, []))
             assert b["outer"][s * nn + i] == CODE.get(outers, 0 if not outers else 3)
+
+
+# ---- the reference's own known answers for the simplex numerics -------------
+# src/test/sequence/TestInterpolator.cpp:129-282 and TestGslUtils.cpp:76-115,
+# restated with fixed seeds (the reference seeds with time(0), Utils.hpp:48-50).
+# They pin oracle/simplex.py's interpolators and LU, which the GPU tests compare
+# the kernels with bitwise, and the host set-up code that makes the stage plans'
+# weights (tet_barycentric, tet_owner_pick) and the contact correctors' LU
+# (csrc/contact.hpp through gsl_lu), bitwise against the oracle.
+
+def _rand_pts(rng, n, dim):
+    return [tuple(float(x) for x in rng.uniform(-1e6, 1e6, dim)) for _ in range(n)]
+
+
+def _rand_lam(rng, n):
+    lam = rng.uniform(0, 1, n)
+    return lam / (lam[0] + lam[1] + lam[2] + (lam[3] if n == 4 else 0.0))
+
+
+def _f3(x):  # TetrahedronInterpolator.linear's f
+    return 5 * x[0] + 8 * x[1] - 4 * x[2] - 2
+
+
+def _q3(x):  # TetrahedronInterpolator.quadratic's f and its gradient
+    return (8 * x[0] * x[0] + 10 * x[0] * x[1] - 9 * x[0] * x[2] - 15 * x[1] * x[1] + 6 * x[1] * x[2]
+            - 7 * x[2] * x[2] + 5 * x[0] + 8 * x[1] - 7 * x[2] - 2)
+
+
+def _g3(x):
+    return (16 * x[0] + 10 * x[1] - 9 * x[2] + 5, -30 * x[1] + 10 * x[0] + 6 * x[2] + 8,
+            -14 * x[2] + 6 * x[1] - 9 * x[0] - 7)
+
+
+def _comb(lam, pts):
+    d = len(pts[0])
+    return tuple(sum(lam[i] * pts[i][k] for i in range(len(pts))) for k in range(d))
+
+
+def tet_known_answer_cases(n=1000, seed=129):
+    """(c, q) pairs as TestInterpolator.cpp:183-264 draws them: four random
+    vertices in [-1e6, 1e6]^3 and a random convex combination."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        c = _rand_pts(rng, 4, 3)
+        out.append((c, _comb(_rand_lam(rng, 4), c)))
+    return out
+
+
+def test_tetrahedron_interpolator_linear_known_answers():
+    """TetrahedronInterpolator.linear (TestInterpolator.cpp:183-207): exact for a
+    linear f within EQUALITY_TOLERANCE * |f(q)|; a point outside throws."""
+    for c, q in tet_known_answer_cases():
+        v = [_f3(x) for x in c]
+        assert abs(S.tet_linear(c, v, q) - _f3(q)) <= S.EQUALITY_TOLERANCE * abs(_f3(q))
+        out = tuple(2 * c[0][k] + c[1][k] - c[2][k] - c[3][k] for k in range(3))
+        with pytest.raises(ValueError):
+            S.tet_linear(c, v, out)
+
+
+def test_tetrahedron_interpolator_quadratic_known_answers():
+    """TetrahedronInterpolator.quadratic (TestInterpolator.cpp:210-244): exact for
+    a quadratic f with its gradients; a point outside throws."""
+    for c, q in tet_known_answer_cases(seed=210):
+        v, g = [_q3(x) for x in c], [_g3(x) for x in c]
+        assert abs(S.tet_quadratic(c, v, g, q) - _q3(q)) <= S.EQUALITY_TOLERANCE * abs(_q3(q))
+        out = tuple(c[0][k] - c[1][k] - c[2][k] + 2 * c[3][k] for k in range(3))
+        with pytest.raises(ValueError):
+            S.tet_quadratic(c, v, g, out)
+
+
+def test_interpolate_in_owner_known_answers(H):
+    """TriangleInterpolator / TetrahedronInterpolator.interpolateInOwner
+    (TestInterpolator.cpp:178-185, 247-257): the owner holding q has value 1
+    at every vertex, the others 1e100 -- the answer is exactly 1.  The host
+    pick the stage plans use (tet_owner_pick) == the oracle's, bitwise."""
+    assert S.tri_interpolate_in_owner([(0, 0), (0, 1), (1, 0), (1, 1)], [1, 1, 1, 1e100], (0.2, 0.2)) == 1
+    c6 = [(0, 0, 0), (0, 1, 0), (1, 0, 0), (0, 0, 1), (0, 1, 1), (1, 0, 1)]
+    v6 = [1, 1, 1, 1, 1e100, 1e100]
+    assert S.tet_interpolate_in_owner(c6, v6, (0.1, 0.1, 0.1)) == 1
+    slots, lam = H.tet_owner_pick([list(map(float, p)) for p in c6], [0.1, 0.1, 0.1])
+    tr, lam_o = S.tet_owner_pick(c6, (0.1, 0.1, 0.1))
+    assert tuple(slots) == tuple(tr) and tuple(lam) == tuple(lam_o)
+    assert lam[0] * v6[slots[0]] + lam[1] * v6[slots[1]] + lam[2] * v6[slots[2]] + lam[3] * v6[slots[3]] == 1
+    # the space-time prism of interpolateInSpaceTime (common.hpp:102-129): host == oracle everywhere
+    pts = [(0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 0, 1), (0, 1, 1)]
+    rng = np.random.default_rng(102)
+    for _ in range(300):
+        a, b = rng.uniform(0, 1, 2)
+        if a + b > 1:
+            a, b = 1 - a, 1 - b
+        q = (float(a), float(b), float(rng.uniform(0, 1)))
+        hs, hl = H.tet_owner_pick([list(map(float, p)) for p in pts], list(q))
+        os_, ol = S.tet_owner_pick(pts, q)
+        assert tuple(hs) == tuple(os_) and tuple(hl) == tuple(ol)
+    with pytest.raises(Exception):
+        H.tet_owner_pick([list(map(float, p)) for p in pts], [2.0, 2.0, 0.5])
+
+
+def test_tetrahedron_barycentric_host_equals_oracle(H):
+    """The stage plans' CELL weights (host linal::barycentricCoordinates) ==
+    the oracle's, bitwise, on the known-answer cases."""
+    for c, q in tet_known_answer_cases(300, seed=142):
+        assert tuple(H.tet_barycentric(*[list(x) for x in c], list(q))) == S.barycentric4(*c, q)
+
+
+def test_quadratic_min_max_known_answers():
+    """Triangle / TetrahedronInterpolator.quadraticMinMax (TestInterpolator.cpp:
+    267-282): f = |x|^2 with its gradients; the quadratic value at 0 is 0, below
+    every vertex value, and the limiter returns exactly 1.  hybridInterpolate
+    (what the stage uses) falls back to the linear form there instead: 1.5."""
+    assert S.tri_min_max([(0, 1), (1, 0), (-1, -1)], [1, 1, 2], [(0, 2), (2, 0), (-2, -2)], (0, 0)) == 1
+    c = [(0, 0, 1), (0, 1, 0), (1, 0, 0), (-1, -1, -1)]
+    v, g = [1, 1, 1, 3], [(0, 0, 2), (0, 2, 0), (2, 0, 0), (-2, -2, -2)]
+    assert S.tet_min_max(c, v, g, (0, 0, 0)) == 1
+    assert S.tet_quadratic(c, v, g, (0, 0, 0)) == 0
+    assert S.tet_hybrid(c, v, g, (0, 0, 0)) == 1.5
+
+
+def test_triangle_interpolator_known_answers():
+    """TriangleInterpolator.linear / .quadratic (TestInterpolator.cpp:129-175) on
+    the oracle's restatement (the 2-D simplex path is not built: no 2-D config)."""
+    rng = np.random.default_rng(129)
+    f = lambda x: 5 * x[0] + 8 * x[1] - 2  # noqa: E731
+    fq = lambda x: 8 * x[0] * x[0] + 10 * x[0] * x[1] - 15 * x[1] * x[1] + 5 * x[0] + 8 * x[1] - 2  # noqa: E731
+    gq = lambda x: (16 * x[0] + 10 * x[1] + 5, -30 * x[1] + 10 * x[0] + 8)  # noqa: E731
+    for _ in range(1000):
+        c = _rand_pts(rng, 3, 2)
+        q = _comb(_rand_lam(rng, 3), c)
+        assert abs(S.tri_linear(c, [f(x) for x in c], q) - f(q)) <= S.EQUALITY_TOLERANCE * abs(f(q))
+        assert abs(S.tri_quadratic(c, [fq(x) for x in c], [gq(x) for x in c], q) - fq(q)) <= \
+            S.EQUALITY_TOLERANCE * abs(fq(q))
+        out = tuple(-2 * c[0][k] + c[1][k] + 2 * c[2][k] for k in range(2))
+        with pytest.raises(ValueError):
+            S.tri_linear(c, [f(x) for x in c], out)
+        out = tuple(3 * c[0][k] - c[1][k] - c[2][k] for k in range(2))
+        with pytest.raises(ValueError):
+            S.tri_quadratic(c, [fq(x) for x in c], [gq(x) for x in c], out)
+
+
+def test_gsl_utils_known_answers(H):
+    """GslUtils.determinant / solveLinearSystem (TestGslUtils.cpp:76-115) through
+    the oracle's GSL LU and csrc/contact.hpp's (host instantiation of the code the
+    contact kernels run): det(0_5) = 0, det(1_6) = 0, det(I_9) = 1, det(-I_7) =
+    -1 exactly; a 9 x 9 Vandermonde determinant within eps = 1e-2 relative
+    (GslUtils.hpp:15); 5 I x = 5 * 1 gives x = 1 exactly; a singular 1_5 system is
+    refused (gsl_linalg_LU_solve: matrix is singular); random 6 x 6 systems."""
+    def odet(A):
+        LU, _, sg = S._gsl_lu_decomp(np.asarray(A, dtype=float).tolist())
+        return S._gsl_lu_det(LU, sg)
+    cases = [(np.zeros((5, 5)), 0.0), (np.ones((6, 6)), 0.0), (np.eye(9), 1.0), (-np.eye(7), -1.0)]
+    for A, want in cases:
+        assert odet(A) == want
+        assert H.gsl_lu(A) == want
+    rng = np.random.default_rng(76)
+    a = rng.uniform(-1, 1, 9)  # linal::random<Vector<9>>() in [-1, 1]
+    V = np.array([[a[i] ** j for j in range(9)] for i in range(9)])
+    det = 1.0
+    for i in range(9):
+        for j in range(i + 1, 9):
+            det *= a[j] - a[i]
+    assert abs(odet(V) - det) <= abs(det) * 1e-2
+    assert H.gsl_lu(V) == odet(V)  # bitwise: the same restated algorithm
+    x = H.gsl_lu(5 * np.eye(4), [5.0] * 4)
+    assert x == [1.0] * 4
+    LU, perm, _ = S._gsl_lu_decomp((5 * np.eye(4)).tolist())
+    assert S._gsl_lu_solve(LU, perm, [5.0] * 4) == [1.0] * 4
+    with pytest.raises(Exception, match="singular"):
+        H.gsl_lu(np.ones((5, 5)), [1.0] * 5)
+    for _ in range(200):
+        A = rng.uniform(-1e12, 1e12, (6, 6))
+        b = rng.uniform(-1e12, 1e12, 6)
+        xh = H.gsl_lu(A, b.tolist())
+        LU, perm, _ = S._gsl_lu_decomp(A.tolist())
+        assert xh == S._gsl_lu_solve(LU, perm, b.tolist())
+        # linal::approximatelyEqual(A * x, b): relative 1e-9 per component on the scale of b
+        r = A @ np.array(xh) - b
+        assert np.all(np.abs(r) <= 1e-6 * (np.abs(A) @ np.abs(np.array(xh)) + np.abs(b)))
