@@ -22,6 +22,7 @@
 
 using namespace gcmx;
 static_assert(GCMX_MAX_BORDER_Q == kMaxBorderQ, "border quantity limit");
+static_assert(GCMX_MAX_FACE_CONDITIONS == kMaxFaceConds && GCMX_NO_FACE_CONDITION == kNoFaceCond, "face maps");
 
 namespace {
 
@@ -172,6 +173,17 @@ struct gcmx_border_nodes {
 	gcmx_ctx* ctx = nullptr;
 	int axis = 0, side = 0, n = 0;
 	int* nodes_d = nullptr;
+};
+
+// Per-node conditions of a body's faces (gcmx_face_map_create): one byte per
+// face node, the index of the last condition whose area holds it or
+// kNoFaceCond; the conditions' tables are written on the stream every step.
+struct gcmx_face_map {
+	gcmx_ctx* ctx = nullptr;
+	uint8_t* map_d[6] = {};
+	unsigned used[6] = {};  // per face: bit k = condition k occurs on it
+	BorderQ* bq_d = nullptr;
+	FaceCond* fc_d = nullptr;
 };
 
 namespace {
@@ -1458,6 +1470,120 @@ gcmx_status step_faces_impl(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 }  // namespace
 
 extern "C" {
+
+gcmx_status gcmx_face_map_create(gcmx_ctx* c, const uint8_t* const node_condition[6], gcmx_face_map** out) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!out || !node_condition) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	*out = nullptr;
+	auto m = std::unique_ptr<gcmx_face_map, void (*)(gcmx_face_map*)>(new gcmx_face_map(), gcmx_face_map_destroy);
+	m->ctx = c;
+	for (int f = 0; f < 2 * c->D; f++) {
+		if (!node_condition[f]) continue;
+		size_t n = 1;
+		for (int d = 0; d < c->D; d++)
+			if (d != f / 2) n *= (size_t)c->geo.sizes[d];
+		unsigned used = 0;
+		for (size_t i = 0; i < n; i++) {
+			const unsigned v = node_condition[f][i];
+			if (v == kNoFaceCond) continue;
+			if (v >= (unsigned)kMaxFaceConds)
+				return fail(GCMX_ERR_INVALID_ARG, "face map: condition index >= " + std::to_string(kMaxFaceConds));
+			used |= 1u << v;
+		}
+		if (!used) continue;  // no condition on this face: its ghosts stay as they are
+		m->used[f] = used;
+		HIP_TRY(hipMalloc(&m->map_d[f], n));
+		HIP_TRY(hipMemcpy(m->map_d[f], node_condition[f], n, hipMemcpyHostToDevice));
+	}
+	HIP_TRY(hipMalloc(&m->bq_d, kMaxFaceConds * sizeof(BorderQ)));
+	HIP_TRY(hipMalloc(&m->fc_d, kMaxFaceConds * sizeof(FaceCond)));
+	*out = m.release();
+	return GCMX_OK;
+}
+
+void gcmx_face_map_destroy(gcmx_face_map* m) {
+	if (!m) return;
+	if (m->ctx) {
+		hipSetDevice(m->ctx->device);
+		hipStreamSynchronize(m->ctx->stream);  // a pending step may still read the maps
+	}
+	for (uint8_t* p : m->map_d) hipFree(p);
+	hipFree(m->bq_d);
+	hipFree(m->fc_d);
+	delete m;
+}
+
+gcmx_status gcmx_step_face_map(gcmx_ctx* c, double tau, const gcmx_face_map* m, int n_cond,
+                               const gcmx_face* conds) {
+	gcmx_status s = check_ctx(c);
+	if (s) return s;
+	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
+	if (!m || m->ctx != c) return fail(GCMX_ERR_INVALID_ARG, "face map of another context");
+	if (n_cond < 0 || n_cond > kMaxFaceConds || (n_cond > 0 && !conds))
+		return fail(GCMX_ERR_INVALID_ARG, "0.." + std::to_string(kMaxFaceConds) + " conditions expected");
+	const int D = c->D;
+	unsigned on = 0;
+	for (int f = 0; f < 2 * D; f++)
+		if (m->map_d[f]) {
+			if (m->used[f] >> n_cond) return fail(GCMX_ERR_INVALID_ARG, "the face map names a condition not given");
+			on |= 1u << f;
+		}
+	FaceTables t{};
+	t.n = n_cond;
+	unsigned pressure = 0;  // conditions that set PRESSURE (the fused ghosts cannot form its trace)
+	for (int k = 0; k < n_cond; k++) {
+		if ((s = border_q(c, conds[k].n_quantities, conds[k].quantities, conds[k].values, t.bq[k])) != GCMX_OK)
+			return s;
+		FaceCond& fc = t.fc[k];
+		for (int q = 0; q < t.bq[k].n; q++) {
+			const int comp = quantity_comp(D, t.bq[k].q[q]);
+			if (comp < 0) {
+				pressure |= 1u << k;
+				continue;
+			}
+			fc.mask |= 1u << comp;
+			fc.two_v[comp] = 2 * t.bq[k].v[q];  // the last setting of a component wins
+		}
+	}
+	if ((s = build_tables(c, tau)) != GCMX_OK) return s;
+	if ((s = halo_wait(c)) != GCMX_OK) return s;
+	launch_set_face_tables(m->bq_d, m->fc_d, t, c->stream);
+	HIP_TRY(hipGetLastError());
+	c->last_ode_fused = false;
+	bool fused = D == 3 && effective_path(c) == GCMX_PATH_FUSED && fused_faces_supported(c->geo) &&
+	             (c->faces_written & ~on) == 0 && (!c->iso_het || c->het_ok);
+	for (int f = 2; f < 2 * D && fused; f++)
+		if (m->used[f] & pressure) fused = false;
+	auto fill = [&](int f) -> gcmx_status {
+		gcmx_status st = halo_wait(c);
+		if (st) return st;
+		Timed tm(c, "face_fill", 0.0, c->stream);
+		launch_face_fill_map(c->cur, c->geo, f / 2, (f & 1) ? 1 : -1, m->map_d[f], m->bq_d, c->stream);
+		HIP_TRY(hipGetLastError());
+		c->faces_written |= 1u << f;
+		return GCMX_OK;
+	};
+	if (fused) {
+		// x faces in memory, y/z faces formed inside the one-pass step per face node
+		for (int f = 0; f < 2; f++)
+			if (m->map_d[f] && (s = fill(f)) != GCMX_OK) return s;
+		FaceBC fb{};
+		for (int f = 2; f < 6; f++)
+			if (m->map_d[f]) {
+				fb.on |= 1u << (f - 2);
+				fb.map[f - 2] = m->map_d[f];
+			}
+		fb.conds = m->fc_d;
+		return fused_step(c, fb.on ? &fb : nullptr, true);
+	}
+	for (int a = 0; a < D; a++) {  // BorderConditions::apply(mesh, a), then the stage (Engine.cpp:90-121)
+		for (int f = 2 * a; f < 2 * a + 2; f++)
+			if (m->map_d[f] && (s = fill(f)) != GCMX_OK) return s;
+		if ((s = stage_impl(c, a, tau)) != GCMX_OK) return s;
+	}
+	return GCMX_OK;
+}
 
 gcmx_status gcmx_set_fp_mode(gcmx_ctx* c, gcmx_fp_mode mode) {
 	gcmx_status s = check_ctx(c);

@@ -200,6 +200,41 @@ __global__ __launch_bounds__(256) void k_face_fill(double* __restrict__ cur, Geo
 	border_point(cur, g, base, axis, side > 0 ? -1 : 1, bq);
 }
 
+// Every node of the face with a per-node condition map (gcmx_face_map): node i
+// (the other axes' inner indices, last fastest) takes condition bq[map[i]]; a
+// node no condition covers keeps its ghosts (BorderConditions::apply visits only
+// the nodes of its conditions, BorderConditions.hpp:81-91).
+__global__ __launch_bounds__(256) void k_face_fill_map(double* __restrict__ cur, Geo g, int axis, int side,
+                                                       const uint8_t* __restrict__ map,
+                                                       const BorderQ* __restrict__ bq) {
+	int ext[2] = {1, 1}, ax[2] = {0, 0}, n = 0;
+	for (int d = 0; d < g.D; d++)
+		if (d != axis) {
+			ax[n] = d;
+			ext[n] = g.sizes[d];
+			n++;
+		}
+	const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= (long long)ext[0] * ext[1]) return;
+	const unsigned c = map[i];
+	if (c == kNoFaceCond) return;
+	long long base = g.origin + (long long)(side > 0 ? g.sizes[axis] - 1 : 0) * g.stride[axis];
+	if (n == 1) base += i * g.stride[ax[0]];
+	if (n == 2) base += (i / ext[1]) * g.stride[ax[0]] + (i % ext[1]) * g.stride[ax[1]];
+	border_point(cur, g, base, axis, side > 0 ? -1 : 1, bq[c]);  // the table read in place
+}
+
+// A face map's condition tables into device memory, ordered on the stream (no
+// host synchronisation; kernel-argument values read with uniform indices only).
+__global__ __launch_bounds__(64) void k_set_face_tables(BorderQ* __restrict__ bq, FaceCond* __restrict__ fc,
+                                                        FaceTables t) {
+	if (threadIdx.x != 0) return;
+	for (int k = 0; k < t.n; k++) {
+		bq[k] = t.bq[k];
+		fc[k] = t.fc[k];
+	}
+}
+
 // ---------------------------------------------------------------- launchers --
 
 template <int D, int BS>
@@ -306,6 +341,19 @@ void launch_face_fill(double* cur, const Geo& g, int axis, int side, const Borde
 		if (d != axis) n *= g.sizes[d];
 	hipLaunchKernelGGL(k_face_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cur, g, axis,
 	                   side, bq);
+}
+
+void launch_face_fill_map(double* cur, const Geo& g, int axis, int side, const uint8_t* map_d,
+                          const BorderQ* bq_d, hipStream_t st) {
+	long long n = 1;
+	for (int d = 0; d < g.D; d++)
+		if (d != axis) n *= g.sizes[d];
+	hipLaunchKernelGGL(k_face_fill_map, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cur, g, axis, side,
+	                   map_d, bq_d);
+}
+
+void launch_set_face_tables(BorderQ* bq_d, FaceCond* fc_d, const FaceTables& t, hipStream_t st) {
+	hipLaunchKernelGGL(k_set_face_tables, dim3(1), dim3(64), 0, st, bq_d, fc_d, t);
 }
 
 }  // namespace gcmx

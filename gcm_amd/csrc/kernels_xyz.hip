@@ -455,7 +455,19 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	auto stz = [&](int c, int t, int y, double v) { out_p.st_nt(c, plane + (unsigned)y * sty + zo + (unsigned)t * stx, v); };
 #endif
 	// ghost value of component j on face f: -inner + 2 f(t) if overridden, else the mirror
-	auto ghost = [&](int f, int j, double v) { return ((fb.mask[f] >> j) & 1u) ? -v + fb.two_v[f][j] : v; };
+	// ghost value of component j of node x + t on face f: a face with a per-node map
+	// (partial faces) takes the face node's own condition (none: the ghost stays 0);
+	// pos = the node's z (y faces) or y (z faces)
+	auto ghost = [&](int f, int t, int pos, int j, double v) -> double {
+		if (fb.map[f]) {
+			const int xx = (t == 1 && !two) ? x : (t == 0 && !one) ? x + 1 : x + t;
+			const unsigned c = fb.map[f][(size_t)xx * (f < 2 ? Z : Y) + pos];
+			if (c == kNoFaceCond) return 0.0;
+			const FaceCond& fc = fb.conds[c];
+			return ((fc.mask >> j) & 1u) ? -v + fc.two_v[j] : v;
+		}
+		return ((fb.mask[f] >> j) & 1u) ? -v + fb.two_v[f][j] : v;
+	};
 
 	const int wv = z >> 6, ln = z & 63;  // wave in block, lane
 	if constexpr (NB) {  // zero halos (z ghosts stay zero without a z face); counters
@@ -645,7 +657,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll
 				for (int kk = 0; kk < W; kk++)
 					if (kk == ks) v = win[t][q][kk];
-				const double gv = ghost(f, wcomp(WMY, q), v);
+				const double gv = ghost(f, t, zc, wcomp(WMY, q), v);
 #pragma unroll
 				for (int kk = 0; kk < W; kk++)
 					if (kk == k) win[t][q][kk] = gv;
@@ -717,9 +729,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 						const int q = wslot(WMZ, j);
 						rg[wv][t][q][BS + ln] = yv[t][j];
 						if constexpr (FACES) {  // z ghosts: wave 0's left halo, the last wave's right halo
-							if ((fb.on & 4u) && z >= 1 && z <= BS) rg[0][t][q][BS - z] = ghost(2, j, yv[t][j]);
+							if ((fb.on & 4u) && z >= 1 && z <= BS) rg[0][t][q][BS - z] = ghost(2, t, y, j, yv[t][j]);
 							if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
-								rg[NW - 1][t][q][BS + 2 * (Z - 1) - z - 64 * (NW - 1)] = ghost(3, j, yv[t][j]);
+								rg[NW - 1][t][q][BS + 2 * (Z - 1) - z - 64 * (NW - 1)] = ghost(3, t, y, j, yv[t][j]);
 						}
 						if (edge) egp[(t * NWZ + q) * BS] = yv[t][j];
 					}
@@ -737,9 +749,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 						if constexpr (FACES) {
 							// idle lanes leave the z ghost slots to the face (or their zero)
 							if (UNI || z < Z || z >= Z + BS) zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
-							if ((fb.on & 4u) && z >= 1 && z <= BS) zl[t][q][BS - z] = ghost(2, j, yv[t][j]);
+							if ((fb.on & 4u) && z >= 1 && z <= BS) zl[t][q][BS - z] = ghost(2, t, y, j, yv[t][j]);
 							if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
-								zl[t][q][BS + 2 * (Z - 1) - z] = ghost(3, j, yv[t][j]);
+								zl[t][q][BS + 2 * (Z - 1) - z] = ghost(3, t, y, j, yv[t][j]);
 						} else {
 							zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
 						}

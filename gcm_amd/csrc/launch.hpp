@@ -39,6 +39,11 @@ void launch_border_fill(double* cur, const Geo& g, int axis, int inner_sign, int
 // The same over every node of the face (axis, side = -1 / +1).
 void launch_face_fill(double* cur, const Geo& g, int axis, int side, const BorderQ& bq,
                       hipStream_t st);
+// The same over a per-node face map (gcmx_face_map): node i of the face takes
+// condition bq_d[map_d[i]], none when map_d[i] == kNoFaceCond (ghosts untouched).
+void launch_face_fill_map(double* cur, const Geo& g, int axis, int side, const uint8_t* map_d,
+                          const BorderQ* bq_d, hipStream_t st);
+
 
 // kernels_fast.hip -- 3-D, homogeneous, structured isotropic-elastic matrices.
 // Per-axis values the fast kernels receive by value (kernel arguments, i.e.
@@ -58,10 +63,26 @@ bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& 
                    int x1, hipStream_t st);
 // The one-pass step needs 2*bs <= Z <= 1024 (one block spans a whole z row).
 bool fused_supported(const Geo& g);
-// Uniform cubic border conditions on the y/z faces, as the one-pass step consumes
+// One cubic border condition as the one-pass step applies it to a ghost: the
+// components in `mask` set to -inner + two_v[c], the others mirrored
+// (BorderConditions.hpp:94-114; two_v = 2 * timeDependency(t)).
+struct FaceCond {
+	unsigned mask;
+	unsigned pad_;
+	double two_v[9];
+};
+constexpr int kMaxFaceConds = 8;  // conditions of one per-node face map (gcmx_face_map)
+constexpr uint8_t kNoFaceCond = 255;
+// Cubic border conditions on the y/z faces, as the one-pass step consumes
 // them (face f: 0 y-, 1 y+, 2 z-, 3 z+): the ghosts are the mirrored inner nodes
 // with the components in mask[f] set to -inner + two_v[f][c]
-// (BorderConditions.hpp:94-114; two_v = 2 * timeDependency(t)).
+// (BorderConditions.hpp:94-114; two_v = 2 * timeDependency(t)).  A face with a
+// per-node map (map[f] != null: PARTIAL faces, e.g. titan's cylinder,
+// launcher/ndi.hpp:309-315) takes each face node's own condition
+// conds[map[f][node]] instead -- the last condition whose area holds the node --
+// and kNoFaceCond for a node no condition covers, whose ghosts stay zero (the
+// reference never writes them); maps are [x][z] (y faces) / [x][y] (z faces)
+// over the context's inner nodes.
 struct FaceBC {
 	unsigned on;          // bit f: face f has a condition
 	unsigned mask[4];     // overridden components
@@ -70,7 +91,16 @@ struct FaceBC {
 	// stress component of the step's result times `ode` (Ode.hpp:28-37) when ode_on
 	unsigned ode_on;
 	double ode;
+	const uint8_t* map[4];
+	const FaceCond* conds;
 };
+// Condition tables of a face map into device memory, ordered on the stream.
+struct FaceTables {
+	int n;
+	BorderQ bq[kMaxFaceConds];
+	FaceCond fc[kMaxFaceConds];
+};
+void launch_set_face_tables(BorderQ* bq_d, FaceCond* fc_d, const FaceTables& t, hipStream_t st);
 // The one-pass step with FaceBC face conditions (on != 0) needs bs <= 2, Z <= 512
 // and Y, Z >= 2*bs + 2; a FaceBC with on == 0 carries only the ODE factor.
 bool fused_faces_supported(const Geo& g);

@@ -40,6 +40,7 @@ SYMBOLS = [
     "gcmx_set_kernel_path", "gcmx_set_step_schedule", "gcmx_set_fp_mode", "gcmx_get_fp_mode", "gcmx_effective_path", "gcmx_last_step_path",
     "gcmx_border_fill",
     "gcmx_border_nodes_create", "gcmx_border_apply", "gcmx_border_nodes_destroy", "gcmx_step_faces",
+    "gcmx_face_map_create", "gcmx_face_map_destroy", "gcmx_step_face_map",
     "gcmx_copy_box",
     "gcmx_ode_maxwell", "gcmx_step_ode", "gcmx_last_ode_fused",
     "gcmx_comm_unique_id", "gcmx_comm_init_opts", "gcmx_comm_init", "gcmx_comm_channels_per_peer",
@@ -131,6 +132,10 @@ def lib() -> ctypes.CDLL:
     L.gcmx_border_nodes_destroy.argtypes = [vp]
     L.gcmx_border_nodes_destroy.restype = None
     L.gcmx_step_faces.argtypes = [vp, ctypes.c_double, ctypes.POINTER(Face)]
+    L.gcmx_face_map_create.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(vp)]
+    L.gcmx_face_map_destroy.argtypes = [vp]
+    L.gcmx_face_map_destroy.restype = None
+    L.gcmx_step_face_map.argtypes = [vp, ctypes.c_double, vp, ctypes.c_int, ctypes.POINTER(Face)]
     L.gcmx_copy_box.argtypes = [vp, ip, ip, vp, ip]
     L.gcmx_ode_maxwell.argtypes = [vp, ctypes.c_double, dp, ctypes.c_int]
     L.gcmx_step_ode.argtypes = [vp, ctypes.c_double, ctypes.POINTER(Face), dp, ctypes.c_int]
@@ -335,6 +340,23 @@ class Context:
         list of (quantity code, value) in the reference's application order."""
         _check(lib().gcmx_step_faces(self._ptr, tau, self._faces(faces)))
 
+    def face_map(self, node_condition: Sequence[Optional[np.ndarray]]) -> "FaceMap":
+        """gcmx_face_map_create: per face (2*axis + (side > 0)) None or one uint8
+        per face node (other axes increasing, last fastest): condition index or
+        255 (GCMX_NO_FACE_CONDITION)."""
+        return FaceMap(self, node_condition)
+
+    def step_face_map(self, tau: float, fmap: "FaceMap", conditions: Sequence[Sequence[tuple]]):
+        """gcmx_step_face_map: conditions[k] = [(quantity code, value), ...] at Clock::Time()."""
+        arr = (Face * max(1, len(conditions)))()
+        for k, lst in enumerate(conditions):
+            arr[k].enabled = 1
+            arr[k].n_quantities = len(lst)
+            for i, (q, v) in enumerate(lst):
+                arr[k].quantities[i] = q
+                arr[k].values[i] = v
+        _check(lib().gcmx_step_face_map(self._ptr, tau, fmap.ptr, len(conditions), arr))
+
     def step_ode(self, tau: float, tau0: Sequence[float], faces=None):
         """gcmx_step_ode: the step (gcmx_step, or gcmx_step_faces with `faces`) then
         MaxwellViscosityOde, folded into the one-pass step's stores where it can be."""
@@ -444,6 +466,29 @@ class Context:
     @property
     def device_bytes(self) -> int:
         return lib().gcmx_device_bytes(self._ptr)
+
+
+class FaceMap:
+    """gcmx_face_map: per-node face conditions, uploaded once."""
+
+    def __init__(self, ctx: "Context", node_condition):
+        self._ctx = ctx  # keeps the context alive
+        self._maps = [None if m is None else np.ascontiguousarray(m, dtype=np.uint8).reshape(-1)
+                      for m in list(node_condition) + [None] * (6 - len(node_condition))]
+        ptrs = (ctypes.c_void_p * 6)(*[None if m is None else m.ctypes.data for m in self._maps])
+        self.ptr = ctypes.c_void_p()
+        _check(lib().gcmx_face_map_create(ctx.ptr, ptrs, ctypes.byref(self.ptr)))
+
+    def close(self):
+        if self.ptr and self.ptr.value:
+            lib().gcmx_face_map_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class BorderNodes:

@@ -371,10 +371,46 @@ HipBorderConditions<D>::HipBorderConditions(const Task& task, const HipMesh<D>& 
 		for (int e : eff) uniform = uniform && e == eff[0];
 		faceCondition[f] = eff.empty() ? -1 : eff[0];
 	}
+	if (!uniform && conditions.size() <= GCMX_MAX_FACE_CONDITIONS) {
+		// partial faces: each face node's last condition, as one byte per face node
+		std::array<std::vector<uint8_t>, 6> maps;
+		const uint8_t* ptr[6] = {};
+		for (int f = 0; f < 2 * D; f++) {
+			maps[f].resize(effective[f].size());
+			for (size_t k = 0; k < effective[f].size(); k++)
+				maps[f][k] = effective[f][k] < 0 ? (uint8_t)GCMX_NO_FACE_CONDITION : (uint8_t)effective[f][k];
+			ptr[f] = maps[f].data();
+		}
+		if (gcmx_face_map_create(mesh.ctx(), ptr, &faceMap_) != GCMX_OK) {
+			faceMap_ = nullptr;  // the per-stage node-list path stays available
+			for (auto& done : conditions) {
+				gcmx_border_nodes_destroy(done.leftD);
+				gcmx_border_nodes_destroy(done.rightD);
+			}
+			conditions.clear();
+			throw Exception(std::string("gcmx_face_map_create: ") + gcmx_last_error());
+		}
+	}
+}
+
+template <int D>
+int HipBorderConditions<D>::conditionsAt(gcmx_face* out) const {
+	for (size_t k = 0; k < conditions.size(); k++) {
+		const Condition& c = conditions[k];
+		out[k] = gcmx_face{};
+		out[k].enabled = 1;
+		out[k].n_quantities = (int)c.values.size();
+		for (size_t i = 0; i < c.values.size(); i++) {
+			out[k].quantities[i] = quantityCode(c.values[i].first);
+			out[k].values[i] = c.values[i].second(Clock::Time());
+		}
+	}
+	return (int)conditions.size();
 }
 
 template <int D>
 HipBorderConditions<D>::~HipBorderConditions() {
+	gcmx_face_map_destroy(faceMap_);
 	for (auto& c : conditions) {
 		gcmx_border_nodes_destroy(c.leftD);
 		gcmx_border_nodes_destroy(c.rightD);
@@ -516,7 +552,7 @@ void Engine<D>::nextTimeStep() {
 	bool plain = true, faces = true, xcontacts = D == 3;
 	for (const Body& b : bodies) {
 		plain = plain && b.border->empty() && b.contacts.empty();
-		faces = faces && b.border->uniformFaces() && b.contacts.empty();
+		faces = faces && (b.border->uniformFaces() || b.border->faceMap()) && b.contacts.empty();
 		xcontacts = xcontacts && b.border->empty();
 		for (const auto& contact : b.contacts) xcontacts = xcontacts && contact.direction == 0;
 	}
@@ -558,9 +594,18 @@ void Engine<D>::nextTimeStep() {
 		// runs the step (fused where admissible) with the faces' values at
 		// Clock::Time() -- the time all D stages of the reference step see.
 		for (Body& b : bodies) {
+			HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(*b.mesh);
+			if (const gcmx_face_map* fm = b.border->faceMap()) {
+				// partial faces: each face node's own last condition, the whole step in
+				// the library (one pass where admissible), then the ODEs
+				gcmx_face conds[GCMX_MAX_FACE_CONDITIONS];
+				const int n = b.border->conditionsAt(conds);
+				gcmxCheck(gcmx_step_face_map(mesh.ctx(), Clock::TimeStep(), fm, n, conds), "gcmx_step_face_map");
+				for (auto& ode : b.odes) ode->apply(*b.mesh, Clock::TimeStep());
+				continue;
+			}
 			gcmx_face f[6];
 			b.border->faces(f);
-			HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(*b.mesh);
 			if (oneMaxwell(b)) {
 				const auto& tau0 = mesh.deviceTau0();
 				gcmxCheck(gcmx_step_ode(mesh.ctx(), Clock::TimeStep(), f, tau0.data(), (int)tau0.size()),

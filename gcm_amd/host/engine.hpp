@@ -206,6 +206,11 @@ public:
 	virtual bool uniformFaces() const { return false; }
 	/// gcmx_face per face (2*D entries, faces[2*axis + side]) at Clock::Time().
 	virtual void faces(gcmx_face*) const {}
+	/// Non-uniform faces held as a per-node face map (gcmx_face_map): the whole
+	/// step runs through gcmx_step_face_map.  Null when there is none.
+	virtual const gcmx_face_map* faceMap() const { return nullptr; }
+	/// Every condition's quantities at Clock::Time() (the face map's conditions).
+	virtual int conditionsAt(gcmx_face*) const { return 0; }
 };
 
 /// BorderConditions<Mesh> (BorderConditions.hpp:23-121): node lists found on the
@@ -223,6 +228,8 @@ public:
 	bool empty() const override { return conditions.empty(); }
 	bool uniformFaces() const override { return uniform; }
 	void faces(gcmx_face* out) const override;
+	const gcmx_face_map* faceMap() const override { return faceMap_; }
+	int conditionsAt(gcmx_face* out) const override;
 
 private:
 	struct Condition {
@@ -235,6 +242,7 @@ private:
 	std::vector<Condition> conditions;
 	bool uniform = false;
 	std::array<int, 6> faceCondition{{-1, -1, -1, -1, -1, -1}};  // per face: condition or -1
+	gcmx_face_map* faceMap_ = nullptr;  // non-uniform faces, <= GCMX_MAX_FACE_CONDITIONS conditions
 };
 
 /// engine/cubic/ContactConditions.hpp:20-68 (adhesion: plain copy)

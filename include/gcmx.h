@@ -194,6 +194,29 @@ typedef struct gcmx_face {
 } gcmx_face;
 gcmx_status gcmx_step_faces(gcmx_ctx* ctx, double tau, const gcmx_face* faces);
 
+/* PARTIAL faces (a condition's area covers part of a face, e.g. the titan
+ * preset's cylinder, launcher/ndi.hpp:309-315): one byte per face node, the
+ * index of the LAST condition whose area holds the node (BorderConditions::apply
+ * runs the conditions in order and a later one rewrites the whole ghost,
+ * BorderConditions.hpp:81-114), or GCMX_NO_FACE_CONDITION where none does (the
+ * reference never writes those ghosts).  node_condition[f], f = 2*axis + (side >
+ * 0), covers the face's inner nodes with the other axes in increasing order,
+ * the last fastest (y faces [x][z], z faces [x][y], x faces [y][z]); NULL = no
+ * condition on that face.  The maps are uploaded once (a body's border nodes are
+ * static).  gcmx_step_face_map = for s = 0..dim-1: the conditions' fills of the
+ * faces of axis s, then gcmx_stage(s) -- with conds[k] the k-th condition's
+ * quantities and values at Clock::Time() (at most GCMX_MAX_FACE_CONDITIONS).  In
+ * 3-D it keeps the one-pass step on the same terms as gcmx_step_faces (each face
+ * node's ghost formed from its own condition inside the kernel); results are
+ * identical either way. */
+#define GCMX_MAX_FACE_CONDITIONS 8
+#define GCMX_NO_FACE_CONDITION 255
+typedef struct gcmx_face_map gcmx_face_map;
+gcmx_status gcmx_face_map_create(gcmx_ctx* ctx, const uint8_t* const node_condition[6], gcmx_face_map** out);
+void        gcmx_face_map_destroy(gcmx_face_map* map);
+gcmx_status gcmx_step_face_map(gcmx_ctx* ctx, double tau, const gcmx_face_map* map, int n_conditions,
+                               const gcmx_face* conditions);
+
 /* Replaces ContactCopier::apply (engine/cubic/ContactConditions.hpp:56-68):
  * copy a box of `dst`'s current layer from a same-sized box of `src`'s current
  * layer (boxes as local multi-indices [min, max), may include ghosts).  Both
