@@ -297,6 +297,31 @@ __device__ __forceinline__ void waterfall(unsigned key, F f) {
 	}
 }
 
+// A double / int made wave-uniform (SGPR-resident) by v_readfirstlane.
+__device__ __forceinline__ double rfl(double v) {
+	const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+	const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+	const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+	return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ IsoAxis iso_uniform(const IsoAxis& t) {
+	IsoAxis r;
+	r.a = rfl(t.a);
+	r.b = rfl(t.b);
+	r.g = rfl(t.g);
+	r.p1 = rfl(t.p1);
+	r.p2 = rfl(t.p2);
+	r.s = rfl(t.s);
+#pragma unroll
+	for (int i = 0; i < 3; i++) {
+		r.c1[i] = rfl(t.c1[i]);
+		r.c2[i] = rfl(t.c2[i]);
+	}
+	r.kf1 = __builtin_amdgcn_readfirstlane(t.kf1);
+	r.kf2 = __builtin_amdgcn_readfirstlane(t.kf2);
+	return r;
+}
+
 // Component held in window slot q of a stage whose window mask is `mask`.
 __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 	int n = 0;
@@ -458,6 +483,11 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// ghost value of component j of node x + t on face f: a face with a per-node map
 	// (partial faces) takes the face node's own condition (none: the ghost stays 0);
 	// pos = the node's z (y faces) or y (z faces)
+	// per-material table k (wave-uniform: waterfall) with every field made
+	// wave-uniform by readfirstlane, so the tables live in SGPRs like the
+	// homogeneous step's kernel-argument tables (as plain loads they took 26
+	// VGPRs each and the HET kernel sat at 252 VGPRs)
+	auto mt = [&](unsigned k) -> IsoAxis { return iso_uniform(mtab[k]); };
 	auto ghost = [&](int f, int t, int pos, int j, double v) -> double {
 		if (fb.map[f]) {
 			const int xx = (t == 1 && !two) ? x : (t == 0 && !one) ? x + 1 : x + t;
@@ -624,7 +654,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		if constexpr (HET) {
 			waterfall(key, [&](unsigned k) {
 				const unsigned m0 = k & 255u, m1 = k >> 8;
-				x_compute(pre, wc, cv, xr, mtab[m0], mtab[m1], m0 == m1);
+				x_compute(pre, wc, cv, xr, mt(m0), mt(m1), m0 == m1);
 			});
 		} else {
 			x_compute(pre, wc, cv, xr, AX, AX, true);
@@ -707,7 +737,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cp[(t * NCY + wslot(CMY, j)) * ZT]; },
 				    yv[t]);
 			};
-			if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mtab[k]); });
+			if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mt(k)); });
 			else go(AY);
 		}
 	};
@@ -799,7 +829,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				    A, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
 				    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
 		};
-		if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mtab[k]); });
+		if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mt(k)); });
 		else go(AZ);
 		if (fb.ode_on) {  // MaxwellViscosityOde: sigma *= exp(-tau / tau0), the stored product (Ode.hpp:34-35)
 #pragma unroll
