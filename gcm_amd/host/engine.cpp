@@ -2,6 +2,8 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <string>
 
@@ -136,7 +138,121 @@ HipMesh<D>::HipMesh(const Task&, size_t id_, const typename CubicGrid<D>::Constr
 
 template <int D>
 HipMesh<D>::~HipMesh() {
-	gcmx_destroy(ctx_);
+	if (ownsCtx_) gcmx_destroy(ctx_);
+}
+
+// ---------------------------------------------------------------------- stacks --
+
+/// Calls f(it) for every node of a grid of `sizes` INCLUDING bs ghost layers.
+template <int D, class F>
+static void forEachAll(const std::array<int, D>& sizes, int bs, F f) {
+	std::array<int, D> it;
+	for (int d = 0; d < D; d++) it[d] = -bs;
+	while (true) {
+		f(it);
+		int d = D - 1;
+		for (; d >= 0; d--) {
+			if (++it[d] < sizes[d] + bs) break;
+			it[d] = -bs;
+		}
+		if (d < 0) break;
+	}
+}
+
+template <int D>
+void HipMesh<D>::joinStack(const std::shared_ptr<HipMesh<D>>& stack, int axis, int offset) {
+	if (stack_) throw Exception("the body is in a stack already");
+	if (ownsCtx_) gcmx_destroy(ctx_);  // its device layers live in the stack
+	ctx_ = stack->ctx_;
+	ownsCtx_ = false;
+	stack_ = stack;
+	stackAxis_ = axis;
+	stackOffset_ = offset;
+}
+
+template <int D>
+HostState<D> HipMesh<D>::setUpMember(const Task& task) {
+	if (pdeIsSetUp) throw Exception("setUpPde called twice");
+	pdeIsSetUp = true;
+	HostState<D> st = buildHostState<D>(task, *this);
+	matrices = st.matrices;
+	maximalEigenvalue = st.maximalEigenvalue;
+	materialNumbers_ = st.materialNumber;
+	if (matrices.size() > 1) matIdAll_ = st.matId;
+	return st;
+}
+
+template <int D>
+void HipMesh<D>::setUpStack(const std::vector<std::shared_ptr<HipMesh<D>>>& members,
+                            const std::vector<HostState<D>>& states) {
+	if (pdeIsSetUp) throw Exception("setUpPde called twice");
+	pdeIsSetUp = true;
+	// one table over the members' material conditions; bitwise-equal ones shared
+	// (a stack of one material stays homogeneous: the non-HET one-pass step)
+	std::vector<const GcmMatrices<D>*> table;
+	std::vector<real> tau0;
+	std::vector<std::vector<int>> remap(members.size());
+	for (size_t k = 0; k < members.size(); k++)
+		for (size_t c = 0; c < states[k].matrices.size(); c++) {
+			const GcmMatrices<D>& m = states[k].matrices[c];
+			int found = -1;
+			for (size_t t = 0; t < table.size() && found < 0; t++)
+				if (std::memcmp(table[t], &m, sizeof(m)) == 0 && std::memcmp(&tau0[t], &states[k].tau0[c], sizeof(real)) == 0)
+					found = (int)t;
+			if (found < 0) {
+				found = (int)table.size();
+				table.push_back(&m);
+				tau0.push_back(states[k].tau0[c]);
+			}
+			remap[k].push_back(found);
+		}
+	if (table.size() > 255) throw Exception("a stack holds at most 255 materials");
+	// the stack's all-nodes state: every member's inner nodes and its ghost layers
+	// on the other axes; along the stack axis a member's ghost layers at a contact
+	// are its neighbour's inner layers (the stack's own ghosts only at its ends)
+	const int bs = this->borderSize, a = members.empty() ? 0 : members[0]->stackAxis_;
+	std::vector<real> pde((size_t)this->sizeOfAllNodes() * M, 0.0);
+	std::vector<uint8_t> ids((size_t)this->sizeOfAllNodes(), 0);
+	std::vector<int> used(table.size(), 0);
+	for (size_t k = 0; k < members.size(); k++) {
+		const HipMesh<D>& mb = *members[k];
+		forEachAll<D>(mb.sizes, bs, [&](const IntD& it) {
+			if ((it[a] < 0 && k > 0) || (it[a] >= mb.sizes[a] && k + 1 < members.size())) return;
+			IntD is = it;
+			is[a] += mb.stackOffset_;
+			const size_t src = (size_t)mb.getIndex(it), dst = (size_t)this->getIndex(is);
+			for (int c = 0; c < M; c++) pde[dst * M + c] = states[k].pde[src * M + c];
+			const int t = remap[k][states[k].matId[src]];
+			ids[dst] = (uint8_t)t;
+			bool inner = true;
+			for (int d = 0; d < D; d++) inner = inner && it[d] >= 0 && it[d] < mb.sizes[d];
+			if (inner) used[(size_t)t] = 1;
+		});
+	}
+	std::vector<int> dev(table.size(), -1);
+	int nUsed = 0;
+	for (size_t t = 0; t < table.size(); t++)
+		if (used[t]) dev[t] = nUsed++;
+	std::vector<real> U((size_t)nUsed * D * M * M), U1(U.size()), L((size_t)nUsed * D * M);
+	deviceTau0_.assign(nUsed, 0);
+	maximalEigenvalue = 0;
+	for (size_t t = 0; t < table.size(); t++) {
+		if (dev[t] < 0) continue;
+		deviceTau0_[dev[t]] = tau0[t];
+		maximalEigenvalue = std::fmax(maximalEigenvalue, table[t]->getMaximalEigenvalue());
+		for (int s = 0; s < D; s++) {
+			const size_t o = ((size_t)dev[t] * D + s);
+			std::copy(table[t]->m[s].U.begin(), table[t]->m[s].U.end(), U.begin() + o * M * M);
+			std::copy(table[t]->m[s].U1.begin(), table[t]->m[s].U1.end(), U1.begin() + o * M * M);
+			std::copy(table[t]->m[s].L.begin(), table[t]->m[s].L.end(), L.begin() + o * M);
+		}
+	}
+	gcmxCheck(gcmx_set_materials(ctx_, nUsed, U.data(), U1.data(), L.data()), "gcmx_set_materials");
+	if (nUsed > 1) {
+		for (auto& m : ids) m = (uint8_t)std::max(0, dev[m]);
+		gcmxCheck(gcmx_set_material_ids(ctx_, ids.data()), "gcmx_set_material_ids");
+	}
+	gcmxCheck(gcmx_upload(ctx_, pde.data()), "gcmx_upload");
 }
 
 template <int D>
@@ -275,6 +391,18 @@ void HipMesh<D>::setUpPde(const Task& task) {
 template <int D>
 std::vector<real> HipMesh<D>::pdeAll() const {
 	std::vector<real> out((size_t)this->sizeOfAllNodes() * M);
+	if (stack_) {  // this member's part of the stack (its ghost layers at a contact:
+		           // the neighbour's inner layers, as the contact copy leaves them)
+		const std::vector<real> all = stack_->pdeAll();
+		const int bs = this->borderSize;
+		forEachAll<D>(this->sizes, bs, [&](const IntD& it) {
+			IntD is = it;
+			is[stackAxis_] += stackOffset_;
+			const size_t src = (size_t)stack_->getIndex(is), dst = (size_t)this->getIndex(it);
+			for (int c = 0; c < M; c++) out[dst * M + c] = all[src * M + c];
+		});
+		return out;
+	}
 	gcmxCheck(gcmx_download(ctx_, out.data()), "gcmx_download");
 	return out;
 }
@@ -461,14 +589,29 @@ template <int D>
 Engine<D>::Engine(const Task& task, int device_) : AbstractEngine(task), device(device_) {
 	if (task.globalSettings.dimensionality != D) throw Exception("dimensionality mismatch");
 	createGridsAndContacts(task);
+	buildStacks(task);
+	std::map<size_t, HostState<D>> memberStates;
 	for (const auto& tb : task.bodies) {
 		Body& body = getBody(tb.first);
-		body.mesh->setUpPde(task);
+		if (body.stack)
+			memberStates.emplace(tb.first, std::dynamic_pointer_cast<HipMesh<D>>(body.mesh)->setUpMember(task));
+		else
+			body.mesh->setUpPde(task);
 		body.gcm = body.factory->createGcm(task);
 		body.border = body.factory->createBorder(task, body.mesh);
 		for (const Snapshotters::T snapType : task.globalSettings.snapshottersId)
 			body.snapshotters.push_back(body.factory->createSnapshotter(task, snapType));
 		for (const Odes::T odeType : tb.second.odes) body.odes.push_back(body.factory->createOde(odeType));
+	}
+	for (Body& lead : bodies) {  // every stack's set-up from its members' host states
+		if (!lead.stackLead) continue;
+		std::vector<std::shared_ptr<HipMesh<D>>> members;
+		std::vector<HostState<D>> states;
+		for (size_t id : stackOrder_.at(lead.mesh->id)) {
+			members.push_back(std::dynamic_pointer_cast<HipMesh<D>>(getBody(id).mesh));
+			states.push_back(std::move(memberStates.at(id)));
+		}
+		lead.stack->setUpStack(members, states);
 	}
 	afterConstruction(task);
 }
@@ -546,6 +689,91 @@ void Engine<D>::createGridsAndContacts(const Task& task) {
 	}
 }
 
+// Stacks (HipMesh::joinStack): chains of 3-D bodies along y or z whose every
+// contact lies along that axis, between bodies of equal sizes and starts on the
+// other two axes, with no border conditions and the same ODEs.  Their contact
+// copies then only ever write what the stack's own stages read, so the chain
+// runs as one grid.  GCMX_NO_STACKS=1 keeps the separate bodies (A/B, tests).
+template <int D>
+void Engine<D>::buildStacks(const Task& task) {
+	if (D != 3) return;
+	if (const char* e = std::getenv("GCMX_NO_STACKS"))
+		if (std::atoi(e) != 0) return;
+	auto hasBorder = [&](size_t id) {
+		const auto f = task.cubicBorderConditions.find(id);
+		return f != task.cubicBorderConditions.end() && !f->second.empty();
+	};
+	for (int a = 1; a < D; a++) {
+		std::map<size_t, bool> ok;  // every contact along a, partners of equal cross-section
+		for (Body& b : bodies) {
+			bool good = !b.stack && !b.contacts.empty() && !hasBorder(b.mesh->id);
+			for (const auto& c : b.contacts) {
+				if (c.direction != a) good = false;
+				const Body& o = getBody(c.neighborId);
+				for (int d = 0; d < D; d++)
+					if (d != a && (o.mesh->sizes[d] != b.mesh->sizes[d] || o.mesh->start[d] != b.mesh->start[d]))
+						good = false;
+			}
+			ok[b.mesh->id] = good;
+		}
+		std::map<size_t, bool> seen;
+		for (Body& b : bodies) {
+			const size_t id0 = b.mesh->id;
+			if (!ok[id0] || seen[id0]) continue;
+			std::vector<size_t> comp, todo{id0};
+			seen[id0] = true;
+			bool allGood = true;
+			while (!todo.empty()) {  // the bodies connected to id0 by contacts
+				const size_t id = todo.back();
+				todo.pop_back();
+				comp.push_back(id);
+				for (const auto& c : getBody(id).contacts) {
+					if (!ok[c.neighborId]) allGood = false;
+					if (!seen[c.neighborId]) {
+						seen[c.neighborId] = true;
+						todo.push_back(c.neighborId);
+					}
+				}
+			}
+			if (!allGood || comp.size() < 2) continue;
+			std::sort(comp.begin(), comp.end(),
+			          [&](size_t p, size_t q) { return getBody(p).mesh->start[a] < getBody(q).mesh->start[a]; });
+			bool chain = true;
+			int total = 0;
+			for (size_t k = 0; k < comp.size(); k++) {
+				const auto& m = *getBody(comp[k]).mesh;
+				if (k > 0) {
+					const auto& p = *getBody(comp[k - 1]).mesh;
+					chain = chain && m.start[a] == p.start[a] + p.sizes[a];
+					chain = chain && task.bodies.at(comp[k]).odes == task.bodies.at(comp[0]).odes;
+				}
+				total += m.sizes[a];
+			}
+			if (!chain) continue;
+			auto cp = constructionPack<D>(task, comp[0]);
+			cp.sizes[a] = total;
+			auto stack = std::make_shared<HipMesh<D>>(task, comp[0], cp, device);
+			int off = 0;
+			for (size_t id : comp) {
+				Body& m = getBody(id);
+				auto hm = std::dynamic_pointer_cast<HipMesh<D>>(m.mesh);
+				hm->joinStack(stack, a, off);
+				off += hm->sizes[a];
+				m.stack = stack;
+				m.contacts.clear();  // inside the stack: its own rows
+			}
+			getBody(comp[0]).stackLead = true;
+			stackOrder_[comp[0]] = comp;
+		}
+	}
+}
+
+template <int D>
+HipMesh<D>* Engine<D>::unitMesh(Body& b) {
+	if (b.stack) return b.stackLead ? b.stack.get() : nullptr;
+	return &dynamic_cast<HipMesh<D>&>(*b.mesh);
+}
+
 // Engine.cpp:90-121
 template <int D>
 void Engine<D>::nextTimeStep() {
@@ -576,7 +804,9 @@ void Engine<D>::nextTimeStep() {
 					contact.copier->apply(dynamic_cast<HipMesh<D>&>(*body.mesh),
 					                      dynamic_cast<const HipMesh<D>&>(*getBody(contact.neighborId).mesh));
 		for (Body& b : bodies) {
-			HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(*b.mesh);
+			HipMesh<D>* um = unitMesh(b);
+			if (!um) continue;  // a stack member stepped by its lead
+			HipMesh<D>& mesh = *um;
 			if (oneMaxwell(b)) {
 				const auto& tau0 = mesh.deviceTau0();
 				gcmxCheck(gcmx_step_ode(mesh.ctx(), Clock::TimeStep(), nullptr, tau0.data(), (int)tau0.size()),
@@ -584,7 +814,7 @@ void Engine<D>::nextTimeStep() {
 				continue;
 			}
 			std::static_pointer_cast<HipGridCharacteristicMethod<D>>(b.gcm)->step(Clock::TimeStep(), mesh);
-			for (auto& ode : b.odes) ode->apply(*b.mesh, Clock::TimeStep());
+			for (auto& ode : b.odes) ode->apply(mesh, Clock::TimeStep());
 		}
 		return;
 	}
@@ -594,14 +824,16 @@ void Engine<D>::nextTimeStep() {
 		// runs the step (fused where admissible) with the faces' values at
 		// Clock::Time() -- the time all D stages of the reference step see.
 		for (Body& b : bodies) {
-			HipMesh<D>& mesh = dynamic_cast<HipMesh<D>&>(*b.mesh);
+			HipMesh<D>* um = unitMesh(b);
+			if (!um) continue;
+			HipMesh<D>& mesh = *um;
 			if (const gcmx_face_map* fm = b.border->faceMap()) {
 				// partial faces: each face node's own last condition, the whole step in
 				// the library (one pass where admissible), then the ODEs
 				gcmx_face conds[GCMX_MAX_FACE_CONDITIONS];
 				const int n = b.border->conditionsAt(conds);
 				gcmxCheck(gcmx_step_face_map(mesh.ctx(), Clock::TimeStep(), fm, n, conds), "gcmx_step_face_map");
-				for (auto& ode : b.odes) ode->apply(*b.mesh, Clock::TimeStep());
+				for (auto& ode : b.odes) ode->apply(mesh, Clock::TimeStep());
 				continue;
 			}
 			gcmx_face f[6];
@@ -613,7 +845,7 @@ void Engine<D>::nextTimeStep() {
 				continue;
 			}
 			gcmxCheck(gcmx_step_faces(mesh.ctx(), Clock::TimeStep(), f), "gcmx_step_faces");
-			for (auto& ode : b.odes) ode->apply(*b.mesh, Clock::TimeStep());
+			for (auto& ode : b.odes) ode->apply(mesh, Clock::TimeStep());
 		}
 		return;
 	}
@@ -625,8 +857,10 @@ void Engine<D>::nextTimeStep() {
 					contact.copier->apply(dynamic_cast<HipMesh<D>&>(*body.mesh),
 					                      dynamic_cast<const HipMesh<D>&>(*getBody(contact.neighborId).mesh));
 		for (Body& body : bodies) {
-			body.gcm->stage(stage, Clock::TimeStep(), *body.mesh);
-			body.mesh->swapCurrAndNextPdeTimeLayer(0);
+			HipMesh<D>* um = unitMesh(body);
+			if (!um) continue;
+			body.gcm->stage(stage, Clock::TimeStep(), *um);
+			um->swapCurrAndNextPdeTimeLayer(0);
 		}
 	}
 	applyOdes();
@@ -635,8 +869,11 @@ void Engine<D>::nextTimeStep() {
 // Engine.cpp:115-119: ODEs after all stages of the step.
 template <int D>
 void Engine<D>::applyOdes() {
-	for (Body& body : bodies)
-		for (auto& ode : body.odes) ode->apply(*body.mesh, Clock::TimeStep());
+	for (Body& body : bodies) {
+		HipMesh<D>* um = unitMesh(body);
+		if (!um) continue;
+		for (auto& ode : body.odes) ode->apply(*um, Clock::TimeStep());
+	}
 }
 
 template <int D>

@@ -13,6 +13,7 @@
 // through include/gcmx.h; the host keeps set-up and the time loop.
 #pragma once
 
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -167,7 +168,28 @@ public:
 	const std::vector<uint8_t>& materialIdsAll() const { return matIdAll_; }
 	const std::vector<int>& materialNumbers() const { return materialNumbers_; }
 
+	/// STACKS.  3-D bodies stacked along y or z whose every contact is an adhesion
+	/// contact over a whole face (equal sizes and starts on the other two axes)
+	/// run as ONE grid, the stack: ContactCopier::apply fills a body's ghost layers
+	/// at the contact with the neighbour's current layer right before the stage of
+	/// the contact's axis (Engine.cpp:99-107, ContactConditions.hpp:56-68) -- what
+	/// the stack's stage reads there anyway -- so every inner node is bitwise that
+	/// of the separate bodies (TestEngine.cpp:27-87 pins split == unsplit), and the
+	/// step keeps the one-pass kernel instead of three per-stage passes.  A member
+	/// keeps its own host data (set-up, materials, snapshots) and reads its part of
+	/// the stack's device layers; the stack is a HipMesh over the combined box.
+	void joinStack(const std::shared_ptr<HipMesh<D>>& stack, int axis, int offset);
+	const std::shared_ptr<HipMesh<D>>& stackMesh() const { return stack_; }
+	/// A stack member's DefaultMesh::setUpPde, host half only (the stack uploads).
+	HostState<D> setUpMember(const Task& task);
+	/// The stack's set-up from its members' host states, members in stack order.
+	void setUpStack(const std::vector<std::shared_ptr<HipMesh<D>>>& members,
+	                const std::vector<HostState<D>>& states);
+
 private:
+	std::shared_ptr<HipMesh<D>> stack_;  // set for a stack member
+	int stackAxis_ = -1, stackOffset_ = 0;
+	bool ownsCtx_ = true;
 	gcmx_ctx* ctx_ = nullptr;
 	int device;
 	real maximalEigenvalue = 0;
@@ -379,6 +401,8 @@ private:
 	struct Body {
 		std::shared_ptr<AbstractFactoryBase<D>> factory;
 		std::shared_ptr<AbstractMesh<D>> mesh;
+		std::shared_ptr<HipMesh<D>> stack;  // the stack this body belongs to (HipMesh::joinStack)
+		bool stackLead = false;             // the member that steps the stack
 		std::shared_ptr<GridCharacteristicMethodBase> gcm;
 		std::shared_ptr<AbstractBorderConditions> border;
 		struct Contact {
@@ -391,10 +415,15 @@ private:
 		std::vector<std::shared_ptr<Snapshotter>> snapshotters;
 	};
 	std::vector<Body> bodies;
+	std::map<size_t, std::vector<size_t>> stackOrder_;  // lead id -> member ids along the stack axis
 	int device;
 	Body& getBody(size_t id);
 	const Body& getBody(size_t id) const;
 	void createGridsAndContacts(const Task& task);
+	void buildStacks(const Task& task);
+	/// The mesh a body's step runs on: its own, its stack's (the lead member), or
+	/// none (the other members of a stack).
+	HipMesh<D>* unitMesh(Body& b);
 	void applyOdes();
 };
 
