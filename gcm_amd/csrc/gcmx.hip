@@ -877,10 +877,19 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 	c->layer_elems = (size_t)c->M * (size_t)g.cs;
 
 	const size_t bytes = c->layer_elems * sizeof(double);
-	// Layers: two allocations, or (GCMX_LAYER_GAP = bytes, measurement only) one
-	// allocation holding layer A, `gap` bytes (rounded to 256), then layer B.
-	long long gap = -1;
-	if (const char* e = std::getenv("GCMX_LAYER_GAP")) gap = round_up(std::max(0LL, std::atoll(e)), 256);
+	// Layers: ONE allocation holding layer A, a 2 MiB gap, then layer B (both
+	// 2 MiB-aligned: a layer is a whole number of 2 MiB fragments whenever its size
+	// is).  Measured on one MI355X, fresh processes back to back (profiles/r4/swing):
+	// the 512^3 step 4.198-4.200 ms with gaps of 0 / 4 KiB / 64 KiB / 2 MiB
+	// against 4.243-4.259 ms for two separate allocations (nine processes) --
+	// where the two layers lie relative to each other in HBM moves the streaming
+	// step by ~1 %.  GCMX_LAYER_GAP = bytes (rounded to 256) sets the gap, < 0
+	// gives two separate allocations (measurement only).
+	long long gap = 2LL << 20;
+	if (const char* e = std::getenv("GCMX_LAYER_GAP")) {
+		const long long v = std::atoll(e);
+		gap = v < 0 ? -1 : round_up(v, 256);
+	}
 	bool alloc_ok;
 	if (gap >= 0) {
 		alloc_ok = hipMalloc(&c->layers_block, 2 * bytes + (size_t)gap) == hipSuccess;

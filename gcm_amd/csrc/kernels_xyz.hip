@@ -487,7 +487,14 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// wave-uniform by readfirstlane, so the tables live in SGPRs like the
 	// homogeneous step's kernel-argument tables (as plain loads they took 26
 	// VGPRs each and the HET kernel sat at 252 VGPRs)
+#ifndef GCMX_HET_RFL
+#define GCMX_HET_RFL 1
+#endif
+#if GCMX_HET_RFL
 	auto mt = [&](unsigned k) -> IsoAxis { return iso_uniform(mtab[k]); };
+#else
+	auto mt = [&](unsigned k) -> const IsoAxis& { return mtab[k]; };
+#endif
 	auto ghost = [&](int f, int t, int pos, int j, double v) -> double {
 		if (fb.map[f]) {
 			const int xx = (t == 1 && !two) ? x : (t == 0 && !one) ? x + 1 : x + t;

@@ -38,7 +38,7 @@ run trace rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o 
 run bare3 python bench.py $BA
 run prio env GCMX_STREAM_PRIO=normal python bench.py $BA
 for g in 1 2 4 8; do run pre$g python bench.py $BA --prealloc-gb $g; done
-for gap in 0 4096 65536 2097152 1073741824; do run gap$gap env GCMX_LAYER_GAP=$gap python bench.py $BA; done
+for gap in -1 0 4096 65536 2097152 1073741824; do run gap$gap env GCMX_LAYER_GAP=$gap python bench.py $BA; done
 run emu8 python bench.py --emulate-slabs 8 --steps 5 --reps 2
 run bare4 python bench.py $BA
 run trace2 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace2 -o run -- python3 bench.py $BA
