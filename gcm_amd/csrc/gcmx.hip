@@ -149,6 +149,7 @@ struct gcmx_ctx {
 	int channels_per_peer = -1;     // NCCL_NCHANNELS_PER_PEER in effect (0: RCCL's default)
 	int nranks = 1, rank = 0, left = -1, right = -1;
 	bool halo_pending = false;     // an exchange is in flight on comm_stream (ev_halo)
+	bool step_posted = false;      // the current step posted its new boundary planes already
 	bool halo_fresh = false;       // the current layer's ghost planes hold its neighbours' planes
 	double* halo_layer = nullptr;  // the layer the pending exchange fills
 	std::vector<int> halo_comps;
@@ -1203,11 +1204,13 @@ struct SlabJoin {
 // `fb`: y/z face conditions (x faces already filled in memory), or null.
 // `final`: the step's result is the new state (no separate ODE pass follows).
 // Only then may the boundary-first / X-slab schedules post the exchange of the
-// new boundary planes inside the step; otherwise the next step's halo_ensure
-// posts it after the ODE pass.  So every rank posts exactly once per step
-// whatever it decides locally (ODE folded or not, one-pass or per-stage path),
-// and the neighbours' posts pair up (a rank posting a second
-// generation after a non-folded ODE mismatched RCCL's send/recv counts).
+// new boundary planes inside the step (step_posted); otherwise end_step posts
+// the finished layer.  Every step API call thus ends with exactly one post of
+// the new state, whatever the rank decided locally (ODE folded or not, one-pass
+// or per-stage path, schedule), so the neighbours' posts pair up step by step
+// and at the final gcmx_sync (a rank posting a second generation
+// after a non-folded ODE mismatched RCCL's send/recv counts; a rank posting one
+// step later than its neighbour left the last wait unmatched).
 gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb, bool final) {
 	gcmx_status s = GCMX_OK;
 	// One pass per step (k_fused_xyz: cur -> nxt, then swap).  Ghost planes of
@@ -1254,6 +1257,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb, bool final) {
 			s = halo_post(c);
 			std::swap(c->cur, c->nxt);
 			if (s) return s;
+			c->step_posted = true;
 		}
 		ok = ok && xyz("fused_xyz", bs, X - bs, c->stream, c->rows_per_block);
 	} else if (sched == GCMX_SCHED_XSLAB && X >= 4 * bs) {
@@ -1290,6 +1294,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb, bool final) {
 			s = halo_post(c);
 			std::swap(c->cur, c->nxt);
 			if (s) return s;
+			c->step_posted = true;
 		}
 	} else {
 		if (halo) {
@@ -1308,6 +1313,7 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb, bool final) {
 			s = halo_post(c);
 			std::swap(c->cur, c->nxt);
 			if (s) return s;
+			c->step_posted = true;
 		}
 	}
 	if (!ok) return fail(GCMX_ERR_UNSUPPORTED, "fused path launch failed");
@@ -1345,7 +1351,24 @@ bool ode_foldable(const gcmx_ctx* c, const StepOde& ode) {
 	return ode.on && c->mat_d == nullptr && ode.f.size() == 1 && c->bs <= 2 && c->geo.sizes[2] <= 512;
 }
 
+// Every step API call ends here: the new state's boundary planes are posted
+// unless the one-pass schedule posted them inside the step already.
+gcmx_status end_step(gcmx_ctx* c) {
+	if (!has_halo(c) || c->step_posted) return GCMX_OK;
+	gcmx_status s = halo_wait(c);
+	if (s) return s;
+	return halo_post(c);
+}
+
+gcmx_status step_body(gcmx_ctx* c, double tau, const StepOde& ode);
+
 gcmx_status step_impl(gcmx_ctx* c, double tau, const StepOde& ode) {
+	c->step_posted = false;
+	gcmx_status s = step_body(c, tau, ode);
+	return s ? s : end_step(c);
+}
+
+gcmx_status step_body(gcmx_ctx* c, double tau, const StepOde& ode) {
 	gcmx_status s = build_tables(c, tau);
 	if (s) return s;
 	c->last_ode_fused = false;
@@ -1406,7 +1429,15 @@ int gcmx_last_ode_fused(gcmx_ctx* c) { return c && c->last_ode_fused ? 1 : 0; }
 
 namespace {
 
+gcmx_status step_faces_body(gcmx_ctx* c, double tau, const gcmx_face* faces, const StepOde& ode);
+
 gcmx_status step_faces_impl(gcmx_ctx* c, double tau, const gcmx_face* faces, const StepOde& ode) {
+	c->step_posted = false;
+	gcmx_status s = step_faces_body(c, tau, faces, ode);
+	return s ? s : end_step(c);
+}
+
+gcmx_status step_faces_body(gcmx_ctx* c, double tau, const gcmx_face* faces, const StepOde& ode) {
 	gcmx_status s = GCMX_OK;
 	c->last_ode_fused = false;
 	const int D = c->D;
@@ -1523,10 +1554,21 @@ void gcmx_face_map_destroy(gcmx_face_map* m) {
 	delete m;
 }
 
+static gcmx_status step_face_map_body(gcmx_ctx* c, double tau, const gcmx_face_map* m, int n_cond,
+                                      const gcmx_face* conds);
+
 gcmx_status gcmx_step_face_map(gcmx_ctx* c, double tau, const gcmx_face_map* m, int n_cond,
                                const gcmx_face* conds) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
+	c->step_posted = false;
+	s = step_face_map_body(c, tau, m, n_cond, conds);
+	return s ? s : end_step(c);
+}
+
+static gcmx_status step_face_map_body(gcmx_ctx* c, double tau, const gcmx_face_map* m, int n_cond,
+                                      const gcmx_face* conds) {
+	gcmx_status s = GCMX_OK;
 	if (!std::isfinite(tau)) return fail(GCMX_ERR_INVALID_ARG, "non-finite time step");
 	if (!m || m->ctx != c) return fail(GCMX_ERR_INVALID_ARG, "face map of another context");
 	if (n_cond < 0 || n_cond > kMaxFaceConds || (n_cond > 0 && !conds))

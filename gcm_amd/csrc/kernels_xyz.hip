@@ -297,31 +297,6 @@ __device__ __forceinline__ void waterfall(unsigned key, F f) {
 	}
 }
 
-// A double / int made wave-uniform (SGPR-resident) by v_readfirstlane.
-__device__ __forceinline__ double rfl(double v) {
-	const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-	const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
-	const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
-	return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ IsoAxis iso_uniform(const IsoAxis& t) {
-	IsoAxis r;
-	r.a = rfl(t.a);
-	r.b = rfl(t.b);
-	r.g = rfl(t.g);
-	r.p1 = rfl(t.p1);
-	r.p2 = rfl(t.p2);
-	r.s = rfl(t.s);
-#pragma unroll
-	for (int i = 0; i < 3; i++) {
-		r.c1[i] = rfl(t.c1[i]);
-		r.c2[i] = rfl(t.c2[i]);
-	}
-	r.kf1 = __builtin_amdgcn_readfirstlane(t.kf1);
-	r.kf2 = __builtin_amdgcn_readfirstlane(t.kf2);
-	return r;
-}
-
 // Component held in window slot q of a stage whose window mask is `mask`.
 __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 	int n = 0;
@@ -418,6 +393,10 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	__shared__ double eg[NB ? 2 : 1][NB ? NW : 1][2][NB ? 2 : 1][NB ? NWZ : 1][BS];  // [row&1][wave][side][node][comp][k]
 	__shared__ int rdy[NB ? NW : 1];                                               // last row whose edges are in eg
 	__shared__ double cl[BS + 1][2][NCY][ZT];  // node-only Y components, rows y..y+BS (ring)
+	// HET: the first kHetLds materials' tables in LDS (short-latency reads of the
+	// table a waterfall pass picks; higher ids read global memory)
+	constexpr int kHetLds = 16;
+	__shared__ IsoAxis hlds[HET ? kHetLds : 1];
 
 	const int z = threadIdx.x;
 	const int Y = g.sizes[1], Z = g.sizes[2];
@@ -479,22 +458,13 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 	auto stz = [&](int c, int t, int y, double v) { out_p.st_nt(c, plane + (unsigned)y * sty + zo + (unsigned)t * stx, v); };
 #endif
-	// ghost value of component j on face f: -inner + 2 f(t) if overridden, else the mirror
-	// ghost value of component j of node x + t on face f: a face with a per-node map
-	// (partial faces) takes the face node's own condition (none: the ghost stays 0);
+	// per-material table k (k wave-uniform: waterfall); the first kHetLds
+	// materials come from the LDS copy made at kernel start, the rest from HBM
+	auto mt = [&](unsigned k) -> const IsoAxis& { return k < (unsigned)kHetLds ? hlds[k] : mtab[k]; };
+	// ghost value of component j of node x + t on face f: -inner + 2 f(t) if
+	// overridden, else the mirror; a face with a per-node map (partial faces)
+	// takes the face node's own condition (none: the ghost stays 0);
 	// pos = the node's z (y faces) or y (z faces)
-	// per-material table k (wave-uniform: waterfall) with every field made
-	// wave-uniform by readfirstlane, so the tables live in SGPRs like the
-	// homogeneous step's kernel-argument tables (as plain loads they took 26
-	// VGPRs each and the HET kernel sat at 252 VGPRs)
-#ifndef GCMX_HET_RFL
-#define GCMX_HET_RFL 1
-#endif
-#if GCMX_HET_RFL
-	auto mt = [&](unsigned k) -> IsoAxis { return iso_uniform(mtab[k]); };
-#else
-	auto mt = [&](unsigned k) -> const IsoAxis& { return mtab[k]; };
-#endif
 	auto ghost = [&](int f, int t, int pos, int j, double v) -> double {
 		if (fb.map[f]) {
 			const int xx = (t == 1 && !two) ? x : (t == 0 && !one) ? x + 1 : x + t;
@@ -650,11 +620,12 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			u1_apply<0>(A, rr[t], xr[t]);
 		}
 	};
-	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9]) {
+	// HET: the two nodes' materials of row r as one key (node x in bits 0-7)
+	auto key_of = [&](int r) -> unsigned { return mat_of(0, r) | (mat_of(1, r) << 8); };
+	// key: key_of(r), loaded ahead by the caller (HET)
+	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9], unsigned key) {
 		PairWin wc;
 		double cv[2][9];
-		unsigned key = 0;
-		if constexpr (HET) key = mat_of(0, r) | (mat_of(1, r) << 8);
 		pair_load(P2{}, wc, r);
 		cv_load(cv, r);
 		sched_fence();
@@ -669,6 +640,16 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 
 	double win[2][NWY][W];
+	// HET: material keys of the window's rows (slot k: row y - BS + k), each loaded
+	// once, one row ahead of its X stage, and reused by that row's Y and Z stages
+	unsigned hk[W];
+#pragma unroll
+	for (int k = 0; k < W; k++) hk[k] = 0;
+	if constexpr (HET) {  // tables into LDS (het tables are allocated for 256 materials)
+		for (int i = z; i < kHetLds * (int)(sizeof(IsoAxis) / 4); i += ZT)
+			reinterpret_cast<unsigned*>(hlds)[i] = reinterpret_cast<const unsigned*>(mtab)[i];
+		__syncthreads();
+	}
 	// node-only Y components: ring slot of row r; per-lane pointer with the
 	// (node, component) part as a constant LDS offset
 	auto cl_at = [&](int r) { return &cl[(r + BS) % (BS + 1)][0][0][z]; };
@@ -707,8 +688,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		double xr[2][9];
 		if (r >= 0 && r < Y) {
 			XPre pre;
+			if constexpr (HET) hk[k] = key_of(r);
 			x_load_ahead(pre, r);
-			x_stage(pre, r, xr);
+			x_stage(pre, r, xr, hk[k]);
 		} else {
 #pragma unroll
 			for (int t = 0; t < 2; t++)
@@ -744,7 +726,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cp[(t * NCY + wslot(CMY, j)) * ZT]; },
 				    yv[t]);
 			};
-			if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mt(k)); });
+			if constexpr (HET) waterfall(t ? hk[BS] >> 8 : hk[BS] & 255u, [&](unsigned k) { go(mt(k)); });
 			else go(AY);
 		}
 	};
@@ -836,7 +818,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				    A, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
 				    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
 		};
-		if constexpr (HET) waterfall(mat_of(t, y), [&](unsigned k) { go(mt(k)); });
+		if constexpr (HET) waterfall(t ? hk[BS] >> 8 : hk[BS] & 255u, [&](unsigned k) { go(mt(k)); });
 		else go(AZ);
 		if (fb.ode_on) {  // MaxwellViscosityOde: sigma *= exp(-tau / tau0), the stored product (Ode.hpp:34-35)
 #pragma unroll
@@ -848,16 +830,21 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		}
 	};
 	// X stage of row y+BS+1 -> window slot W-1 (ghost rows: zero, or the y+ face's mirror)
-	auto x_enter = [&](int y, const XPre& pre) {
+	auto x_enter = [&](int y, const XPre& pre, unsigned kn) {
 #pragma unroll
 		for (int t = 0; t < 2; t++)
 #pragma unroll
 			for (int q = 0; q < NWY; q++)
 #pragma unroll
 				for (int o = 0; o < W - 1; o++) win[t][q][o] = win[t][q][o + 1];
+		if constexpr (HET) {
+#pragma unroll
+			for (int o = 0; o < W - 1; o++) hk[o] = hk[o + 1];
+			hk[W - 1] = kn;
+		}
 		double xr[2][9];
 		sched_fence();
-		x_stage(pre, clamp_row(y + BS + 1), xr);
+		x_stage(pre, clamp_row(y + BS + 1), xr, kn);
 		push(xr, W - 1, y + BS + 1);
 		sched_fence();
 		if constexpr (FACES) {
@@ -872,6 +859,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		double yv[2][9];
 		XPre pre;
 		const int rn = clamp_row(y + BS + 1);
+		unsigned kn = 0;  // HET: row rn's materials, one row ahead of its X stage
+		if constexpr (HET) kn = key_of(rn);
 		y_stage(y, yv);
 		TX2_T(0);
 		publish(y, yv);
@@ -900,7 +889,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			z_stage_store(t, y, yv);
 		}
 		TX2_T(3);
-		x_enter(y, pre);
+		x_enter(y, pre, kn);
 		TX2_T(5);
 	};
 	for (int y = yb; y < ye; y++) row(y);

@@ -499,7 +499,8 @@ HipBorderConditions<D>::HipBorderConditions(const Task& task, const HipMesh<D>& 
 		for (int e : eff) uniform = uniform && e == eff[0];
 		faceCondition[f] = eff.empty() ? -1 : eff[0];
 	}
-	if (!uniform && conditions.size() <= GCMX_MAX_FACE_CONDITIONS) {
+	const char* noMaps = std::getenv("GCMX_NO_FACE_MAPS");  // 1: node lists only
+	if (!uniform && conditions.size() <= GCMX_MAX_FACE_CONDITIONS && !(noMaps && std::atoi(noMaps) != 0)) {
 		// partial faces: each face node's last condition, as one byte per face node
 		std::array<std::vector<uint8_t>, 6> maps;
 		const uint8_t* ptr[6] = {};

@@ -18,3 +18,8 @@ for i in 1 2; do
   timeout -k 10 200 python bench.py --steps 20 --warmup 5 --reps 5 --no-cpu-baseline > $OUT/bench$i.json 2> $OUT/bench$i.err || exit 1
   python3 -c "import json;d=json.load(open('$OUT/bench$i.json'));r=d['roofline'];print(d['ms_per_step'],r['kernel_avg_ms'],r['frac'],d['process_state']['layers']['one_allocation'],d['process_state']['clock'])"
 done
+# x-marching access-pattern probe beside the copy and the 2-plane pattern
+XM_ONLY=1 timeout -k 10 120 ./tools/xyz_probe > $OUT/xyz_probe_xm.txt 2>&1; echo "probe rc=$?"; cat $OUT/xyz_probe_xm.txt
+# heterogeneous one-pass step at 256^3 (two materials, free surfaces), the verdict's 0.85 ms
+timeout -k 10 200 python scripts/bench_physics.py --n 256 --layers --steps 20 > $OUT/het256.json 2> $OUT/het256.err; cat $OUT/het256.json
+timeout -k 10 200 python scripts/bench_physics.py --n 256 --steps 20 > $OUT/free256.json 2> $OUT/free256.err; cat $OUT/free256.json

@@ -191,7 +191,7 @@ def test_engine_border_conditions_time_dependent(H):
                                                "Syz": lambda t: 0.0}),
                            (0, ("cylinder", 3, (0, 4, 6), (20, 4, 6)), {"Vx": f})]})
     oe, he = run_both(H, s3)
-    assert he.path(0) == "split"
+    assert he.path(0) == "fused"  # the cylinder covers part of face x-: a face map
     assert_bodies_equal(oe, he, s3)
 
 
@@ -315,8 +315,9 @@ def test_engine_snapshotters(H, tmp_path, monkeypatch):
         assert open(stem % "detector" + ".txt").read() == want
 
 
-def ystack(bodies_sizes, axis=1, materials=None, maxwell=False):
-    """3-D bodies stacked along `axis` (adhesion contacts over whole faces)."""
+def ystack(bodies_sizes, axis=1, materials=None, maxwell=False, at=None):
+    """3-D bodies stacked along `axis` (adhesion contacts over whole faces), a
+    pressure sphere centred at `at` along it (default: 1.5 before the first contact)."""
     X, Y, Z = 10, 12, 64
     cubics, off = {}, 0
     for i, w in enumerate(bodies_sizes):
@@ -325,7 +326,7 @@ def ystack(bodies_sizes, axis=1, materials=None, maxwell=False):
         cubics[i] = (sz, st)
         off += w
     c = [X / 2, Y / 2, Z / 2]
-    c[axis] = bodies_sizes[0] - 1.5
+    c[axis] = bodies_sizes[0] - 1.5 if at is None else at
     return spec(3, 2, [1, 1, 1], cubics, 0.9, (4, 2, 1), snaps=5,
                 inhomogeneities=materials or [],
                 quantities=[(("sphere", 5.0, tuple(c)), "PRESSURE", 10.0)],
@@ -352,7 +353,7 @@ def test_engine_stack_equals_one_body(H, monkeypatch, axis, widths):
         got = inner(he.pde(b.id), 2, 3)
         want = inner(b.pde.reshape(he.pde(b.id).shape), 2, 3)
         assert np.array_equal(got, want), f"body {b.id}: {int((got != want).sum())} differ"
-    one = H.Engine(host_task(ystack([sum(widths)], axis)))
+    one = H.Engine(host_task(ystack([sum(widths)], axis, at=widths[0] - 1.5)))
     one.run()
     whole = inner(one.pde(0), 2, 3)
     parts = np.concatenate([inner(he.pde(i), 2, 3) for i in range(len(widths))], axis=axis)

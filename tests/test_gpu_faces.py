@@ -235,16 +235,20 @@ def test_engine_free_surfaces_one_pass(H):
     assert np.array_equal(got, want), f"{int((got != want).sum())} inner values differ"
 
 
-def test_engine_partial_face_uses_node_lists(H):
-    """A condition covering part of a face (titan's cylinder, ndi.hpp:309-315) keeps
-    the per-stage path with device-resident node lists."""
+@pytest.mark.parametrize("maps", [True, False])
+def test_engine_partial_face_uses_node_lists(H, monkeypatch, maps):
+    """A condition covering part of a face (titan's cylinder, ndi.hpp:309-315):
+    with face maps the one-pass step, with GCMX_NO_FACE_MAPS=1 the per-stage path
+    with device-resident node lists; both bitwise == the oracle."""
+    if not maps:
+        monkeypatch.setenv("GCMX_NO_FACE_MAPS", "1")
     N = 12
     s = spec(3, 2, [1, 1, 1], {0: ([N, N, N], [0, 0, 0])}, 0.9, (4, 2, 1), snaps=4,
              quantities=[(("sphere", 3, (6, 6, 6)), "PRESSURE", 1.0)],
              borders={0: [(1, ("infinite",), {q: (lambda t: 0.0) for q in FREE[1]}),
                           (1, ("cylinder", 2.5, (6, -5, 6), (6, 20, 6)), {"Vy": lambda t: -0.3})]})
     oe, he = run_both(H, s)
-    assert he.last_path(0) == "split"
+    assert he.last_path(0) == ("fused" if maps else "split")
     got = he.pde(0)
     want = oe.bodies[0].pde.reshape(got.shape)
     assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"

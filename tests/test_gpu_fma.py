@@ -236,9 +236,10 @@ def test_fma_full_size_512_within_tolerance_of_exact(G):
     assert 0 < r <= TOL, r
 
 
-def _xbodies(widths):
+def _xbodies(widths, cx=None):
     """3-D bodies stacked along x with the given widths (contacts along the
-    stage-0 axis only: the engine's one-pass path), pressure sphere across them."""
+    stage-0 axis only: the engine's one-pass path), pressure sphere across them
+    centred at global x = cx (default: 1.5 left of the first contact)."""
     from tests.taskspec import spec
     Y, Z = 20, 64
     cubics, x0 = {}, 0
@@ -246,7 +247,8 @@ def _xbodies(widths):
         cubics[i] = ([w, Y, Z], [x0, 0, 0])
         x0 += w
     return spec(3, 2, [1, 1, 1], cubics, 0.9, (4, 2, 1), snaps=6,
-                quantities=[(("sphere", 6.0, (widths[0] - 1.5, Y / 2, Z / 2)), "PRESSURE", 10.0)])
+                quantities=[(("sphere", 6.0, (widths[0] - 1.5 if cx is None else cx, Y / 2, Z / 2)),
+                                "PRESSURE", 10.0)])
 
 
 @pytest.mark.parametrize("widths", [[12, 12], [7, 5, 12], [9, 8, 7]])
@@ -262,7 +264,7 @@ def test_fma_engine_xbodies_equal_one_body(G, monkeypatch, widths):
     split = H.Engine(host_task(_xbodies(widths)))
     split.run()
     assert all(split.last_path(i) == "fused" for i in range(len(widths)))
-    one = H.Engine(host_task(_xbodies([sum(widths)])))
+    one = H.Engine(host_task(_xbodies([sum(widths)], cx=widths[0] - 1.5)))
     one.run()
     parts = [split.pde(i)[2:-2, 2:-2, 2:-2] for i in range(len(widths))]
     whole = one.pde(0)[2:-2, 2:-2, 2:-2]
@@ -284,7 +286,7 @@ def test_fma_step_ode_fused_equals_step_then_ode(G, faces):
     stores multiplies the same values the separate pass would), and within the
     tolerance of the oracle's stages + MaxwellViscosityOde (Ode.hpp:28-37)."""
     import math
-    q = G.QUANTITY_CODES
+    from gcm_amd.gcmx import QUANTITY_CODES as q
     fc = [[(q["Sxx"], 0.0), (q["Sxy"], 0.0), (q["Sxz"], 0.0)], None,
           [(q["Syy"], -0.3), (q["Syz"], 0.0)], [(q["Vy"], 0.1)],
           [(q["Szz"], 0.0), (q["Sxz"], 0.0), (q["Syz"], 0.0)], None] if faces else None

@@ -152,6 +152,107 @@ __global__ __launch_bounds__(512, 2) void k_probe_tx(const double* __restrict__ 
 	if (!STORE && acc == 1234.5) out[0] = acc;
 }
 
+// x-marching: a block is a tile of TYB = TY + 2*BS y rows
+// (one wave each) x 64 z lanes, marching x over XC planes.  Each lane keeps the
+// X window (planes x-BS..x+BS of the 6 window components) in registers and loads
+// ONE new plane per x step (6 window + 3 node-only components: 9 loads); the X
+// results go to LDS, the Y stage of the TY inner rows reads rows y-BS..y+BS from
+// LDS, the Z stage reads z-BS..z+BS of the Y results from LDS, and the 60 inner
+// lanes of the TY inner rows store (z tiles overlap by 2*BS columns: the X and Y
+// stages of the halo rows / columns are recomputed, the stores start at
+// unaligned 60-column offsets).  Loads per stored node: 9 * TYB/TY * 64/60 plus
+// the 2*BS-plane x prologue per chunk.  Trivial arithmetic.
+template <int TY, int XC>
+__global__ __launch_bounds__(64 * (TY + 2 * BS)) void k_probe_xm(const double* __restrict__ in,
+                                                                 double* __restrict__ out) {
+	constexpr int TYB = TY + 2 * BS, ZO = 64 - 2 * BS, W = 2 * BS + 1;
+	__shared__ double xs[6][TYB][64];
+	__shared__ double ys[6][TY][64];
+	const int lane = threadIdx.x & 63, row = threadIdx.x >> 6;
+	const int ntz = (N + ZO - 1) / ZO, nty = (N + TY - 1) / TY;
+	const int b = blockIdx.x;
+	const int tz = b % ntz, ty = (b / ntz) % nty, tx = b / (ntz * nty);
+	const int z = tz * ZO - BS + lane, y = ty * TY - BS + row, x0 = tx * XC;
+	const bool zin = z >= 0 && z < N, yin = y >= 0 && y < N;
+	const int zc = zin ? z : (z < 0 ? 0 : N - 1), yc = yin ? y : (y < 0 ? 0 : N - 1);
+	const long long col = ORIGIN + (long long)yc * STY + zc;
+	double win[6][W];
+#pragma unroll
+	for (int k = 0; k < W - 1; k++)  // prologue: planes x0-BS .. x0+BS-1
+#pragma unroll
+		for (int c = 0; c < 6; c++) win[c][k + 1] = in[c * CS + col + (long long)(x0 - BS + k) * STX];
+	for (int x = x0; x < x0 + XC; x++) {
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+#pragma unroll
+			for (int k = 0; k < W - 1; k++) win[c][k] = win[c][k + 1];
+			win[c][W - 1] = in[c * CS + col + (long long)(x + BS) * STX];
+		}
+		double node[3];
+#pragma unroll
+		for (int c = 0; c < 3; c++) node[c] = in[(6 + c) * CS + col + (long long)x * STX];
+		__syncthreads();
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			double s = 0;
+#pragma unroll
+			for (int k = 0; k < W; k++) s += win[c][k];
+			xs[c][row][lane] = s;
+		}
+		__syncthreads();
+		const bool inner_row = row >= BS && row < BS + TY;
+		double yv[6];
+		if (inner_row) {
+#pragma unroll
+			for (int c = 0; c < 6; c++) {
+				double s = 0;
+#pragma unroll
+				for (int k = -BS; k <= BS; k++) s += xs[c][row + k][lane];
+				yv[c] = s;
+				ys[c][row - BS][lane] = s;
+			}
+		}
+		__syncthreads();
+		const bool store = inner_row && lane >= BS && lane < 64 - BS && zin && yin;
+		if (store) {
+			const long long o = col + (long long)x * STX;
+#pragma unroll
+			for (int c = 0; c < 6; c++) {
+				double s = yv[c];
+#pragma unroll
+				for (int k = -BS; k <= BS; k++)
+					if (k) s += ys[c][row - BS][lane + k];
+				__builtin_nontemporal_store(s, out + c * CS + o);
+			}
+#pragma unroll
+			for (int c = 0; c < 3; c++) __builtin_nontemporal_store(node[c], out + (6 + c) * CS + o);
+		}
+	}
+}
+
+template <int TY, int XC>
+void xmarch(const double* in, double* out) {
+	const double nodes = (double)N * N * N;
+	constexpr int ZO = 64 - 2 * BS;
+	const int ntz = (N + ZO - 1) / ZO, nty = (N + TY - 1) / TY;
+	dim3 grid(ntz * nty * (N / XC));
+	hipEvent_t a, b;
+	CK(hipEventCreate(&a));
+	CK(hipEventCreate(&b));
+	for (int r = 0; r < 11; r++) {
+		if (r == 1) CK(hipEventRecord(a));
+		hipLaunchKernelGGL((k_probe_xm<TY, XC>), grid, dim3(64 * (TY + 2 * BS)), 0, 0, in, out);
+	}
+	CK(hipEventRecord(b));
+	CK(hipEventSynchronize(b));
+	float ms = 0;
+	CK(hipEventElapsedTime(&ms, a, b));
+	ms /= 10;
+	const double loads = 9.0 * (TY + 2 * BS) / TY * 64.0 / ZO * (XC + 2.0 * BS * 6.0 / 9.0) / XC;
+	std::printf("x-march TY %2d (+%d halo rows) XC %3d: %.2f loads/node: %.3f ms (%.0f GB/s)\n", TY, 2 * BS, XC,
+	            loads, ms, 144.0 * nodes / (ms * 1e6));
+}
+
 template <int TX, int KOPS, bool BAR = false>
 void ops_tx(const double* in, double* out, int chunk, size_t shm = 0) {
 	const double nodes = (double)N * N * N;
@@ -234,6 +335,15 @@ int main() {
 	CK(hipMalloc(&out, bytes));
 	CK(hipMemset(in, 0, bytes));
 	CK(hipMemset(out, 0, bytes));
+	if (std::getenv("XM_ONLY")) {  // the x-marching family beside the copy and the 2-plane pattern
+		family<1, 1>(in, out, 128);
+		family_tx<2>(in, out, 128);
+		xmarch<12, 64>(in, out);
+		xmarch<12, 128>(in, out);
+		xmarch<8, 128>(in, out);
+		xmarch<4, 128>(in, out);
+		return 0;
+	}
 	family<1, 1>(in, out, 128);
 	family<2, 1>(in, out, 128);
 	family<2, 2>(in, out, 128);
