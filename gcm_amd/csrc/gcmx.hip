@@ -706,8 +706,8 @@ void refresh_fast(gcmx_ctx* c) {
 		                        &c->L[(size_t)sx * M], c->iso[sx]);
 	c->iso_fast = fits;
 	// heterogeneous one-pass step: per-node ids and every material of the structure
-	bool het = !fits && D == 3 && c->mat_d != nullptr && c->n_mat >= 1 && fast_layout_ok(c->geo) &&
-	           het_supported(c->geo);
+	bool het = !fits && D == 3 && c->mat_d != nullptr && c->n_mat >= 1 && c->n_mat <= kHetMaxMaterials &&
+	           fast_layout_ok(c->geo) && het_supported(c->geo);
 	for (int m = 0; het && m < c->n_mat; m++)
 		for (int sx = 0; het && sx < D; sx++) {
 			IsoAxis tmp{};

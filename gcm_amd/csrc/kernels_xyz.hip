@@ -283,6 +283,21 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	} while (0)
 #endif
 
+// Timing knobs (A/B builds only; the defaults are the product): per-node face
+// maps compiled into the FACES ghosts; face values read from LDS instead of the
+// kernel arguments; HET_AB 1 = every material uses the kernel-argument table,
+// 2 = also no material-id loads (both give wrong HET results: timing only).
+#ifndef GCMX_TX2_FACEMAP
+#define GCMX_TX2_FACEMAP 1
+#endif
+#ifndef GCMX_TX2_FACE_LDS
+#define GCMX_TX2_FACE_LDS 0
+#endif
+#ifndef GCMX_HET_AB
+#define GCMX_HET_AB 0
+#endif
+
+
 // Runs f(k) once for every distinct key among the active lanes, with k uniform
 // (an SGPR value: per-material tables indexed by it are scalar loads), every lane
 // inside the call whose key is k.  One pass when the wave's key is uniform.
@@ -393,10 +408,12 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	__shared__ double eg[NB ? 2 : 1][NB ? NW : 1][2][NB ? 2 : 1][NB ? NWZ : 1][BS];  // [row&1][wave][side][node][comp][k]
 	__shared__ int rdy[NB ? NW : 1];                                               // last row whose edges are in eg
 	__shared__ double cl[BS + 1][2][NCY][ZT];  // node-only Y components, rows y..y+BS (ring)
-	// HET: the first kHetLds materials' tables in LDS (short-latency reads of the
-	// table a waterfall pass picks; higher ids read global memory)
-	constexpr int kHetLds = 16;
-	__shared__ IsoAxis hlds[HET ? kHetLds : 1];
+	// HET: every material's tables in LDS (<= kHetMaxMaterials, host-checked).  A
+	// global (or flat: LDS-or-global) table load in the row loop would count in
+	// vmcnt, and waiting for it would wait for every row-ahead load issued before
+	// it -- the software pipeline collapses (measured: HET 256^3 +34 %).
+	__shared__ IsoAxis hlds[HET ? kHetMaxMaterials : 1];
+	__shared__ double flds[FACES && GCMX_TX2_FACE_LDS ? 4 : 1][9];  // 2 f(t) of the y/z faces
 
 	const int z = threadIdx.x;
 	const int Y = g.sizes[1], Z = g.sizes[2];
@@ -458,22 +475,52 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 	auto stz = [&](int c, int t, int y, double v) { out_p.st_nt(c, plane + (unsigned)y * sty + zo + (unsigned)t * stx, v); };
 #endif
-	// per-material table k (k wave-uniform: waterfall); the first kHetLds
-	// materials come from the LDS copy made at kernel start, the rest from HBM
-	auto mt = [&](unsigned k) -> const IsoAxis& { return k < (unsigned)kHetLds ? hlds[k] : mtab[k]; };
-	// ghost value of component j of node x + t on face f: -inner + 2 f(t) if
-	// overridden, else the mirror; a face with a per-node map (partial faces)
-	// takes the face node's own condition (none: the ghost stays 0);
-	// pos = the node's z (y faces) or y (z faces)
-	auto ghost = [&](int f, int t, int pos, int j, double v) -> double {
-		if (fb.map[f]) {
+	// per-material table k (k wave-uniform: waterfall), from the LDS copy made at
+	// kernel start
+	// per-material table k (k wave-uniform: waterfall), from the LDS copy made at
+	// kernel start.  Measured alternatives: scalar loads through
+	// the constant address space spill VGPRs; separate one-table / two-table X
+	// paths double the X stage's code; both are slower.
+	auto mt = [&](unsigned k) -> const IsoAxis& {
+		if constexpr (GCMX_HET_AB >= 1) return AX;
+		return hlds[k];
+	};
+	auto two_v = [&](int f, int j) -> double {
+		if constexpr (FACES && GCMX_TX2_FACE_LDS) return flds[f][j];
+		return fb.two_v[f][j];
+	};
+	// The condition of face f at node x + t (pos = the node's z on y faces, its y
+	// on z faces), resolved once per node: the overridden components and their
+	// 2 f(t) (components in `need` only).  A face with a per-node map (partial
+	// faces) takes the face node's own condition; none: the ghost stays 0.
+	struct GhostRule {
+		unsigned mask;
+		bool none;
+		double two[9];
+	};
+	auto ghost_rule = [&](int f, int t, int pos, unsigned need) -> GhostRule {
+		GhostRule r;
+		r.none = false;
+		if (GCMX_TX2_FACEMAP && fb.map[f]) {
 			const int xx = (t == 1 && !two) ? x : (t == 0 && !one) ? x + 1 : x + t;
 			const unsigned c = fb.map[f][(size_t)xx * (f < 2 ? Z : Y) + pos];
-			if (c == kNoFaceCond) return 0.0;
-			const FaceCond& fc = fb.conds[c];
-			return ((fc.mask >> j) & 1u) ? -v + fc.two_v[j] : v;
+			r.none = c == kNoFaceCond;
+			const FaceCond& fc = fb.conds[r.none ? 0u : c];
+			r.mask = r.none ? 0u : fc.mask;
+#pragma unroll
+			for (int j = 0; j < 9; j++)
+				if ((need >> j) & 1u) r.two[j] = r.none ? 0.0 : fc.two_v[j];
+		} else {
+			r.mask = fb.mask[f];
+#pragma unroll
+			for (int j = 0; j < 9; j++)
+				if ((need >> j) & 1u) r.two[j] = two_v(f, j);
 		}
-		return ((fb.mask[f] >> j) & 1u) ? -v + fb.two_v[f][j] : v;
+		return r;
+	};
+	// ghost value of component j: -inner + 2 f(t) if overridden, else the mirror
+	auto ghost = [](const GhostRule& r, int j, double v) -> double {
+		return r.none ? 0.0 : ((r.mask >> j) & 1u) ? -v + r.two[j] : v;
 	};
 
 	const int wv = z >> 6, ln = z & 63;  // wave in block, lane
@@ -621,7 +668,10 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		}
 	};
 	// HET: the two nodes' materials of row r as one key (node x in bits 0-7)
-	auto key_of = [&](int r) -> unsigned { return mat_of(0, r) | (mat_of(1, r) << 8); };
+	auto key_of = [&](int r) -> unsigned {
+		if constexpr (GCMX_HET_AB >= 2) return 0u;
+		return mat_of(0, r) | (mat_of(1, r) << 8);
+	};
 	// key: key_of(r), loaded ahead by the caller (HET)
 	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9], unsigned key) {
 		PairWin wc;
@@ -646,10 +696,15 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll
 	for (int k = 0; k < W; k++) hk[k] = 0;
 	if constexpr (HET) {  // tables into LDS (het tables are allocated for 256 materials)
-		for (int i = z; i < kHetLds * (int)(sizeof(IsoAxis) / 4); i += ZT)
+		for (int i = z; i < kHetMaxMaterials * (int)(sizeof(IsoAxis) / 4); i += ZT)
 			reinterpret_cast<unsigned*>(hlds)[i] = reinterpret_cast<const unsigned*>(mtab)[i];
-		__syncthreads();
 	}
+	if constexpr (FACES && GCMX_TX2_FACE_LDS) {
+#pragma unroll
+		for (int c = 0; c < 36; c++)
+			if (z == c) flds[c / 9][c % 9] = fb.two_v[c / 9][c % 9];
+	}
+	if constexpr (HET || (FACES && GCMX_TX2_FACE_LDS)) __syncthreads();
 	// node-only Y components: ring slot of row r; per-lane pointer with the
 	// (node, component) part as a constant LDS offset
 	auto cl_at = [&](int r) { return &cl[(r + BS) % (BS + 1)][0][0][z]; };
@@ -668,18 +723,20 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// index, resolved by compile-time selects; rare path)
 	auto mirror_slot = [&](int k, int ks, int f) {
 #pragma unroll
-		for (int t = 0; t < 2; t++)
+		for (int t = 0; t < 2; t++) {
+			const GhostRule gr = ghost_rule(f, t, zc, WMY);
 #pragma unroll
 			for (int q = 0; q < NWY; q++) {
 				double v = 0.0;
 #pragma unroll
 				for (int kk = 0; kk < W; kk++)
 					if (kk == ks) v = win[t][q][kk];
-				const double gv = ghost(f, t, zc, wcomp(WMY, q), v);
+				const double gv = ghost(gr, wcomp(WMY, q), v);
 #pragma unroll
 				for (int kk = 0; kk < W; kk++)
 					if (kk == k) win[t][q][kk] = gv;
 			}
+		}
 	};
 	// prologue: X results of rows yb-BS .. yb+BS (rows < 0 or >= Y are ghosts)
 #pragma unroll
@@ -730,6 +787,26 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			else go(AY);
 		}
 	};
+	// z ghosts of row y (FACES): lanes 1..BS form the z- face's ghost columns,
+	// lanes Z-1-BS..Z-2 the z+ face's, put(side, node, window slot, value) -- one
+	// divergent region per face and row, entered only by the waves holding those
+	// lanes, one condition lookup per node
+	auto z_ghosts = [&](int y, const double (&yv)[2][9], auto&& put) {
+		const int wu = __builtin_amdgcn_readfirstlane(z >> 6);
+#pragma unroll
+		for (int side = 0; side < 2; side++) {
+			const int lo = side ? Z - 1 - BS : 1, hi = side ? Z - 2 : BS;
+			if (!((fb.on >> (2 + side)) & 1u) || wu * 64 > hi || wu * 64 + 63 < lo) continue;
+			if (z < lo || z > hi) continue;
+#pragma unroll
+			for (int t = 0; t < 2; t++) {
+				const GhostRule gr = ghost_rule(2 + side, t, y, WMZ);
+#pragma unroll
+				for (int j = 0; j < 9; j++)
+					if ((WMZ >> j) & 1u) put(side, t, wslot(WMZ, j), ghost(gr, j, yv[t][j]));
+			}
+		}
+	};
 	// hand the Y results of row y to the Z stage: NB, own region + edge ring +
 	// counter; otherwise the block buffer between two barriers
 	auto publish = [&](int y, const double (&yv)[2][9]) {
@@ -747,13 +824,13 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 					if ((WMZ >> j) & 1u) {
 						const int q = wslot(WMZ, j);
 						rg[wv][t][q][BS + ln] = yv[t][j];
-						if constexpr (FACES) {  // z ghosts: wave 0's left halo, the last wave's right halo
-							if ((fb.on & 4u) && z >= 1 && z <= BS) rg[0][t][q][BS - z] = ghost(2, t, y, j, yv[t][j]);
-							if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
-								rg[NW - 1][t][q][BS + 2 * (Z - 1) - z - 64 * (NW - 1)] = ghost(3, t, y, j, yv[t][j]);
-						}
 						if (edge) egp[(t * NWZ + q) * BS] = yv[t][j];
 					}
+			if constexpr (FACES)  // z ghosts: wave 0's left halo, the last wave's right halo
+				z_ghosts(y, yv, [&](int side, int t, int q, double v) {
+					if (side == 0) rg[0][t][q][BS - z] = v;
+					else rg[NW - 1][t][q][BS + 2 * (Z - 1) - z - 64 * (NW - 1)] = v;
+				});
 			// edges in LDS before the counter says so (LDS only: global memory keeps flowing)
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			__hip_atomic_store(&rdy[wv], y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -768,13 +845,15 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 						if constexpr (FACES) {
 							// idle lanes leave the z ghost slots to the face (or their zero)
 							if (UNI || z < Z || z >= Z + BS) zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
-							if ((fb.on & 4u) && z >= 1 && z <= BS) zl[t][q][BS - z] = ghost(2, t, y, j, yv[t][j]);
-							if ((fb.on & 8u) && z >= Z - 1 - BS && z <= Z - 2)
-								zl[t][q][BS + 2 * (Z - 1) - z] = ghost(3, t, y, j, yv[t][j]);
 						} else {
 							zl[t][q][BS + z] = live ? yv[t][j] : 0.0;
 						}
 					}
+			if constexpr (FACES)
+				z_ghosts(y, yv, [&](int side, int t, int q, double v) {
+					if (side == 0) zl[t][q][BS - z] = v;
+					else zl[t][q][BS + 2 * (Z - 1) - z] = v;
+				});
 			__syncthreads();
 		}
 	};

@@ -71,6 +71,9 @@ struct FaceCond {
 	unsigned pad_;
 	double two_v[9];
 };
+// Materials of the heterogeneous one-pass step: their tables live in LDS (more
+// materials take the per-stage path).
+constexpr int kHetMaxMaterials = 32;
 constexpr int kMaxFaceConds = 8;  // conditions of one per-node face map (gcmx_face_map)
 constexpr uint8_t kNoFaceCond = 255;
 // Cubic border conditions on the y/z faces, as the one-pass step consumes

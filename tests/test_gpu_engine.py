@@ -41,10 +41,15 @@ def run_both(H, s, steps=None):
     return oe, he
 
 
-def assert_bodies_equal(oe, he, s):
+def assert_bodies_equal(oe, he, s, inner_only=False):
+    """Bitwise equal bodies; inner_only: the inner nodes only -- the one-pass step
+    forms y/z face ghosts in registers and never writes them, while the oracle's
+    ghost layers keep the last per-stage fill (scratch no output reads)."""
     for b in oe.bodies:
         got = he.pde(b.id)
         want = b.pde.reshape(got.shape)
+        if inner_only:
+            got, want = inner(got, s["bs"], s["D"]), inner(want, s["bs"], s["D"])
         assert np.array_equal(got, want), f"body {b.id}: {int((got != want).sum())} values differ"
 
 
@@ -192,7 +197,7 @@ def test_engine_border_conditions_time_dependent(H):
                            (0, ("cylinder", 3, (0, 4, 6), (20, 4, 6)), {"Vx": f})]})
     oe, he = run_both(H, s3)
     assert he.path(0) == "fused"  # the cylinder covers part of face x-: a face map
-    assert_bodies_equal(oe, he, s3)
+    assert_bodies_equal(oe, he, s3, inner_only=True)
 
 
 def test_engine_setup_areas_waves_vectors_3d(H):

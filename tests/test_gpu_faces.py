@@ -251,6 +251,8 @@ def test_engine_partial_face_uses_node_lists(H, monkeypatch, maps):
     assert he.last_path(0) == ("fused" if maps else "split")
     got = he.pde(0)
     want = oe.bodies[0].pde.reshape(got.shape)
+    if maps:  # the one-pass step never writes y/z face ghosts (oracle: scratch)
+        got, want = got[2:-2, 2:-2, 2:-2], want[2:-2, 2:-2, 2:-2]
     assert np.array_equal(got, want), f"{int((got != want).sum())} values differ"
 
 

@@ -395,3 +395,20 @@ def test_heterogeneous_one_pass_step_matches_oracle(G, bs, sizes, layout):
     k = ctx.profile_read()
     assert "HET" in k["fused_xyz"]["kernel"], k
     ctx.close()
+
+
+def test_heterogeneous_many_materials_take_per_stage_path(G):
+    """More materials than the one-pass step keeps in LDS (kHetMaxMaterials = 32):
+    the per-stage path with per-node matrices, still bitwise == the oracle."""
+    mats = tuple((4.0 + 0.1 * i, 2.0, 1.0) for i in range(40))
+    b = oracle_body(3, 2, [6, 12, 64], materials=mats, courant=0.9)
+    random_materials(b, seed=9)
+    random_state(b, seed=10, ghosts=False)
+    ctx = context_for(b)
+    for step in range(2):
+        for s in range(3):
+            b.stage(s, 0.9)
+        ctx.step(0.9)
+        assert ctx.last_path != "fused"
+        assert_same(ctx, b, f"40 materials step {step}")
+    ctx.close()
