@@ -1344,11 +1344,29 @@ gcmx_status ode_factors(gcmx_ctx* c, double tau, const double* tau0, int n_mat, 
 }
 
 gcmx_status ode_apply(gcmx_ctx* c, const std::vector<double>& f);
+gcmx_status ode_upload(gcmx_ctx* c, const std::vector<double>& f);
 
 // The ODE rides in the one-pass step's store epilogue when the step runs
-// k_step_tx2 over one material (the factor is then one number).
+// k_step_tx2: over one material (the factor is one number), or over per-node
+// materials on the heterogeneous one-pass step (per-material factors, each
+// node's own read from LDS).  Call after build_tables (het_ok is per tau).
 bool ode_foldable(const gcmx_ctx* c, const StepOde& ode) {
-	return ode.on && c->mat_d == nullptr && ode.f.size() == 1 && c->bs <= 2 && c->geo.sizes[2] <= 512;
+	if (!ode.on || c->bs > 2 || c->geo.sizes[2] > 512) return false;
+	if (!c->mat_d) return ode.f.size() == 1;
+	return c->iso_het && c->het_ok && (int)ode.f.size() <= kHetMaxMaterials;
+}
+
+// Fills fb's ODE fields for a folded ODE (the HET factors uploaded in stream order).
+gcmx_status ode_fold(gcmx_ctx* c, const StepOde& ode, FaceBC& fb) {
+	fb.ode_on = 1;
+	if (!c->mat_d) {
+		fb.ode = ode.f[0];
+		return GCMX_OK;
+	}
+	gcmx_status s = ode_upload(c, ode.f);
+	if (s) return s;
+	fb.ode_f = c->ode_d;
+	return GCMX_OK;
 }
 
 // Every step API call ends here: the new state's boundary planes are posted
@@ -1381,8 +1399,8 @@ gcmx_status step_body(gcmx_ctx* c, double tau, const StepOde& ode) {
 	}
 	if (ode_foldable(c, ode)) {
 		FaceBC fb{};
-		fb.ode_on = 1;
-		fb.ode = ode.f[0];
+		s = ode_fold(c, ode, fb);
+		if (s) return s;
 		s = fused_step(c, &fb, true);
 		if (s) return s;
 		c->last_ode_fused = true;
@@ -1487,8 +1505,8 @@ gcmx_status step_faces_body(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 			}
 		const bool fold = ode_foldable(c, ode);
 		if (fold) {
-			fb.ode_on = 1;
-			fb.ode = ode.f[0];
+			s = ode_fold(c, ode, fb);
+			if (s) return s;
 		}
 		s = fused_step(c, (fb.on || fold) ? &fb : nullptr, !(ode.on && !fold));
 		if (s) return s;
@@ -1781,6 +1799,19 @@ gcmx_status gcmx_ode_maxwell(gcmx_ctx* c, double tau, const double* tau0, int n_
 namespace {
 
 // k_scale_stress over the current layer (the separate ODE pass).
+// Per-material factors into the context's device slot: they travel as kernel
+// arguments, ordered on the stream after the previous launch that read the
+// slot -- no host sync.
+gcmx_status ode_upload(gcmx_ctx* c, const std::vector<double>& f) {
+	if (!c->ode_d) HIP_TRY(hipMalloc(&c->ode_d, 256 * sizeof(double)));
+	OdeFactors v{};
+	v.n = (int)f.size();
+	for (int m = 0; m < v.n; m++) v.f[m] = f[m];
+	launch_set_factors(c->ode_d, v, c->stream);
+	HIP_TRY(hipGetLastError());
+	return GCMX_OK;
+}
+
 gcmx_status ode_apply(gcmx_ctx* c, const std::vector<double>& f) {
 	gcmx_status s = halo_wait(c);
 	if (s) return s;
@@ -1789,13 +1820,8 @@ gcmx_status ode_apply(gcmx_ctx* c, const std::vector<double>& f) {
 		Timed t(c, "ode_maxwell", 2.0 * 8.0 * (c->M - c->D) * (double)c->geo.n_inner, c->stream);
 		launch_scale_stress(c->cur, c->geo, nullptr, nullptr, f[0], c->stream);
 	} else {
-		// the factors travel as kernel arguments into the context's device slot,
-		// ordered on the stream after the previous scaling that read it: no host sync
-		if (!c->ode_d) HIP_TRY(hipMalloc(&c->ode_d, 256 * sizeof(double)));
-		OdeFactors v{};
-		v.n = n_mat;
-		for (int m = 0; m < n_mat; m++) v.f[m] = f[m];
-		launch_set_factors(c->ode_d, v, c->stream);
+		gcmx_status s2 = ode_upload(c, f);
+		if (s2) return s2;
 		Timed t(c, "ode_maxwell", (2.0 * 8.0 * (c->M - c->D) + 1.0) * (double)c->geo.n_inner, c->stream);
 		launch_scale_stress(c->cur, c->geo, c->mat_d, c->ode_d, 0.0, c->stream);
 	}

@@ -413,6 +413,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// vmcnt, and waiting for it would wait for every row-ahead load issued before
 	// it -- the software pipeline collapses (measured: HET 256^3 +34 %).
 	__shared__ IsoAxis hlds[HET ? kHetMaxMaterials : 1];
+	__shared__ double hode[HET ? kHetMaxMaterials : 1];  // HET: folded ODE factor per material
 	__shared__ double flds[FACES && GCMX_TX2_FACE_LDS ? 4 : 1][9];  // 2 f(t) of the y/z faces
 
 	const int z = threadIdx.x;
@@ -698,6 +699,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	if constexpr (HET) {  // tables into LDS (het tables are allocated for 256 materials)
 		for (int i = z; i < kHetMaxMaterials * (int)(sizeof(IsoAxis) / 4); i += ZT)
 			reinterpret_cast<unsigned*>(hlds)[i] = reinterpret_cast<const unsigned*>(mtab)[i];
+		if (fb.ode_on && fb.ode_f && z < kHetMaxMaterials) hode[z] = fb.ode_f[z];
 	}
 	if constexpr (FACES && GCMX_TX2_FACE_LDS) {
 #pragma unroll
@@ -900,8 +902,11 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		if constexpr (HET) waterfall(t ? hk[BS] >> 8 : hk[BS] & 255u, [&](unsigned k) { go(mt(k)); });
 		else go(AZ);
 		if (fb.ode_on) {  // MaxwellViscosityOde: sigma *= exp(-tau / tau0), the stored product (Ode.hpp:34-35)
+			double f = fb.ode;
+			if constexpr (HET)  // the node's own material's factor
+				if (fb.ode_f) f = hode[t ? hk[BS] >> 8 : hk[BS] & 255u];
 #pragma unroll
-			for (int c = 3; c < 9; c++) zv[c] = zv[c] * fb.ode;
+			for (int c = 3; c < 9; c++) zv[c] = zv[c] * f;
 		}
 		if (t == 0 ? one : two) {
 #pragma unroll

@@ -94,6 +94,7 @@ struct FaceBC {
 	// stress component of the step's result times `ode` (Ode.hpp:28-37) when ode_on
 	unsigned ode_on;
 	double ode;
+	const double* ode_f;  // HET: per-material factors (device, indexed by the node's id)
 	const uint8_t* map[4];
 	const FaceCond* conds;
 };

@@ -106,7 +106,9 @@ void        gcmx_destroy(gcmx_ctx* ctx);
 gcmx_status gcmx_set_materials(gcmx_ctx* ctx, int n_mat, const double* U,
                                const double* U1, const double* L);
 /* One byte per node of the all-nodes array (getIndex order); NULL means every
- * node uses material 0.  Ghost entries are ignored. */
+ * node uses material 0.  Ghost entries are ignored.  With per-node ids the 3-D
+ * step runs in one pass for up to 32 materials (their tables held in LDS, and
+ * floor(q) = 0 with equal axes per material); more take the per-stage path. */
 gcmx_status gcmx_set_material_ids(gcmx_ctx* ctx, const uint8_t* ids_all_nodes);
 
 /* Whole current time layer, host <-> device (DefaultMesh::pdeVariables). */

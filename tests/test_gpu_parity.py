@@ -397,6 +397,35 @@ def test_heterogeneous_one_pass_step_matches_oracle(G, bs, sizes, layout):
     ctx.close()
 
 
+@pytest.mark.parametrize("faces", [False, True])
+def test_heterogeneous_step_ode_fused_equals_step_then_ode(G, faces):
+    """MaxwellViscosityOde (Ode.hpp:28-37) folded into the heterogeneous one-pass
+    step's stores: each node's stresses times ITS material's exp(-tau / tau0[m]).
+    gcmx_step_ode == gcmx_step (gcmx_step_faces) followed by gcmx_ode_maxwell's
+    per-node pass, bitwise, with random ids (two materials in most lane pairs)."""
+    from gcm_amd.gcmx import QUANTITY_CODES as q
+    fc = [[(q["Sxx"], 0.0), (q["Sxy"], 0.0), (q["Sxz"], 0.0)], None,
+          [(q["Syy"], -0.3), (q["Syz"], 0.0)], [(q["Vy"], 0.1)],
+          [(q["Szz"], 0.0), (q["Sxz"], 0.0), (q["Syz"], 0.0)], None] if faces else None
+    mats = ((4.0, 2.0, 1.0), (1.0, 2.0, 0.8), (2.5, 0.0, 3.0))
+    b = oracle_body(3, 2, [8, 16, 64], materials=mats, courant=0.9)
+    random_materials(b, seed=5)
+    random_state(b, seed=6, ghosts=False)
+    tau = 0.9 / np.sqrt((3.0 + 6.0) / 2.5)
+    tau0 = [3.0, 0.5, 7.0]
+    a, c = context_for(b), context_for(b)
+    for _ in range(3):
+        if faces:
+            a.step_faces(tau, fc)
+        else:
+            a.step(tau)
+        a.ode_maxwell(tau, tau0)
+        c.step_ode(tau, tau0, fc)
+        assert c.last_ode_fused and c.last_path == "fused"
+    assert not a.last_ode_fused
+    assert np.array_equal(a.download(), c.download())
+    a.close(); c.close()
+
 def test_heterogeneous_many_materials_take_per_stage_path(G):
     """More materials than the one-pass step keeps in LDS (kHetMaxMaterials = 32):
     the per-stage path with per-node matrices, still bitwise == the oracle."""
