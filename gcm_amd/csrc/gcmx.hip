@@ -202,7 +202,7 @@ hipEvent_t take_event(gcmx_ctx* c) {
 		ev = c->event_pool.back();
 		c->event_pool.pop_back();
 	} else {
-		hipEventCreate(&ev);
+		(void)hipEventCreate(&ev);
 	}
 	return ev;
 }
@@ -221,11 +221,11 @@ struct Timed {
 		b = bucket_id(c, name);
 		a = take_event(c);
 		e = take_event(c);
-		hipEventRecord(a, st);
+		(void)hipEventRecord(a, st);
 	}
 	~Timed() {
 		if (b < 0) return;
-		hipEventRecord(e, st);
+		(void)hipEventRecord(e, st);
 		c->pending.push_back({b, bytes, a, e});
 		if (kname) c->buckets[b].kernel = kname;
 	}
@@ -234,8 +234,8 @@ struct Timed {
 void drain_timings(gcmx_ctx* c) {
 	for (auto& p : c->pending) {
 		float ms = 0;
-		hipEventSynchronize(p.b);
-		hipEventElapsedTime(&ms, p.a, p.b);
+		(void)hipEventSynchronize(p.b);
+		(void)hipEventElapsedTime(&ms, p.a, p.b);
 		c->buckets[p.bucket].total_ms += ms;
 		c->buckets[p.bucket].launches += 1;
 		c->buckets[p.bucket].bytes += p.bytes;
@@ -939,18 +939,18 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 
 void gcmx_destroy(gcmx_ctx* c) {
 	if (!c) return;
-	hipSetDevice(c->device);
+	(void)hipSetDevice(c->device);
 	if (c->comm) {  // bounded: a stalled exchange aborts the communicator
 		if (c->comm_stream) (void)wait_stream(c, c->comm_stream, "gcmx_destroy");
 		if (c->stream && c->comm) (void)wait_stream(c, c->stream, "gcmx_destroy");
 	}
-	if (c->stream) hipStreamSynchronize(c->stream);
-	if (c->comm_stream) hipStreamSynchronize(c->comm_stream);
-	if (c->inner_stream) hipStreamSynchronize(c->inner_stream);
-	if (c->bnd_stream) hipStreamSynchronize(c->bnd_stream);
+	if (c->stream) (void)hipStreamSynchronize(c->stream);
+	if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+	if (c->inner_stream) (void)hipStreamSynchronize(c->inner_stream);
+	if (c->bnd_stream) (void)hipStreamSynchronize(c->bnd_stream);
 	drain_timings(c);
-	for (hipEvent_t ev : c->event_pool) hipEventDestroy(ev);
-	if (c->probe_stream) hipStreamSynchronize(c->probe_stream);
+	for (hipEvent_t ev : c->event_pool) (void)hipEventDestroy(ev);
+	if (c->probe_stream) (void)hipStreamSynchronize(c->probe_stream);
 	if (c->comm) {  // non-blocking communicator: finalize (bounded), then destroy; abort on failure
 		ncclResult_t r = ncclCommFinalize(c->comm);
 		if (r == ncclSuccess || r == ncclInProgress) {
@@ -977,27 +977,27 @@ void gcmx_destroy(gcmx_ctx* c) {
 		L.ctx[c->lrank] = nullptr;
 	}
 	if (c->layers_block) {
-		hipFree(c->layers_block);
+		(void)hipFree(c->layers_block);
 	} else {
-		hipFree(c->layer_a);
-		hipFree(c->layer_b);
+		(void)hipFree(c->layer_a);
+		(void)hipFree(c->layer_b);
 	}
-	hipFree(c->probe_d);
-	if (c->probe_stream) hipStreamDestroy(c->probe_stream);
-	hipFree(c->tabs_d);
-	hipFree(c->mat_d);
-	hipFree(c->nodes_d);
-	hipFree(c->ode_d);
-	hipFree(c->het_d);
-	if (c->ev_ready) hipEventDestroy(c->ev_ready);
-	if (c->ev_halo) hipEventDestroy(c->ev_halo);
-	if (c->ev_fork) hipEventDestroy(c->ev_fork);
-	if (c->ev_join) hipEventDestroy(c->ev_join);
-	if (c->ev_bnd) hipEventDestroy(c->ev_bnd);
-	if (c->stream) hipStreamDestroy(c->stream);
-	if (c->comm_stream) hipStreamDestroy(c->comm_stream);
-	if (c->inner_stream) hipStreamDestroy(c->inner_stream);
-	if (c->bnd_stream) hipStreamDestroy(c->bnd_stream);
+	(void)hipFree(c->probe_d);
+	if (c->probe_stream) (void)hipStreamDestroy(c->probe_stream);
+	(void)hipFree(c->tabs_d);
+	(void)hipFree(c->mat_d);
+	(void)hipFree(c->nodes_d);
+	(void)hipFree(c->ode_d);
+	(void)hipFree(c->het_d);
+	if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+	if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
+	if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+	if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+	if (c->ev_bnd) (void)hipEventDestroy(c->ev_bnd);
+	if (c->stream) (void)hipStreamDestroy(c->stream);
+	if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+	if (c->inner_stream) (void)hipStreamDestroy(c->inner_stream);
+	if (c->bnd_stream) (void)hipStreamDestroy(c->bnd_stream);
 	delete c;
 }
 
@@ -1032,7 +1032,7 @@ gcmx_status gcmx_set_material_ids(gcmx_ctx* c, const uint8_t* ids) {
 	gcmx_status s = check_ctx(c);
 	if (s) return s;
 	if (!ids) {
-		hipFree(c->mat_d);
+		(void)hipFree(c->mat_d);
 		c->mat_d = nullptr;
 		c->max_mat_id = -1;
 	} else {
@@ -1189,14 +1189,13 @@ struct SlabJoin {
 	gcmx_ctx* c;
 	bool inner = false, bnd = false;
 	~SlabJoin() {
-		if (bnd) {
-			hipEventRecord(c->ev_bnd, c->bnd_stream);
-			hipStreamWaitEvent(c->stream, c->ev_bnd, 0);
-		}
-		if (inner) {
-			hipEventRecord(c->ev_join, c->inner_stream);
-			hipStreamWaitEvent(c->stream, c->ev_join, 0);
-		}
+		if (bnd) join(c->ev_bnd, c->bnd_stream);
+		if (inner) join(c->ev_join, c->inner_stream);
+	}
+	// event join; should the event calls fail, a host join keeps the order
+	void join(hipEvent_t ev, hipStream_t side) {
+		if (hipEventRecord(ev, side) != hipSuccess || hipStreamWaitEvent(c->stream, ev, 0) != hipSuccess)
+			(void)hipStreamSynchronize(side);
 	}
 };
 
@@ -1563,12 +1562,12 @@ gcmx_status gcmx_face_map_create(gcmx_ctx* c, const uint8_t* const node_conditio
 void gcmx_face_map_destroy(gcmx_face_map* m) {
 	if (!m) return;
 	if (m->ctx) {
-		hipSetDevice(m->ctx->device);
-		hipStreamSynchronize(m->ctx->stream);  // a pending step may still read the maps
+		(void)hipSetDevice(m->ctx->device);
+		(void)hipStreamSynchronize(m->ctx->stream);  // a pending step may still read the maps
 	}
-	for (uint8_t* p : m->map_d) hipFree(p);
-	hipFree(m->bq_d);
-	hipFree(m->fc_d);
+	for (uint8_t* p : m->map_d) (void)hipFree(p);
+	(void)hipFree(m->bq_d);
+	(void)hipFree(m->fc_d);
 	delete m;
 }
 
@@ -1718,7 +1717,7 @@ gcmx_status gcmx_border_fill(gcmx_ctx* c, int axis, int side, int n_nodes, const
 	const size_t need = (size_t)n_nodes * c->D;
 	HIP_TRY(hipStreamSynchronize(c->stream));  // scratch reuse (gcmx_border_apply has none)
 	if (need > c->nodes_cap) {
-		hipFree(c->nodes_d);
+		(void)hipFree(c->nodes_d);
 		c->nodes_d = nullptr;
 		c->nodes_cap = 0;
 		HIP_TRY(hipMalloc(&c->nodes_d, need * sizeof(int)));
@@ -1749,7 +1748,7 @@ gcmx_status gcmx_border_nodes_create(gcmx_ctx* c, int axis, int side, int n_node
 			return fail(GCMX_ERR_OOM, "device allocation failed");
 		}
 		if (hipMemcpy(h->nodes_d, nodes, bytes, hipMemcpyHostToDevice) != hipSuccess) {
-			hipFree(h->nodes_d);
+			(void)hipFree(h->nodes_d);
 			delete h;
 			return fail(GCMX_ERR_HIP, "node list upload failed");
 		}
@@ -1778,10 +1777,10 @@ gcmx_status gcmx_border_apply(gcmx_ctx* c, const gcmx_border_nodes* h, int n_q, 
 void gcmx_border_nodes_destroy(gcmx_border_nodes* h) {
 	if (!h) return;
 	if (h->ctx) {
-		hipSetDevice(h->ctx->device);
-		hipStreamSynchronize(h->ctx->stream);  // a pending fill may still read the list
+		(void)hipSetDevice(h->ctx->device);
+		(void)hipStreamSynchronize(h->ctx->stream);  // a pending fill may still read the list
 	}
-	hipFree(h->nodes_d);
+	(void)hipFree(h->nodes_d);
 	delete h;
 }
 
@@ -1815,7 +1814,6 @@ gcmx_status ode_upload(gcmx_ctx* c, const std::vector<double>& f) {
 gcmx_status ode_apply(gcmx_ctx* c, const std::vector<double>& f) {
 	gcmx_status s = halo_wait(c);
 	if (s) return s;
-	const int n_mat = (int)f.size();
 	if (!c->mat_d) {
 		Timed t(c, "ode_maxwell", 2.0 * 8.0 * (c->M - c->D) * (double)c->geo.n_inner, c->stream);
 		launch_scale_stress(c->cur, c->geo, nullptr, nullptr, f[0], c->stream);
@@ -2250,10 +2248,10 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 		st = fail(GCMX_ERR_HIP, "copy-ceiling set-up");
 	} else {
 		for (int r = 0; r <= reps && st == GCMX_OK; r++) {
-			hipEventRecord(e0, c->stream);
+			(void)hipEventRecord(e0, c->stream);
 			hipLaunchKernelGGL(k_copy_ceiling, dim3(32768), dim3(256), 0, c->stream,
 			                   static_cast<const copy_d2*>(a), static_cast<copy_d2*>(b), n2);
-			hipEventRecord(e1, c->stream);
+			(void)hipEventRecord(e1, c->stream);
 			float t = 0.0f;
 			if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&t, e0, e1) != hipSuccess)
 				st = fail(GCMX_ERR_HIP, "copy-ceiling timing");
@@ -2322,7 +2320,7 @@ gcmx_status gcmx_clock_probe_start(gcmx_ctx* c, double seconds, double period_us
 	if (!c->probe_stream) HIP_TRY(hipStreamCreateWithFlags(&c->probe_stream, hipStreamNonBlocking));
 	HIP_TRY(hipStreamSynchronize(c->probe_stream));
 	if (cap > c->probe_cap) {
-		hipFree(c->probe_d);
+		(void)hipFree(c->probe_d);
 		c->probe_d = nullptr;
 		c->probe_cap = 0;
 		HIP_TRY(hipMalloc(&c->probe_d, (1 + 2 * (size_t)cap) * sizeof(unsigned long long)));

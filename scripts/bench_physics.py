@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 FACE_FORCE = {0: ["Sxx", "Sxy", "Sxz"], 1: ["Sxy", "Syy", "Syz"], 2: ["Sxz", "Syz", "Szz"]}
 
 
-def task(n, maxwell, layers=False, free=True, xbodies=1):
+def task(n, maxwell, layers=False, free=True, xbodies=1, axis=0, partial=False):
     from gcm_amd import _gcm_host as H
     t = H.Task()
     t.dimensionality = 3
@@ -28,10 +28,12 @@ def task(n, maxwell, layers=False, free=True, xbodies=1):
     t.h = [1.0, 1.0, 1.0]
     t.courant = 0.9
     t.number_of_snaps = 10 ** 6
-    if xbodies > 1:  # the domain as bodies stacked along x: contacts along x (engine: one pass)
-        w = n // xbodies
+    if xbodies > 1:  # the domain as bodies stacked along `axis`: contacts (engine: one pass;
+        w = n // xbodies  # along y / z the engine runs them as one stack)
         for k in range(xbodies):
-            t.add_body(k, [w, n, n], [k * w, 0, 0])
+            sz, st = [n, n, n], [0, 0, 0]
+            sz[axis], st[axis] = w, k * w
+            t.add_body(k, sz, st)
     else:
         t.add_body(0, [n, n, n], [0, 0, 0])
     t.set_default_material(4.0, 2.0, 1.0, tau0=50.0 if maxwell else 0.0)
@@ -42,6 +44,9 @@ def task(n, maxwell, layers=False, free=True, xbodies=1):
     for d, qs in FACE_FORCE.items():  # free surface: zero traction on both faces of axis d
         if free:
             t.add_border_condition(0, d, ("infinite",), {q: (lambda time: 0.0) for q in qs})
+    if free and partial:  # a condition over part of face y- (x < n/2): per-node face maps
+        t.add_border_condition(0, 1, ("box", (-1, -1, -1), (n / 2 - 0.5, 0.5, n + 1)),
+                               {"Vy": (lambda time: -0.1)})
     if maxwell:
         t.add_ode(0, "MAXWELL_VISCOSITY")
     return t
@@ -57,11 +62,15 @@ def main():
                     help="two materials (per-node material ids: the heterogeneous path)")
     ap.add_argument("--xbodies", type=int, default=1,
                     help="split the domain into this many bodies along x (contacts along x)")
+    ap.add_argument("--axis", type=int, default=0, choices=[0, 1, 2],
+                    help="the axis --xbodies stacks the bodies along")
+    ap.add_argument("--partial", action="store_true",
+                    help="free surfaces plus a condition over half of face y- (partial face)")
     ap.add_argument("--free", action=argparse.BooleanOptionalAction, default=True,
                     help="free surfaces on all faces (--no-free: ghosts stay zero)")
     a = ap.parse_args()
     from gcm_amd import _gcm_host as H
-    e = H.Engine(task(a.n, a.maxwell, a.layers, a.free and a.xbodies == 1, a.xbodies))
+    e = H.Engine(task(a.n, a.maxwell, a.layers, a.free and a.xbodies == 1, a.xbodies, a.axis, a.partial))
     free = a.free and a.xbodies == 1
     nb = max(1, a.xbodies)
 
@@ -77,7 +86,8 @@ def main():
     print(json.dumps({
         "metric": "Mnode-steps/s, cubic engine" + (" with free surfaces" if free else "") +
                   (" + Maxwell ODE" if a.maxwell else "") + (", two materials" if a.layers else "") +
-                  (f", {nb} bodies along x with contacts" if nb > 1 else ""),
+                  (" + a condition over half of face y-" if free and a.partial else "") +
+                  (f", {nb} bodies along {'xyz'[a.axis]} with contacts" if nb > 1 else ""),
         "value": round(a.n ** 3 * a.steps / dt / 1e6, 1), "unit": "Mnode-steps/s",
         "ms_per_step": round(dt / a.steps * 1e3, 4), "n": a.n, "steps": a.steps,
         "path": e.path(0), "last_path": [e.last_path(b) for b in range(nb)], "ode_fused": e.ode_fused(0),
