@@ -181,7 +181,8 @@ struct gcmx_border_nodes {
 // kNoFaceCond; the conditions' tables are written on the stream every step.
 struct gcmx_face_map {
 	gcmx_ctx* ctx = nullptr;
-	uint8_t* map_d[6] = {};
+	uint8_t* map_d[6] = {};  // per-node conditions of a face that mixes them
+	int uni[6] = {-1, -1, -1, -1, -1, -1};  // a face whose every node has condition uni[f]: no map
 	unsigned used[6] = {};  // per face: bit k = condition k occurs on it
 	BorderQ* bq_d = nullptr;
 	FaceCond* fc_d = nullptr;
@@ -1550,6 +1551,12 @@ gcmx_status gcmx_face_map_create(gcmx_ctx* c, const uint8_t* const node_conditio
 		}
 		if (!used) continue;  // no condition on this face: its ghosts stay as they are
 		m->used[f] = used;
+		bool whole = true;  // one condition on every node: the face is uniform, no map needed
+		for (size_t i = 0; i < n && whole; i++) whole = node_condition[f][i] == node_condition[f][0];
+		if (whole) {
+			m->uni[f] = node_condition[f][0];
+			continue;
+		}
 		HIP_TRY(hipMalloc(&m->map_d[f], n));
 		HIP_TRY(hipMemcpy(m->map_d[f], node_condition[f], n, hipMemcpyHostToDevice));
 	}
@@ -1593,7 +1600,7 @@ static gcmx_status step_face_map_body(gcmx_ctx* c, double tau, const gcmx_face_m
 	const int D = c->D;
 	unsigned on = 0;
 	for (int f = 0; f < 2 * D; f++)
-		if (m->map_d[f]) {
+		if (m->map_d[f] || m->uni[f] >= 0) {
 			if (m->used[f] >> n_cond) return fail(GCMX_ERR_INVALID_ARG, "the face map names a condition not given");
 			on |= 1u << f;
 		}
@@ -1627,7 +1634,10 @@ static gcmx_status step_face_map_body(gcmx_ctx* c, double tau, const gcmx_face_m
 		gcmx_status st = halo_wait(c);
 		if (st) return st;
 		Timed tm(c, "face_fill", 0.0, c->stream);
-		launch_face_fill_map(c->cur, c->geo, f / 2, (f & 1) ? 1 : -1, m->map_d[f], m->bq_d, c->stream);
+		if (m->map_d[f])
+			launch_face_fill_map(c->cur, c->geo, f / 2, (f & 1) ? 1 : -1, m->map_d[f], m->bq_d, c->stream);
+		else
+			launch_face_fill(c->cur, c->geo, f / 2, (f & 1) ? 1 : -1, t.bq[m->uni[f]], c->stream);
 		HIP_TRY(hipGetLastError());
 		c->faces_written |= 1u << f;
 		return GCMX_OK;
@@ -1635,19 +1645,24 @@ static gcmx_status step_face_map_body(gcmx_ctx* c, double tau, const gcmx_face_m
 	if (fused) {
 		// x faces in memory, y/z faces formed inside the one-pass step per face node
 		for (int f = 0; f < 2; f++)
-			if (m->map_d[f] && (s = fill(f)) != GCMX_OK) return s;
+			if (((on >> f) & 1u) && (s = fill(f)) != GCMX_OK) return s;
 		FaceBC fb{};
 		for (int f = 2; f < 6; f++)
 			if (m->map_d[f]) {
 				fb.on |= 1u << (f - 2);
 				fb.map[f - 2] = m->map_d[f];
+			} else if (m->uni[f] >= 0) {  // uniform face: the condition as kernel arguments
+				const FaceCond& fc = t.fc[m->uni[f]];
+				fb.on |= 1u << (f - 2);
+				fb.mask[f - 2] = fc.mask;
+				for (int j = 0; j < 9; j++) fb.two_v[f - 2][j] = fc.two_v[j];
 			}
 		fb.conds = m->fc_d;
 		return fused_step(c, fb.on ? &fb : nullptr, true);
 	}
 	for (int a = 0; a < D; a++) {  // BorderConditions::apply(mesh, a), then the stage (Engine.cpp:90-121)
 		for (int f = 2 * a; f < 2 * a + 2; f++)
-			if (m->map_d[f] && (s = fill(f)) != GCMX_OK) return s;
+			if (((on >> f) & 1u) && (s = fill(f)) != GCMX_OK) return s;
 		if ((s = stage_impl(c, a, tau)) != GCMX_OK) return s;
 	}
 	return GCMX_OK;

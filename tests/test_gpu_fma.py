@@ -261,6 +261,7 @@ def test_fma_engine_xbodies_equal_one_body(G, monkeypatch, widths):
     from gcm_amd import _gcm_host as H
     from tests.taskspec import host_task, oracle_task
     monkeypatch.setenv("GCMX_FP", "fma")
+    monkeypatch.setenv("GCMX_NO_STACKS", "1")  # separate bodies: the global pairing is what is tested
     split = H.Engine(host_task(_xbodies(widths)))
     split.run()
     assert all(split.last_path(i) == "fused" for i in range(len(widths)))
