@@ -251,6 +251,15 @@ __device__ __forceinline__ double ld_b(const Planes& p, int j, unsigned boff) {
 	typedef const __attribute__((address_space(1))) char* gcb;
 	return *reinterpret_cast<gcptr>(reinterpret_cast<gcb>(p.b[j]) + (unsigned long long)boff);
 }
+// single-use load (streaming: no L2 allocation preference over the reused planes)
+__device__ __forceinline__ double ld_nt_b(const Planes& p, int j, unsigned boff) {
+	typedef const __attribute__((address_space(1))) char* gcb;
+	return __builtin_nontemporal_load(reinterpret_cast<gcptr>(reinterpret_cast<gcb>(p.b[j]) + (unsigned long long)boff));
+}
+__device__ __forceinline__ void st_b(const PlanesW& p, int j, unsigned boff, double v) {
+	typedef __attribute__((address_space(1))) char* gb;
+	*reinterpret_cast<gptr>(reinterpret_cast<gb>(p.b[j]) + (unsigned long long)boff) = v;
+}
 __device__ __forceinline__ void st_nt_b(const PlanesW& p, int j, unsigned boff, double v) {
 	typedef __attribute__((address_space(1))) char* gb;
 	__builtin_nontemporal_store(v, reinterpret_cast<gptr>(reinterpret_cast<gb>(p.b[j]) + (unsigned long long)boff));

@@ -293,6 +293,12 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_TX2_FACE_LDS
 #define GCMX_TX2_FACE_LDS 0
 #endif
+#ifndef GCMX_TX2_STNT
+#define GCMX_TX2_STNT 1  // non-temporal stores of the new layer
+#endif
+#ifndef GCMX_TX2_NTLOAD
+#define GCMX_TX2_NTLOAD 1  // node-only components by non-temporal loads (+0.4 %, profiles/r4/ab)
+#endif
 #ifndef GCMX_HET_AB
 #define GCMX_HET_AB 0
 #endif
@@ -463,8 +469,16 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		const int d = (k == WX - 1 && !two) ? 2 * BS : (k == 0 && !one) ? 1 : k;
 		return ld_b(src, j, opaque_u32(lv + (pxm + (unsigned)d * stx + (unsigned)r * sty) * 8u));
 	};
+	// the node-only components of the own planes: read once, by this lane only
+	auto ldc = [&](int j, int k, int r) {
+		if constexpr (!GCMX_TX2_NTLOAD) return ldx(j, k, r);
+		const int d = (k == WX - 1 && !two) ? 2 * BS : (k == 0 && !one) ? 1 : k;
+		return ld_nt_b(src, j, opaque_u32(lv + (pxm + (unsigned)d * stx + (unsigned)r * sty) * 8u));
+	};
 	auto stz = [&](int c, int t, int y, double v) {
-		st_nt_b(out_p, c, opaque_u32(sv + (plane + (unsigned)t * stx + (unsigned)y * sty) * 8u), v);
+		const unsigned o = opaque_u32(sv + (plane + (unsigned)t * stx + (unsigned)y * sty) * 8u);
+		if constexpr (GCMX_TX2_STNT) st_nt_b(out_p, c, o, v);
+		else st_b(out_p, c, o, v);
 	};
 #else
 	const unsigned base = plane + zc;
@@ -474,6 +488,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		const int d = (k == WX - 1 && !two) ? BS : (k == 0 && !one) ? 1 - BS : k - BS;
 		return src.ld(j, base + (unsigned)r * sty + (unsigned)d * stx);
 	};
+	auto ldc = [&](int j, int k, int r) { return ldx(j, k, r); };
 	auto stz = [&](int c, int t, int y, double v) { out_p.st_nt(c, plane + (unsigned)y * sty + zo + (unsigned)t * stx, v); };
 #endif
 	// per-material table k (k wave-uniform: waterfall), from the LDS copy made at
@@ -629,7 +644,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		for (int t = 0; t < 2; t++)
 #pragma unroll
 			for (int j = 0; j < 9; j++)
-				if ((CMX >> j) & 1u) cv[t][j] = ldx(j, BS + t, r);
+				if ((CMX >> j) & 1u) cv[t][j] = ldc(j, BS + t, r);
 	};
 	auto x_load_ahead = [&](XPre& pre, int r) {
 		pair_load(P0{}, pre.a, r);
