@@ -296,6 +296,9 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_TX2_STNT
 #define GCMX_TX2_STNT 1  // non-temporal stores of the new layer
 #endif
+#ifndef GCMX_TX2_NTOUTER
+#define GCMX_TX2_NTOUTER 0  // timing knob: the outermost window planes by non-temporal loads
+#endif
 #ifndef GCMX_TX2_NTLOAD
 #define GCMX_TX2_NTLOAD 1  // node-only components by non-temporal loads (+0.4 %, profiles/r4/ab)
 #endif
@@ -467,6 +470,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		// planes outside the valid range (x - BS when x is not ours, x + 1 + BS when
 		// x + 1 is not ours) are read by the discarded node only: clamp them
 		const int d = (k == WX - 1 && !two) ? 2 * BS : (k == 0 && !one) ? 1 : k;
+		if (GCMX_TX2_NTOUTER && (k == 0 || k == WX - 1))
+			return ld_nt_b(src, j, opaque_u32(lv + (pxm + (unsigned)d * stx + (unsigned)r * sty) * 8u));
 		return ld_b(src, j, opaque_u32(lv + (pxm + (unsigned)d * stx + (unsigned)r * sty) * 8u));
 	};
 	// the node-only components of the own planes: read once, by this lane only

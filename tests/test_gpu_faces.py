@@ -349,7 +349,7 @@ PARTIAL_CASES = {
 }
 
 
-def partial_body(bs, sizes, conds):
+def partial_body(bs, sizes, conds, materials=((4.0, 2.0, 1.0),)):
     bcs = []
     for axis, side, area, vals in conds:
         if side != 0:  # restrict the area to one face: intersect with the face slab
@@ -361,9 +361,10 @@ def partial_body(bs, sizes, conds):
             elif area[0] == "sphere":  # a sphere whose centre sits on the face touches only it here
                 pass
         bcs.append(O.BorderCondition(axis, area, vals))
+    mats = [O.Material(*m) for m in materials]
     t = O.Task(D=3, border_size=bs, h=[1.0] * 3, cubics={0: (list(sizes), [0] * 3)}, courant=0.9,
-               default_material=O.Material(4.0, 2.0, 1.0), number_of_snaps=1,
-               border_conditions={0: bcs})
+               default_material=mats[0], inhomogeneities=[(("infinite",), m) for m in mats[1:]],
+               number_of_snaps=1, border_conditions={0: bcs})
     return O.Engine(t).bodies[0]
 
 
@@ -397,6 +398,36 @@ def test_step_face_map_matches_oracle(G, name, fp):
             r = float(np.linalg.norm(got - want)) / float(np.linalg.norm(want))
             assert r <= 1e-10, f"partial {name} step {step}: {r}"
         t += tau
+    fmap.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", ["mixed", "bs1"])
+def test_step_face_map_heterogeneous_one_pass(G, name):
+    """Partial faces AND per-node materials (random ids, two materials in most
+    lane pairs) in one one-pass launch (k_step_tx2<..., FACES, HET>): bitwise ==
+    the oracle's BorderConditions::apply + stage sequence with each node's own
+    matrices."""
+    from tests.helpers import random_materials
+    bs, sizes, conds, _, path = PARTIAL_CASES[name]
+    b = partial_body(bs, sizes, conds, materials=((4.0, 2.0, 1.0), (1.0, 2.0, 0.8)))
+    random_materials(b, seed=3)
+    random_state(b, seed=11, ghosts=False)
+    tau = 0.9 / np.sqrt(3.6)  # Courant 0.9 on the faster material: floor(q) = 0 for both
+    ctx = context_for(b)
+    ctx.profile(True)
+    fmap = ctx.face_map(face_maps(b, sizes))
+    t = 0.0
+    for step in range(3):
+        for s in range(3):
+            b.apply_border(s, t)
+            b.stage(s, tau)
+        ctx.step_face_map(tau, fmap, conditions_at(b, t))
+        assert ctx.last_path == path == "fused"
+        assert_same_inner(ctx, b, f"partial HET {name} step {step}")
+        t += tau
+    k = ctx.profile_read()
+    assert "HET" in k["fused_xyz"]["kernel"] and ", FACES," in k["fused_xyz"]["kernel"], k
     fmap.close()
     ctx.close()
 
