@@ -296,6 +296,9 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_TX2_STNT
 #define GCMX_TX2_STNT 1  // non-temporal stores of the new layer
 #endif
+#ifndef GCMX_TX2_ALT
+#define GCMX_TX2_ALT 1  // odd y chunks march down (shared halo rows read at the same time)
+#endif
 #ifndef GCMX_TX2_NTOUTER
 #define GCMX_TX2_NTOUTER 0  // timing knob: the outermost window planes by non-temporal loads
 #endif
@@ -428,6 +431,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const int z = threadIdx.x;
 	const int Y = g.sizes[1], Z = g.sizes[2];
 	int x, yb, xbeg, xend;
+	bool rev;  // this block marches its rows downwards (odd chunks, GCMX_TX2_ALT)
 	{  // XCD-aware chunk-major block order (see k_fused_xyz) over the plane pairs of
 	   // range A [x0, x0 + nplanes), then range B [xb0, xb0 + nplanesb) (may be empty).
 	   // Pairs are GLOBAL: (2k, 2k+1) in the global x index g.gx0 + x, so a range
@@ -445,6 +449,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		xbeg = q < npa ? x0 : xb0;
 		xend = q < npa ? x0 + nplanes : xb0 + nplanesb;
 		yb = (p / npair) * chunk;
+		rev = GCMX_TX2_ALT && ((p / npair) & 1);
 	}
 	const bool one = x >= xbeg;  // node x is ours (else only x + 1 is)
 	const bool two = x + 1 < xend;
@@ -553,7 +558,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll
 				for (int q = 0; q < NWZ; q++) rg[wv][t][q][hs] = 0.0;
 		}
-		if (z < NW) rdy[z] = yb - 1;
+		if (z < NW) rdy[z] = -1;  // rows published, counted in marching order
 		__syncthreads();
 	} else if (z < 2 * BS) {
 		const int gslot = (z < BS) ? z : (Z + z);
@@ -661,7 +666,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	// X results come from zero ghost rows or are replaced by a face's mirror)
 	auto mat_of = [&](int t, int r) -> unsigned {
 		const int xx = (t == 1 && !two) ? x : (t == 0 && !one) ? x + 1 : x + t;
-		const int rr_ = r < Y ? r : Y - 1;
+		const int rr_ = r < 0 ? 0 : (r < Y ? r : Y - 1);
 		return mat[((size_t)xx * Y + rr_) * Z + z];
 	};
 	auto x_compute = [&](const XPre& pre, const PairWin& wc, const double (&cv)[2][9], double (&xr)[2][9],
@@ -727,9 +732,18 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			if (z == c) flds[c / 9][c % 9] = fb.two_v[c / 9][c % 9];
 	}
 	if constexpr (HET || (FACES && GCMX_TX2_FACE_LDS)) __syncthreads();
+	// The row march, in either direction (REV: from the chunk's last row down).
+	// Odd chunks march down, so the halo rows two adjacent chunks both compute
+	// the X stage of are read by both blocks at the same time -- both at the
+	// start or both at the end of their march -- and the second read hits the
+	// caches (a forward-only march reads them at opposite ends of the launch:
+	// 256^3, 64-row chunks, 1.13x the compulsory reads from HBM).
+	auto run = [&](auto RV) {
+	constexpr bool REV = decltype(RV)::value;
+	constexpr int S = REV ? -1 : 1;
 	// node-only Y components: ring slot of row r; per-lane pointer with the
 	// (node, component) part as a constant LDS offset
-	auto cl_at = [&](int r) { return &cl[(r + BS) % (BS + 1)][0][0][z]; };
+	auto cl_at = [&](int r) { return &cl[(r + 2 * BS + 2) % (BS + 1)][0][0][z]; };
 	// row r's X result enters window slot `slot`; its node-only components go to the ring
 	auto push = [&](const double (&xr)[2][9], int slot, int r) {
 		double* cp = cl_at(r);
@@ -760,10 +774,12 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			}
 		}
 	};
-	// prologue: X results of rows yb-BS .. yb+BS (rows < 0 or >= Y are ghosts)
+	// prologue: X results of rows y0-BS .. y0+BS (rows < 0 or >= Y are ghosts);
+	// window slot k holds row y + S*(k - BS) of the current row y
+	const int y0 = REV ? ye - 1 : yb;
 #pragma unroll
 	for (int k = 0; k < W; k++) {
-		const int r = yb - BS + k;
+		const int r = y0 + S * (k - BS);
 		double xr[2][9];
 		if (r >= 0 && r < Y) {
 			XPre pre;
@@ -776,19 +792,22 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll
 				for (int j = 0; j < 9; j++) xr[t][j] = 0.0;
 		}
-		push(xr, k, r);  // rows yb-BS, yb-BS+1 are overwritten in the ring by yb+1, yb+2
+		push(xr, k, r);  // the first BS rows are overwritten in the ring by the last BS
 	}
 	if constexpr (FACES) {  // ghost rows of the prologue window: mirrors of inner rows
 		if (fb.on & 3u) {
 #pragma unroll
 			for (int k = 0; k < W; k++) {
-				const int r = yb - BS + k;
-				if (r < 0 && (fb.on & 1u)) mirror_slot(k, -r - (yb - BS), 0);
-				if (r >= Y && (fb.on & 2u)) mirror_slot(k, 2 * (Y - 1) - r - (yb - BS), 1);
+				const int r = y0 + S * (k - BS);
+				const int f = r < 0 ? 0 : 1, ks = BS + S * ((r < 0 ? -r : 2 * (Y - 1) - r) - y0);
+				if ((r < 0 || r >= Y) && ((fb.on >> f) & 1u) && ks >= 0 && ks < W) mirror_slot(k, ks, f);
 			}
 		}
 	}
-	auto clamp_row = [&](int r) { return r < Y + BS - 1 ? r : Y + BS - 1; };
+	auto clamp_row = [&](int r) {  // rows beyond the ghost rows (their X results go unused)
+		if constexpr (REV) return r > -BS ? r : -BS;
+		return r < Y + BS - 1 ? r : Y + BS - 1;
+	};
 
 #if GCMX_TX2_DIAG
 	unsigned long long dt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -801,7 +820,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		for (int t = 0; t < 2; t++) {
 			auto go = [&](const IsoAxis& A) {
 				node_update<1, BS, KF0>(
-				    A, [&](int j, int o) { return win[t][wslot(WMY, j)][BS + o]; },
+				    A, [&](int j, int o) { return win[t][wslot(WMY, j)][BS + S * o]; },
 				    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cp[(t * NCY + wslot(CMY, j)) * ZT]; },
 				    yv[t]);
 			};
@@ -831,8 +850,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 	// hand the Y results of row y to the Z stage: NB, own region + edge ring +
 	// counter; otherwise the block buffer between two barriers
-	auto publish = [&](int y, const double (&yv)[2][9]) {
-		const int es = y & 1;  // NB: edge ring slot of this row
+	auto publish = [&](int it, int y, const double (&yv)[2][9]) {
+		const int es = it & 1;  // NB: edge ring slot of this row (it: the row's place in the march)
 		if constexpr (NB) {
 			// this lane's edge slot (lanes < BS: left side, >= 64 - BS: right side);
 			// (node, component) as a constant LDS offset
@@ -855,7 +874,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				});
 			// edges in LDS before the counter says so (LDS only: global memory keeps flowing)
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-			__hip_atomic_store(&rdy[wv], y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			__hip_atomic_store(&rdy[wv], it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 		} else {
 			__syncthreads();  // every wave has finished reading zl (previous row's Z stage)
 #pragma unroll
@@ -880,14 +899,14 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		}
 	};
 	// NB: wait for the neighbour waves' edges of row y, copy them into the own halo slots
-	auto collect = [&](int y) {
+	auto collect = [&](int it) {
 		if constexpr (NB && NW > 1) {
-			const int es = y & 1;
+			const int es = it & 1;
 			for (;;) {
-				const int a = wv > 0 ? __hip_atomic_load(&rdy[wv - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
+				const int a = wv > 0 ? __hip_atomic_load(&rdy[wv - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : it;
 				const int b =
-				    wv < NW - 1 ? __hip_atomic_load(&rdy[wv + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : y;
-				if (__builtin_amdgcn_readfirstlane(min(a, b)) >= y) break;
+				    wv < NW - 1 ? __hip_atomic_load(&rdy[wv + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : it;
+				if (__builtin_amdgcn_readfirstlane(min(a, b)) >= it) break;
 				if constexpr (GCMX_TX2_SLEEP > 0) __builtin_amdgcn_s_sleep(GCMX_TX2_SLEEP);
 			}
 			asm volatile("" ::: "memory");
@@ -933,7 +952,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			for (int c = 0; c < 9; c++) stz(c, t, y, live ? zv[c] : 0.0);
 		}
 	};
-	// X stage of row y+BS+1 -> window slot W-1 (ghost rows: zero, or the y+ face's mirror)
+	// X stage of row y+S*(BS+1) -> window slot W-1 (ghost rows: zero, or a face's mirror)
 	auto x_enter = [&](int y, const XPre& pre, unsigned kn) {
 #pragma unroll
 		for (int t = 0; t < 2; t++)
@@ -948,26 +967,27 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		}
 		double xr[2][9];
 		sched_fence();
-		x_stage(pre, clamp_row(y + BS + 1), xr, kn);
-		push(xr, W - 1, y + BS + 1);
+		const int r = y + S * (BS + 1);
+		x_stage(pre, clamp_row(r), xr, kn);
+		push(xr, W - 1, r);
 		sched_fence();
 		if constexpr (FACES) {
-			const int r = y + BS + 1;
-			if ((fb.on & 2u) && r >= Y) {
-				const int ks = 2 * (Y - 1) - r - (y - BS + 1);
-				if (ks >= 0) mirror_slot(W - 1, ks, 1);
+			const int f = r < 0 ? 0 : 1;
+			if ((r < 0 || r >= Y) && ((fb.on >> f) & 1u)) {  // slot of the mirrored row in the next row's window
+				const int ks = BS + S * ((r < 0 ? -r : 2 * (Y - 1) - r) - (y + S));
+				if (ks >= 0 && ks < W) mirror_slot(W - 1, ks, f);
 			}
 		}
 	};
-	auto row = [&](int y) {
+	auto row = [&](int y, int it) {
 		double yv[2][9];
 		XPre pre;
-		const int rn = clamp_row(y + BS + 1);
+		const int rn = clamp_row(y + S * (BS + 1));
 		unsigned kn = 0;  // HET: row rn's materials, one row ahead of its X stage
 		if constexpr (HET) kn = key_of(rn);
 		y_stage(y, yv);
 		TX2_T(0);
-		publish(y, yv);
+		publish(it, y, yv);
 		TX2_T(2);
 		if constexpr (ZS2) {
 			sched_fence();
@@ -979,7 +999,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			sched_fence();
 		}
 		TX2_T(6);
-		collect(y);
+		collect(it);
 		TX2_T(4);
 #pragma unroll
 		for (int t = 0; t < 2; t++) {  // each node's stores right after its Z stage
@@ -996,13 +1016,16 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		x_enter(y, pre, kn);
 		TX2_T(5);
 	};
-	for (int y = yb; y < ye; y++) row(y);
+	for (int it = 0; it < ye - yb; it++) row(REV ? ye - 1 - it : yb + it, it);
 #if GCMX_TX2_DIAG
 	if ((threadIdx.x & 63) == 0) {
 		const int wv = threadIdx.x / 64;
 		for (int i = 0; i < 8; i++) atomicAdd(&g_tx2_diag[wv][i], dt_[i]);
 	}
 #endif
+	};
+	if (rev) run(std::true_type{});
+	else run(std::false_type{});
 }
 
 // ------------------------------------------------------------- launchers --
