@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void k_copy_box(double* __restrict__ dst, Geo 
 
 // cubic::BorderConditions::handleBorderPoint (engine/cubic/BorderConditions.hpp:94-114)
 // for a list of face nodes.  quantity codes: PhysicalQuantities::T.
-__device__ __forceinline__ int quantity_component(int D, int q) {
+__host__ __device__ __forceinline__ int quantity_component(int D, int q) {
 	// Vx..Vz = 2..4 ; Sxx,Sxy,Sxz,Syy,Syz,Szz = 5..10 (VelocitySigmaVariables.cpp:51-66)
 	if (q >= 2 && q <= 4) return (q - 2) < D ? q - 2 : -1;
 	if (q >= 5 && q <= 10) {
@@ -198,6 +198,34 @@ __global__ __launch_bounds__(256) void k_face_fill(double* __restrict__ cur, Geo
 	if (n == 1) base += i * g.stride[ax[0]];
 	if (n == 2) base += (i / ext[1]) * g.stride[ax[0]] + (i % ext[1]) * g.stride[ax[1]];
 	border_point(cur, g, base, axis, side > 0 ? -1 : 1, bq);
+}
+
+// The same for 3-D isotropic elasticity (9 components) and a condition without
+// PRESSURE, as (mask, 2 f(t)) per component -- the last setting of a component
+// wins, as in the quantity loop above: every component in registers, no
+// dynamically indexed arrays (the generic form keeps them in scratch memory);
+// one thread per (face node, component): blockIdx.y = the component.
+__global__ __launch_bounds__(256) void k_face_fill9(double* __restrict__ cur, Geo g, int axis, int side,
+                                                    FaceCond fc) {
+	const int a0 = axis == 0 ? 1 : 0, a1 = axis == 2 ? 1 : 2;  // the other two axes, last fastest
+	const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+	const long long n1 = g.sizes[a1];
+	if (i >= (long long)g.sizes[a0] * n1) return;
+	const long long base = g.origin + (long long)(side > 0 ? g.sizes[axis] - 1 : 0) * g.stride[axis] +
+	                       (i / n1) * g.stride[a0] + (i % n1) * g.stride[a1];
+	const int inner_sign = side > 0 ? -1 : 1;
+	const long long st = g.stride[axis];
+	const int c = blockIdx.y;
+	const bool set = (fc.mask >> c) & 1u;
+	double two = 0.0;
+#pragma unroll
+	for (int k = 0; k < 9; k++)
+		if (k == c) two = fc.two_v[k];
+	double* p = cur + (long long)c * g.cs;
+	for (int a = 1; a <= g.bs; a++) {
+		const double v = p[base + inner_sign * a * st];
+		p[base - inner_sign * a * st] = set ? -v + two : v;
+	}
 }
 
 // Every node of the face with a per-node condition map (gcmx_face_map): node i
@@ -339,8 +367,23 @@ void launch_face_fill(double* cur, const Geo& g, int axis, int side, const Borde
 	long long n = 1;
 	for (int d = 0; d < g.D; d++)
 		if (d != axis) n *= g.sizes[d];
-	hipLaunchKernelGGL(k_face_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cur, g, axis,
-	                   side, bq);
+	const dim3 grid((unsigned)((n + 255) / 256));
+	if (g.D == 3 && g.M == 9) {
+		FaceCond fc{};
+		bool plain = true;
+		for (int k = 0; k < bq.n && plain; k++) {
+			const int c = quantity_component(3, bq.q[k]);
+			if (bq.q[k] == 12) plain = false;  // PRESSURE: the generic form
+			if (c < 0) continue;
+			fc.mask |= 1u << c;
+			fc.two_v[c] = 2 * bq.v[k];
+		}
+		if (plain) {
+			hipLaunchKernelGGL(k_face_fill9, dim3(grid.x, 9), dim3(256), 0, st, cur, g, axis, side, fc);
+			return;
+		}
+	}
+	hipLaunchKernelGGL(k_face_fill, grid, dim3(256), 0, st, cur, g, axis, side, bq);
 }
 
 void launch_face_fill_map(double* cur, const Geo& g, int axis, int side, const uint8_t* map_d,
