@@ -47,6 +47,11 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--no-check", action="store_true")
 ap.add_argument("--reps", type=int, default=5, help="timed repetitions of --steps steps (median)")
 args = ap.parse_args()
+if args.rccl_self and len(args.ranks.split(",")) > 1:
+    # RCCL reads NCCL_NCHANNELS_PER_PEER once per process: the first
+    # communicator's channel rule (gcmx_comm_init) would hold for every later
+    # slab thickness.  One process per rank count (profiles/r4/slab2/).
+    sys.exit("--rccl-self: give one --ranks value per process (RCCL caches the channel count per process)")
 U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
 N, STEPS = args.n, args.steps
 SCHED = {"xslab": gcmx.SCHED_XSLAB, "bfirst": gcmx.SCHED_BFIRST}.get(args.sched, gcmx.SCHED_SINGLE)
