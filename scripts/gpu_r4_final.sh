@@ -26,4 +26,4 @@ for a in "free512:--n 512 --steps 10" "het512:--n 512 --steps 10 --layers" "hetm
   timeout -k 10 300 python3 scripts/bench_physics.py $args > $OUT/phys_$n.json 2> $OUT/phys_$n.err || { echo "$n rc=$?"; exit 1; }
   tail -1 $OUT/phys_$n.json
 done
-TAG=r4final timeout -k 10 900 bash scripts/gpu_profile.sh > $OUT/profile.log 2>&1; echo "profile rc=$?"; tail -3 $OUT/profile.log
+TAG=${PTAG:-r4final} timeout -k 10 900 bash scripts/gpu_profile.sh > $OUT/profile.log 2>&1; echo "profile rc=$?"; tail -3 $OUT/profile.log
