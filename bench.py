@@ -19,6 +19,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from tools import box_state  # noqa: E402  (read-only amdgpu sysfs, measurement context)
+
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 BYTES_PER_NODE_STAGE = 2 * 9 * 8  # read + write the 9-component fp64 state
 
@@ -49,6 +51,12 @@ def parse():
     p.add_argument("--prealloc-gb", type=float, default=0.0,
                    help="measurement only: hold a device buffer of this size (torch) while the "
                         "layers are allocated (shifts their placement in HBM)")
+    p.add_argument("--rccl-self", action="store_true",
+                   help="one GPU: the slab is a one-rank RCCL communicator whose neighbours are "
+                        "itself (gcmx_comm_init(.., 1, 0, 0, 0)): the real ncclSend/ncclRecv group "
+                        "runs every step and the line carries per_rank (exchange timings)")
+    p.add_argument("--no-box-state", action="store_true",
+                   help="do not read / sample the GPU's amdgpu sysfs (tools/box_state.py)")
     p.add_argument("--no-clock-probe", action="store_true",
                    help="no co-resident clock-sampling wave during the timed repetitions")
     p.add_argument("--emulate-slabs", type=int, default=0, metavar="K",
@@ -186,7 +194,35 @@ def clock_summary(samples) -> dict:
             "mhz_p90": round(float(np.percentile(mhz, 90)), 1)}
 
 
-def multi_gpu_parity(dist, world, rank, device, U, U1, L):
+def rank_record(ctx, rank, kernels, steps_total, step_ms):
+    """One rank's exchange / compute split over the timed repetitions, from the
+    library's hipEvent buckets (gcmx_profile_*): the interior and boundary
+    launches, the RCCL group on the comm stream from data-ready to its last
+    kernel (`halo_ms`, per post), the time the compute stream stood still
+    waiting for it (`exposed_wait_ms`, per step: the part of the exchange not
+    hidden behind compute), the bytes one link direction carries per post and
+    the rate that gives."""
+    def avg(name):
+        v = kernels.get(name)
+        return v["total_ms"] / v["launches"] if v and v["launches"] else 0.0
+    hname = "halo_rccl" if "halo_rccl" in kernels else ("halo_loopback" if "halo_loopback" in kernels else None)
+    h = kernels.get(hname) if hname else None
+    halo_ms = avg(hname) if hname else 0.0
+    wait = kernels.get("halo_wait")
+    bytes_dir = h["bytes_per_launch"] if h else 0.0
+    return {"rank": rank, "step_ms": round(step_ms, 4),
+            "interior_ms": round(avg("fused_xyz"), 4),
+            "boundary_ms": round(avg("fused_xyz_boundary"), 4),
+            "halo_ms": round(halo_ms, 4),
+            "halo_posts_per_step": round(h["launches"] / steps_total, 3) if h else 0.0,
+            "exposed_wait_ms": round(wait["total_ms"] / steps_total, 4) if wait else 0.0,
+            "bytes_per_direction": bytes_dir,
+            "GBps_per_direction": round(bytes_dir / (halo_ms * 1e-3) / 1e9, 1) if halo_ms > 0 else None,
+            "transport": hname,
+            "channels_per_peer": ctx.comm_channels_per_peer}
+
+
+def multi_gpu_parity(dist, world, rank, device, U, U1, L, channels):
     """N > 1 self-check of the RCCL X-slab path (halo exchange overlapped with the
     interior X stage): 3 steps on a 12*N x 40 x 64 grid split into N slabs must
     equal, bitwise, the same grid run whole on rank 0's GPU."""
@@ -200,8 +236,10 @@ def multi_gpu_parity(dist, world, rank, device, U, U1, L):
     c.fill_random([Xg, Y, Z], seed)
     obj = [gcm_amd.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
+    # RCCL fixes the channels per peer at the process's first communicator (the
+    # bench's): this one uses the same count (gcmx.h, checked contract)
     c.comm_init(obj[0], world, rank, rank - 1 if rank > 0 else -1,
-                rank + 1 if rank < world - 1 else -1, global_x=Xg)
+                rank + 1 if rank < world - 1 else -1, global_x=Xg, channels_per_peer=channels)
     for _ in range(3):
         c.step(0.9)
     mine = c.download().reshape(Xs + 2 * bs, Y + 2 * bs, Z + 2 * bs, 9)[bs:-bs, bs:-bs, bs:-bs]
@@ -346,6 +384,12 @@ def main():
     U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
     tau = 0.9 * 1.0 / 1.0  # Courant * h / max|lambda| (Engine.cpp:124-140)
 
+    box = None
+    if rank == 0 and not a.no_box_state:
+        try:
+            box = box_state.static_state(device)
+        except Exception as e:  # reported context, never required
+            box = {"error": str(e)}
     t_setup = time.perf_counter()
     hold = None
     if a.prealloc_gb > 0:  # measurement only: shifts the layers' placement
@@ -364,10 +408,12 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         ctx.comm_init(obj[0], world, rank, rank - 1 if rank > 0 else -1,
                       rank + 1 if rank < world - 1 else -1, global_x=N)
+    elif a.rccl_self:
+        ctx.comm_init(gcm_amd.unique_id(), 1, 0, 0, 0)
     ctx.sync()
     parity = None
     if world > 1:
-        parity = multi_gpu_parity(dist, world, rank, device, U, U1, L)
+        parity = multi_gpu_parity(dist, world, rank, device, U, U1, L, ctx.comm_channels_per_peer)
         log(f"[rank {rank}] multi-GPU slab parity: {parity}")
     log(f"[rank {rank}] slab x[{x0},{x0 + X}) of {N}^3, {ctx.device_bytes / 1e9:.1f} GB, "
         f"path {ctx.effective_path}, setup {time.perf_counter() - t_setup:.1f}s")
@@ -394,7 +440,15 @@ def main():
     if not a.no_profile:
         ctx.profile(True)
         ctx.profile_reset()
+    sampler = None
+    if rank == 0 and not a.no_box_state:
+        try:
+            sampler = box_state.Sampler(device).start()
+        except Exception as e:  # reported context, never required
+            log(f"box-state sampler failed: {e}")
     rep_s = []
+    rep_kernels = []  # per repetition: the profile's totals accumulated in that repetition
+    prev = {}
     for _ in range(max(1, a.reps)):
         barrier()
         ctx.sync()
@@ -409,6 +463,13 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = float(tt.item())
         rep_s.append(el)
+        if not a.no_profile:
+            cur = ctx.profile_read()
+            rep_kernels.append({k: (v["total_ms"] - prev.get(k, {}).get("total_ms", 0.0),
+                                    v["launches"] - prev.get(k, {}).get("launches", 0))
+                                for k, v in cur.items()})
+            prev = cur
+    sampled = sampler.stop() if sampler is not None else None
     if not a.no_clock_probe:
         clock = clock_summary(ctx.clock_probe_read())
     kernels = {}
@@ -416,19 +477,39 @@ def main():
         kernels = ctx.profile_read()
         ctx.profile(False)
     el = sorted(rep_s)[len(rep_s) // 2]
+    per_rank = None
+    if (world > 1 or a.rccl_self) and kernels:
+        rec = rank_record(ctx, rank, kernels, a.steps * max(1, a.reps), el / a.steps * 1e3)
+        if dist is not None:
+            recs = [None] * world if rank == 0 else None
+            dist.gather_object(rec, recs, dst=0)
+            per_rank = recs
+        else:
+            per_rank = [rec]
+    # the kernel statistic that matches ms_per_step: the median over the
+    # repetitions of each repetition's mean launch duration
+    rep_avg = {}
+    for k in kernels:
+        avgs = sorted(t / n for t, n in (r.get(k, (0.0, 0)) for r in rep_kernels) if n > 0)
+        if avgs:
+            rep_avg[k] = avgs[len(avgs) // 2]
 
     total_nodes = N ** 3
     value = total_nodes * a.steps / el / 1e6
     roof = None
     if kernels:
         dom_name, dom = max(kernels.items(), key=lambda kv: kv[1]["total_ms"])
-        avg_ms = dom["total_ms"] / max(1, dom["launches"])
+        mean_ms = dom["total_ms"] / max(1, dom["launches"])
+        avg_ms = rep_avg.get(dom_name, mean_ms)
         achieved = dom["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic(N, world, dom_name, dom["kernel"])
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": dom_name, "kernel_avg_ms": round(avg_ms, 4),
+                "kernel": dom_name,
+                # median over the repetitions of each one's mean launch time (the same
+                # statistic as ms_per_step); the mean over every launch beside it
+                "kernel_avg_ms": round(avg_ms, 4), "kernel_mean_all_ms": round(mean_ms, 4),
                 # the instance the library reports it launched (gcmx_profile_kernel)
                 "kernel_symbol": dom["kernel"],
                 "algorithmic_bytes_per_launch": dom["bytes_per_launch"],
@@ -471,8 +552,9 @@ def main():
             "config": {"workload": f"3-D isotropic elastic CubicGrid {N}^3, borderSize 2, "
                                    f"Courant 0.9, tau 0.9, one full time step (3 stages)",
                        "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,
-                       "parallelism": f"x-slab{world}" if world > 1 else "single",
-                       **({"rccl_channels_per_peer": ctx.comm_channels_per_peer} if world > 1 else {}),
+                       "parallelism": f"x-slab{world}" if world > 1 else
+                                      ("single, RCCL self-exchange (one-rank communicator)" if a.rccl_self else "single"),
+                       **({"rccl_channels_per_peer": ctx.comm_channels_per_peer} if world > 1 or a.rccl_self else {}),
                        # the one-pass step's floating-point build (gcmx_set_fp_mode): "fma" =
                        # multiply-adds contracted, the product default, held to the north
                        # star's 1e-10 relative L2 of the reference (tests/test_gpu_fma.py);
@@ -485,10 +567,16 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "multi_gpu_parity": parity,
+            # N > 1 (or --rccl-self): every rank's exchange / compute split (rank_record)
+            "per_rank": per_rank,
             # what distinguishes one process's run from another's on the same box
             # (VERDICT r3 item 1): the layers' placement, the clock under load,
             # the allocation order
             "process_state": {"layers": placement, "clock": clock,
+                              # the box: partition modes, power cap,
+                              # firmware, DPM tables (tools/box_state.py), and the DPM
+                              # levels / power / temperatures sampled during the reps
+                              "box": box, "box_during_reps": sampled,
                               "alloc_order": (f"torch buffer {a.prealloc_gb} GiB, " if hold is not None else "")
                                              + ("layers A+gap+B in one allocation" if placement["one_allocation"]
                                                 else "layer A, layer B, tables"),

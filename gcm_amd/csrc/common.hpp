@@ -86,6 +86,28 @@ __device__ __forceinline__ double vmin(double a, double b) {
 #endif
 }
 
+// The reference's limiter, `if (ans > max) ans = max; else if (ans < min) ans =
+// min` with max / min of the segment ends a, b, returns the median of {ans, a, b}
+// for every non-NaN input.  gfx950 has no v_med3_f64, and the clamp form
+// min(max(ans, min(a, b)), max(a, b)) takes four v_*_f64; this one takes three:
+//   lo = min(x, a), hi = max(x, a):  b >= hi -> hi;  b <= lo -> lo;  else b.
+// Each result is one of the three inputs, so it is the clamp's value (only the
+// sign of an exact zero may differ, as for the clamp form).
+#ifndef GCMX_MED3
+#define GCMX_MED3 1
+#endif
+__device__ __forceinline__ double vmed3(double x, double a, double b) {
+	return vmax(vmin(x, a), vmin(vmax(x, a), b));
+}
+// limit(ans) for the segment (a, b)
+__device__ __forceinline__ double vlimit(double ans, double a, double b) {
+#if GCMX_MED3
+	return vmed3(ans, a, b);
+#else
+	return vmin(vmax(ans, vmin(a, b)), vmax(a, b));
+#endif
+}
+
 // EqualDistanceLineInterpolator::minMaxInterpolate for ONE component
 // (EqualDistanceLineInterpolator.hpp:18-43 + 56-71).  s[0..BS] are the values
 // at the node and its BS neighbours on the foot side.  The Newton recurrence
@@ -101,8 +123,6 @@ __device__ __forceinline__ double newton_minmax(const double (&s)[BS + 1], int k
 		for (int i = 1; i < BS; i++)
 			if (kf == i) { lo = s[i]; hi = s[i + 1]; }
 	}
-	const double mx = vmax(lo, hi);
-	const double mn = vmin(lo, hi);
 	double d[BS + 1];
 #pragma unroll
 	for (int i = 0; i <= BS; i++) d[i] = s[i];
@@ -115,11 +135,12 @@ __device__ __forceinline__ double newton_minmax(const double (&s)[BS + 1], int k
 		ans += d[0];
 	}
 	// if (ans > max) ans = max; else if (ans < min) ans = min;
-	// == min(max(ans, mn), mx) for every non-NaN ans (mn <= mx); only the sign of
-	// an exact zero may differ.
+	// == median(ans, lo, hi) for every non-NaN ans; only the sign of an exact zero
+	// may differ.
 #if GCMX_CLAMP_MINMAX
-	return vmin(vmax(ans, mn), mx);
+	return vlimit(ans, lo, hi);
 #else
+	const double mx = vmax(lo, hi), mn = vmin(lo, hi);
 	return (ans > mx) ? mx : ((ans < mn) ? mn : ans);
 #endif
 }

@@ -147,6 +147,7 @@ struct gcmx_ctx {
 	bool comm_stall = false;        // tests only (gcmx_comm_test_stall): post sends, never receives
 	double comm_timeout_s = 60.0;   // bound of every host wait on RCCL work
 	int channels_per_peer = -1;     // NCCL_NCHANNELS_PER_PEER in effect (0: RCCL's default)
+	long long halo_posted_calls = 0;  // ncclSend + ncclRecv calls posted (gcmx_comm_posted_calls)
 	int nranks = 1, rank = 0, left = -1, right = -1;
 	bool halo_pending = false;     // an exchange is in flight on comm_stream (ev_halo)
 	bool step_posted = false;      // the current step posted its new boundary planes already
@@ -634,33 +635,57 @@ gcmx_status halo_post(gcmx_ctx* c) {
 	// ghost planes [-bs, 0) and [X, X+bs); inner planes [0, bs) and [X-bs, X).
 	HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
 	HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-	ncclResult_t r = ncclGroupStart();
-	if (r != ncclSuccess) return fail(GCMX_ERR_COMM, std::string("ncclGroupStart: ") + ncclGetErrorString(r));
-	// Every failure inside the group still closes it (an open group would
-	// corrupt every later call on the communicator).
-	std::string what;
-	for (int comp : c->halo_comps) {
-		if (r == ncclSuccess && c->left >= 0) {
-			what = "ncclSend/Recv left";
-			r = ncclSend(plane_ptr(c, c->cur, comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream);
-			if ((r == ncclSuccess || r == ncclInProgress) && !c->comm_stall)
-				r = ncclRecv(plane_ptr(c, c->cur, comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream);
+	{
+		// Profiling: the group on comm_stream, from the moment its data is ready
+		// (the compute stream passed ev_ready) to its last kernel; bytes = what
+		// this rank sends to ONE neighbour, i.e. what one link direction carries.
+		Timed t(c, "halo_rccl", 8.0 * (double)n * (double)c->halo_comps.size(), c->comm_stream);
+		t.kname = "ncclGroupStart/ncclSend/ncclRecv/ncclGroupEnd";
+		ncclResult_t r = ncclGroupStart();
+		if (r != ncclSuccess) return fail(GCMX_ERR_COMM, std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+		// Non-blocking communicator: a call may return ncclInProgress, which is
+		// success so far; every later call of the group is still posted.  Every
+		// failure inside the group still closes it (an open group would corrupt
+		// every later call on the communicator).
+		auto ok = [](ncclResult_t v) { return v == ncclSuccess || v == ncclInProgress; };
+		std::string what;
+		int posted = 0;
+		for (int comp : c->halo_comps) {
+			if (ok(r) && c->left >= 0) {
+				what = "ncclSend/Recv left";
+				r = ncclSend(plane_ptr(c, c->cur, comp, 0), n, ncclDouble, c->left, c->comm, c->comm_stream);
+				posted += ok(r);
+				if (ok(r) && !c->comm_stall) {
+					r = ncclRecv(plane_ptr(c, c->cur, comp, -c->bs), n, ncclDouble, c->left, c->comm, c->comm_stream);
+					posted += ok(r);
+				}
+			}
+			if (ok(r) && c->right >= 0) {
+				what = "ncclSend/Recv right";
+				r = ncclSend(plane_ptr(c, c->cur, comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream);
+				posted += ok(r);
+				if (ok(r) && !c->comm_stall) {
+					r = ncclRecv(plane_ptr(c, c->cur, comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream);
+					posted += ok(r);
+				}
+			}
 		}
-		if (r == ncclSuccess && c->right >= 0) {
-			what = "ncclSend/Recv right";
-			r = ncclSend(plane_ptr(c, c->cur, comp, X - c->bs), n, ncclDouble, c->right, c->comm, c->comm_stream);
-			if ((r == ncclSuccess || r == ncclInProgress) && !c->comm_stall)
-				r = ncclRecv(plane_ptr(c, c->cur, comp, X), n, ncclDouble, c->right, c->comm, c->comm_stream);
-		}
+		const ncclResult_t re = ncclGroupEnd();
+		if (!ok(r)) return comm_fail(c, what + ": " + ncclGetErrorString(r));
+		if (!ok(re)) return comm_fail(c, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
+		// every (component, neighbour) pair posted its send and, unless stalled on
+		// purpose (tests), its receive: nothing of the group was skipped
+		const int peers = (c->left >= 0) + (c->right >= 0);
+		const int want = (int)c->halo_comps.size() * peers * (c->comm_stall ? 1 : 2);
+		if (posted != want)
+			return comm_fail(c, "halo exchange group: " + std::to_string(posted) + " of " + std::to_string(want) +
+			                        " sends / receives posted");
+		c->halo_posted_calls += posted;
+		// non-blocking communicator: the group's kernels are on comm_stream once its
+		// state leaves ncclInProgress; ev_halo must be recorded after them
+		gcmx_status se = comm_settle(c, "halo exchange group");
+		if (se) return se;
 	}
-	const ncclResult_t re = ncclGroupEnd();
-	if (r != ncclSuccess && r != ncclInProgress) return comm_fail(c, what + ": " + ncclGetErrorString(r));
-	if (re != ncclSuccess && re != ncclInProgress)
-		return comm_fail(c, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
-	// non-blocking communicator: the group's kernels are on comm_stream once its
-	// state leaves ncclInProgress; ev_halo must be recorded after them
-	gcmx_status se = comm_settle(c, "halo exchange group");
-	if (se) return se;
 	HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
 	c->halo_pending = true;
 	c->halo_layer = c->cur;
@@ -669,11 +694,17 @@ gcmx_status halo_post(gcmx_ctx* c) {
 
 gcmx_status halo_wait(gcmx_ctx* c) {
 	if (!c->halo_pending) return GCMX_OK;
-	if (c->lc) {
-		gcmx_status s = local_wait(c);
-		if (s) return s;
-	} else {
-		HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+	{
+		// Profiling: how long the compute stream stands still at this wait, i.e.
+		// the part of the exchange that is NOT hidden behind compute (an event on
+		// the stream before the wait, one after it)
+		Timed t(c, "halo_wait", 0.0, c->stream);
+		if (c->lc) {
+			gcmx_status s = local_wait(c);
+			if (s) return s;
+		} else {
+			HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+		}
 	}
 	c->halo_pending = false;
 	c->halo_fresh = c->halo_layer == c->cur;
@@ -1907,13 +1938,36 @@ gcmx_status gcmx_comm_unique_id(uint8_t id[GCMX_UNIQUE_ID_BYTES]) {
 // default.  A rank with two distinct peers may need up to twice the CTAs, so
 // the count is sized for that: free CUs / 4, i.e. 4 with >= 16 free CUs, 2 with
 // >= 8, else RCCL's own (0).
-static int channels_for_slab(const Geo& g0, int X, int rows_per_block) {
-	Geo g = g0;
+static int channels_for_slab(int X, int Y, int Z, int bs, int rows_per_block, int cus) {
+	// the one-pass step's launch geometry of an X x Y x Z slab (only what
+	// step_free_cus reads: sizes, bs, the layout's 32-bit addressing bound)
+	Geo g{};
+	g.D = 3;
+	g.M = 9;
+	g.bs = bs;
 	g.sizes[0] = X;
-	g.gx0 = 0;
-	const int bs = g.bs;
-	const int free_cus = X > 2 * bs ? step_free_cus(g, bs, X - bs, rows_per_block) : -1;
+	g.sizes[1] = Y;
+	g.sizes[2] = Z;
+	const long long row = round_up(round_up(bs, kRowAlign) + Z + bs, kRowAlign);
+	g.stride[2] = 1;
+	g.stride[1] = row;
+	g.stride[0] = row * (Y + 2LL * bs);
+	g.cs = round_up(g.stride[0] * (X + 2LL * bs), 64);
+	const int free_cus = X > 2 * bs ? step_free_cus(g, bs, X - bs, rows_per_block, cus) : -1;
 	return free_cus >= 16 ? 4 : free_cus >= 8 ? 2 : 0;
+}
+
+// Process-wide: RCCL reads NCCL_NCHANNELS_PER_PEER once per process, so the
+// channels per peer of every communicator in the process are those in effect
+// when its first one was created (g_rccl_channels, -1 before that);
+// g_rccl_user_env: the user set NCCL_NCHANNELS_PER_PEER, which overrides the rule.
+static std::mutex g_rccl_mu;
+static int g_rccl_channels = -1;
+static bool g_rccl_user_env = false;
+
+static int env_int(const char* name, int dflt) {
+	const char* e = std::getenv(name);
+	return (e && *e) ? std::atoi(e) : dflt;
 }
 
 gcmx_status gcmx_comm_init_opts(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], int nranks, int rank,
@@ -1929,11 +1983,11 @@ gcmx_status gcmx_comm_init_opts(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYT
 	gcmx_comm_options o;
 	if (opt) {
 		o = *opt;
-	} else {
+	} else {  // defaults, each overridable from the environment (gcmx.h)
 		o.global_x = 0;
-		o.channels_per_peer = -1;
-		o.min_ctas = -1;
-		o.max_ctas = -1;
+		o.channels_per_peer = env_int("GCMX_COMM_CHANNELS_PER_PEER", -1);
+		o.min_ctas = env_int("GCMX_COMM_MIN_CTAS", -1);
+		o.max_ctas = env_int("GCMX_COMM_MAX_CTAS", -1);
 		o.timeout_s = 0;
 	}
 	if (o.global_x < 0 || o.channels_per_peer < -1 || o.channels_per_peer > 64)
@@ -1952,19 +2006,38 @@ gcmx_status gcmx_comm_init_opts(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYT
 	// X extent, the rank count, Y, Z, borderSize and the library's block rule --
 	// applied to the THINNEST slab of an even split (floor(global_x / nranks)
 	// planes); a one-rank communicator (the self-exchange) uses its own slab.
-	// Without global_x the rule cannot be rank-consistent: RCCL's default.  The
-	// value reaches RCCL through NCCL_NCHANNELS_PER_PEER, which RCCL reads once
-	// per process (the first communicator decides), unless the user set it.
-	int per_peer = o.channels_per_peer;
-	if (per_peer < 0) {
-		if (nranks == 1) per_peer = channels_for_slab(c->geo, c->geo.sizes[0], c->rows_per_block);
-		else if (o.global_x > 0) per_peer = channels_for_slab(c->geo, o.global_x / nranks, c->rows_per_block);
-		else per_peer = 0;
+	// Without global_x the rule cannot be rank-consistent: RCCL's default
+	// (gcmx_comm_channels_rule).  The value reaches RCCL through
+	// NCCL_NCHANNELS_PER_PEER, which RCCL reads ONCE per process: the checked
+	// contract below sets it (only) before the process's first communicator and
+	// refuses a later communicator that needs another count (GCMX_ERR_STATE)
+	// instead of letting it silently run with the first one's.
+	const int Dg = c->geo.D;
+	const int want = o.channels_per_peer >= 0
+	                     ? o.channels_per_peer
+	                     : gcmx_comm_channels_rule(o.global_x, nranks, c->geo.sizes[0], Dg > 1 ? c->geo.sizes[1] : 1,
+	                                               Dg > 2 ? c->geo.sizes[2] : 1, c->bs, c->rows_per_block, 0);
+	{
+		std::lock_guard<std::mutex> lk(g_rccl_mu);
+		if (g_rccl_channels < 0) {  // the process's first communicator: RCCL's value is still open
+			if (const char* e = std::getenv("NCCL_NCHANNELS_PER_PEER")) {
+				g_rccl_user_env = true;  // the user's choice overrides the rule
+				g_rccl_channels = std::atoi(e);
+			} else {
+				if (want > 0) setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(want).c_str(), 1);
+				g_rccl_channels = want;
+			}
+		} else if (!g_rccl_user_env && want != g_rccl_channels) {
+			return fail(GCMX_ERR_STATE,
+			            "RCCL channels per peer are fixed at " + std::to_string(g_rccl_channels) +
+			                " in this process (RCCL reads NCCL_NCHANNELS_PER_PEER once, at its first communicator); "
+			                "this communicator needs " +
+			                std::to_string(want) +
+			                ": pass gcmx_comm_options.channels_per_peer = " + std::to_string(g_rccl_channels) +
+			                " (every rank alike), or create it in a process of its own");
+		}
+		c->channels_per_peer = g_rccl_channels;
 	}
-	c->channels_per_peer = per_peer;
-	if (per_peer > 0 && !std::getenv("NCCL_NCHANNELS_PER_PEER"))
-		setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(per_peer).c_str(), 0);
-	if (const char* e = std::getenv("NCCL_NCHANNELS_PER_PEER")) c->channels_per_peer = std::atoi(e);
 	c->comm_timeout_s = o.timeout_s > 0 ? o.timeout_s : comm_timeout_seconds();
 	// Non-blocking communicator: every RCCL call returns at once and its state is
 	// polled (comm_settle) under the timeout, so a dead or missing peer surfaces
@@ -1995,6 +2068,16 @@ gcmx_status gcmx_comm_init(gcmx_ctx* c, const uint8_t id[GCMX_UNIQUE_ID_BYTES], 
 }
 
 int gcmx_comm_channels_per_peer(const gcmx_ctx* c) { return c ? c->channels_per_peer : -1; }
+
+int gcmx_comm_channels_rule(int global_x, int nranks, int local_x, int Y, int Z, int bs, int rows_per_block,
+                            int cus) {
+	if (nranks < 1 || global_x < 0 || local_x < 1 || Y < 1 || Z < 1 || bs < 1 || bs > kMaxBs) return -1;
+	if (nranks == 1) return channels_for_slab(local_x, Y, Z, bs, rows_per_block, cus);
+	if (global_x == 0) return 0;  // not rank-consistent without the global extent: RCCL's default
+	return channels_for_slab(global_x / nranks, Y, Z, bs, rows_per_block, cus);
+}
+
+long long gcmx_comm_posted_calls(const gcmx_ctx* c) { return c ? c->halo_posted_calls : -1; }
 
 gcmx_status gcmx_comm_test_stall(gcmx_ctx* c, int on) {
 	if (!c) return fail(GCMX_ERR_INVALID_ARG, "null context");

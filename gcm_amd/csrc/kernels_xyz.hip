@@ -601,7 +601,6 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				for (int i = 1; i <= BS; i++)
 #pragma unroll
 					for (int k = 0; k + i < WX; k++) D[i][k] = (D[i - 1][k + 1] - D[i - 1][k]) * c[i - 1];
-				double mx[WX - 1], mn[WX - 1];  // bounds of segment (k, k+1)
 #pragma unroll
 				for (int t = 0; t < 2; t++) {
 					const int m = t + BS;
@@ -611,19 +610,11 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 						a += D[i][m];
 						b = (i % 2) ? b - D[i][m - i] : b + D[i][m - i];
 					}
-					const double mxp = vmax(D[0][m], D[0][m + 1]), mnp = vmin(D[0][m], D[0][m + 1]);
-					double mxm, mnm;
-					if (t == 1) {  // the -x segment of node 1 is the +x segment of node 0
-						mxm = mx[m - 1];
-						mnm = mn[m - 1];
-					} else {
-						mxm = vmax(D[0][m], D[0][m - 1]);
-						mnm = vmin(D[0][m], D[0][m - 1]);
-					}
-					mx[m] = mxp;
-					mn[m] = mnp;
-					ip[v][t] = vmin(vmax(a, mnp), mxp);
-					im[v][t] = vmin(vmax(b, mnm), mxm);
+					// limiter segments (m, m+1) and (m, m-1): the median form (common.hpp
+					// vlimit) takes three ops per foot, less than sharing the segment
+					// bounds of node 0's +x foot with node 1's -x foot (2 + 2 per foot)
+					ip[v][t] = vlimit(a, D[0][m], D[0][m + 1]);
+					im[v][t] = vlimit(b, D[0][m], D[0][m - 1]);
 				}
 			}
 #pragma unroll
@@ -1199,11 +1190,11 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 // CUs the one-pass step leaves free while it covers planes [x0, x1) in one
 // round (the slab interior of the boundary-first schedule); 0 when its blocks
 // fill every CU or it takes more than one round, -1 when k_step_tx2 does not run.
-int step_free_cus(const Geo& g, int x0, int x1, int req_chunk) {
+int step_free_cus(const Geo& g, int x0, int x1, int req_chunk, int cus_in) {
 	const int Z = g.sizes[2];
 	if (!fused_supported(g) || g.bs > 2 || Z > 512 || x1 <= x0) return -1;
 	const int ZT = Z <= 64 ? 64 : Z <= 128 ? 128 : Z <= 256 ? 256 : 512;
-	const int per_cu = 512 / ZT, cus = GCMX_XYZ_NS::device_cus();
+	const int per_cu = 512 / ZT, cus = cus_in > 0 ? cus_in : GCMX_XYZ_NS::device_cus();
 	const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2;
 	const int chunk = GCMX_XYZ_NS::tx2_chunk_for(g.sizes[1], npair, req_chunk, cus * per_cu);
 	const long long blocks = (long long)((g.sizes[1] + chunk - 1) / chunk) * npair;

@@ -124,7 +124,7 @@ bool het_supported(const Geo& g);
 // `kname`: set to the launched instance's symbol (a static string).
 // [xb0, xb1): an optional second plane range (xb0 >= x1) covered by the same
 // launch (the X-slab boundary sides; two launches on the k_fused_xyz path).
-int step_free_cus(const Geo& g, int x0, int x1, int req_chunk);
+int step_free_cus(const Geo& g, int x0, int x1, int req_chunk, int cus = -1);  // cus <= 0: the device's
 // Two builds of the one-pass step kernels (kernels_xyz.hip): xyz_exact keeps the
 // reference's roundings (bitwise), xyz_fma contracts multiply-adds
 // (gcmx_set_fp_mode).

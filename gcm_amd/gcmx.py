@@ -7,6 +7,7 @@ missing or no GPU is present, construction fails loudly.
 from __future__ import annotations
 
 import ctypes
+import weakref
 import os
 from typing import Optional, Sequence
 
@@ -44,7 +45,7 @@ SYMBOLS = [
     "gcmx_copy_box",
     "gcmx_ode_maxwell", "gcmx_step_ode", "gcmx_last_ode_fused",
     "gcmx_comm_unique_id", "gcmx_comm_init_opts", "gcmx_comm_init", "gcmx_comm_channels_per_peer",
-    "gcmx_comm_test_stall", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
+    "gcmx_comm_channels_rule", "gcmx_comm_posted_calls", "gcmx_comm_test_stall", "gcmx_halo_exchange", "gcmx_halo_exchange_group",
     "gcmx_comm_init_local", "gcmx_local_group_steps", "gcmx_comm_init_loopback",
     "gcmx_sync", "gcmx_stream",
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_profile_kernel",
@@ -147,6 +148,10 @@ def lib() -> ctypes.CDLL:
                                       ctypes.c_int, ctypes.c_int, ctypes.POINTER(CommOptions)]
     L.gcmx_comm_channels_per_peer.argtypes = [vp]
     L.gcmx_comm_channels_per_peer.restype = ctypes.c_int
+    L.gcmx_comm_channels_rule.argtypes = [ctypes.c_int] * 8
+    L.gcmx_comm_channels_rule.restype = ctypes.c_int
+    L.gcmx_comm_posted_calls.argtypes = [vp]
+    L.gcmx_comm_posted_calls.restype = ctypes.c_longlong
     L.gcmx_comm_test_stall.argtypes = [vp, ctypes.c_int]
     L.gcmx_halo_exchange.argtypes = [vp]
     L.gcmx_halo_exchange_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
@@ -221,7 +226,16 @@ class Context:
         self.shape_all = tuple(s + 2 * border_size for s in self.sizes)
         self.n_all = int(np.prod(self.shape_all))
 
+    def _adopt(self, child):
+        """FaceMap / BorderNodes of this context: closed before the context is
+        (their native destroy reads the context's device and stream)."""
+        if not hasattr(self, "_children"):
+            self._children = weakref.WeakSet()
+        self._children.add(child)
+
     def close(self):
+        for ch in list(getattr(self, "_children", ())):
+            ch.close()
         if getattr(self, "_ptr", None) and self._ptr.value:
             lib().gcmx_destroy(self._ptr)
             self._ptr = ctypes.c_void_p()
@@ -394,6 +408,11 @@ class Context:
     def comm_channels_per_peer(self) -> int:
         return lib().gcmx_comm_channels_per_peer(self._ptr)
 
+    @property
+    def comm_posted_calls(self) -> int:
+        """ncclSend + ncclRecv calls the exchange groups posted (gcmx_comm_posted_calls)."""
+        return lib().gcmx_comm_posted_calls(self._ptr)
+
     def comm_test_stall(self, on: bool = True):
         """Tests only: exchange groups post sends but never receives."""
         _check(lib().gcmx_comm_test_stall(self._ptr, 1 if on else 0))
@@ -478,11 +497,14 @@ class FaceMap:
         ptrs = (ctypes.c_void_p * 6)(*[None if m is None else m.ctypes.data for m in self._maps])
         self.ptr = ctypes.c_void_p()
         _check(lib().gcmx_face_map_create(ctx.ptr, ptrs, ctypes.byref(self.ptr)))
+        ctx._adopt(self)
 
     def close(self):
-        if self.ptr and self.ptr.value:
+        # the native destroy reads the context: after Context.close (which closes
+        # its children first) there is nothing left to free here
+        if self.ptr and self.ptr.value and self._ctx.ptr.value:
             lib().gcmx_face_map_destroy(self.ptr)
-            self.ptr = ctypes.c_void_p()
+        self.ptr = ctypes.c_void_p()
 
     def __del__(self):
         try:
@@ -501,11 +523,12 @@ class BorderNodes:
         _check(lib().gcmx_border_nodes_create(ctx.ptr, axis, side, nodes.shape[0],
                                               nodes.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
                                               ctypes.byref(self.ptr)))
+        ctx._adopt(self)
 
     def close(self):
-        if self.ptr and self.ptr.value:
+        if self.ptr and self.ptr.value and self._ctx.ptr.value:
             lib().gcmx_border_nodes_destroy(self.ptr)
-            self.ptr = ctypes.c_void_p()
+        self.ptr = ctypes.c_void_p()
 
     def __del__(self):
         try:
@@ -547,6 +570,14 @@ def test_interpolate(v, g, c, q, lam, device: int = 0):
     out = np.zeros((n, 2), dtype=np.float64)
     _check(lib().gsx_test_interpolate(device, n, _dp(v), _dp(g), _dp(c), _dp(q), _dp(lam), _dp(out)))
     return out[:, 0].copy(), out[:, 1].copy()
+
+
+def channels_rule(global_x: int, nranks: int, local_x: int, Y: int, Z: int, bs: int = 2,
+                  rows_per_block: int = 0, cus: int = 256) -> int:
+    """gcmx_comm_channels_rule: the automatic RCCL channels per peer (pure; no GPU
+    call for cus > 0)."""
+    return lib().gcmx_comm_channels_rule(int(global_x), int(nranks), int(local_x), int(Y), int(Z),
+                                         int(bs), int(rows_per_block), int(cus))
 
 
 def unique_id() -> bytes:

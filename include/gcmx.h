@@ -276,15 +276,22 @@ typedef struct gcmx_comm_options {
 	double timeout_s;         /* bound of host waits on RCCL work; <= 0: the environment's
 	                             GCMX_COMM_TIMEOUT_SECONDS, default 60                       */
 } gcmx_comm_options;
-/* Automatic channels per peer: from inputs every rank holds alike (global_x,
- * nranks, Y, Z, borderSize, the one-pass step's block rule) -- the CUs the
- * interior launch of the thinnest slab of an even split, floor(global_x /
- * nranks) planes, leaves free: >= 16 -> 4 channels, >= 8 -> 2, else RCCL's
- * default; a one-rank communicator uses its own slab; without
- * global_x, RCCL's default.  The value reaches RCCL as NCCL_NCHANNELS_PER_PEER,
- * set in the process environment before the communicator is created unless the
- * user set it (RCCL reads it once per process: the first communicator decides).
- * opt == NULL: every field automatic / default (global_x unknown). */
+/* Channels per peer (checked contract).  Automatic (channels_per_peer = -1):
+ * gcmx_comm_channels_rule of inputs every rank holds alike.  RCCL reads
+ * NCCL_NCHANNELS_PER_PEER ONCE per process, so:
+ *   - before the process's first communicator the library sets it to the
+ *     count that communicator needs (nothing when that is 0, RCCL's default),
+ *     unless the user set it, in which case the user's value holds for every
+ *     communicator of the process and the rule is not applied;
+ *   - a later communicator that needs a different count fails with
+ *     GCMX_ERR_STATE (it would otherwise run silently with the first one's):
+ *     pass the process's count explicitly (gcmx_comm_channels_per_peer of the
+ *     first context), equal on every rank, or use a process of its own.
+ * opt == NULL: global_x unknown, timeout from the environment, and
+ * channels_per_peer / min_ctas / max_ctas from GCMX_COMM_CHANNELS_PER_PEER /
+ * GCMX_COMM_MIN_CTAS / GCMX_COMM_MAX_CTAS when set (tuning), else automatic /
+ * 16 / 32.  Without global_x the automatic rule of a multi-rank communicator
+ * is RCCL's default (0). */
 gcmx_status gcmx_comm_init_opts(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES],
                                 int nranks, int rank, int left, int right,
                                 const gcmx_comm_options* opt);
@@ -294,6 +301,21 @@ gcmx_status gcmx_comm_init(gcmx_ctx* ctx, const uint8_t id[GCMX_UNIQUE_ID_BYTES]
 /* The channels per peer in effect for this context's communicator (0: RCCL's
  * default), -1 without one. */
 int         gcmx_comm_channels_per_peer(const gcmx_ctx* ctx);
+/* The automatic channels-per-peer rule as a pure function (no GPU call when
+ * cus > 0): a one-rank communicator (nranks == 1) sizes it for its own slab of
+ * local_x planes; a multi-rank one for the THINNEST slab of an even split,
+ * floor(global_x / nranks) planes, whatever its own local_x (so ragged ranks
+ * derive the same count), and 0 (RCCL's default) when global_x == 0.  The count
+ * is from the CUs the one-pass step's interior launch of that slab (Y x Z
+ * rows, borderSize bs, rows_per_block, 0 = automatic) leaves free on a device
+ * of `cus` CUs (<= 0: the current device's): >= 16 -> 4, >= 8 -> 2, else 0
+ * (DESIGN.md §5).  -1 for invalid arguments. */
+int         gcmx_comm_channels_rule(int global_x, int nranks, int local_x, int Y, int Z, int bs,
+                                    int rows_per_block, int cus);
+/* ncclSend + ncclRecv calls this context's exchange groups posted so far (a
+ * group that posts fewer than 2 x halo components x neighbours fails with
+ * GCMX_ERR_COMM and aborts the communicator); -1 for a null context. */
+long long   gcmx_comm_posted_calls(const gcmx_ctx* ctx);
 /* Tests only: with on != 0 the context's exchange groups post their sends but
  * never their receives (a peer that never posts), so the exchange cannot
  * complete: the next bounded wait must return GCMX_ERR_COMM. */

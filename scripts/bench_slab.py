@@ -30,6 +30,7 @@ import numpy as np  # noqa: E402
 import gcm_amd  # noqa: E402
 from gcm_amd import gcmx  # noqa: E402
 from gcm_amd.host import isotropic_elastic_matrices  # noqa: E402
+from bench import rank_record  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--sched", default="bfirst", choices=["single", "xslab", "bfirst"])
@@ -49,9 +50,9 @@ ap.add_argument("--reps", type=int, default=5, help="timed repetitions of --step
 args = ap.parse_args()
 if args.rccl_self and len(args.ranks.split(",")) > 1:
     # RCCL reads NCCL_NCHANNELS_PER_PEER once per process: the first
-    # communicator's channel rule (gcmx_comm_init) would hold for every later
-    # slab thickness.  One process per rank count (profiles/r4/slab2/).
-    sys.exit("--rccl-self: give one --ranks value per process (RCCL caches the channel count per process)")
+    # communicator fixes the channel count, and the library refuses a later one
+    # that needs another (gcmx.h, checked contract).  One process per rank count.
+    sys.exit("--rccl-self: give one --ranks value per process (RCCL fixes the channel count per process)")
 U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
 N, STEPS = args.n, args.steps
 SCHED = {"xslab": gcmx.SCHED_XSLAB, "bfirst": gcmx.SCHED_BFIRST}.get(args.sched, gcmx.SCHED_SINGLE)
@@ -107,6 +108,9 @@ for ranks in [int(r) for r in args.ranks.split(",")]:
     c.sync()
     k = c.profile_read()
     c.profile(False)
+    # the exchange / compute split of this rank (bench.py rank_record): halo_ms,
+    # exposed_wait_ms, bytes and GB/s per direction, channels per peer
+    rec = rank_record(c, 0, k, STEPS, el / STEPS * 1e3) if (args.rccl_self or args.loop_gbps >= 0) else None
     c.close()
     ms = el / STEPS * 1e3
     rate = X * N * N * STEPS / el / 1e6
@@ -118,6 +122,7 @@ for ranks in [int(r) for r in args.ranks.split(",")]:
                       "Mnode_steps_per_gpu": round(rate, 1),
                       "projected_job_rate": round(rate * ranks, 1),
                       "kernels": kern,
+                      "per_rank": [rec] if rec else None,
                       "sched": args.sched, "rows": args.rows,
                       "boundary_rows": os.environ.get("GCMX_BOUNDARY_ROWS", "default"),
                       "exchange": "RCCL self-exchange (one-rank communicator)" if args.rccl_self else

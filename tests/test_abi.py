@@ -31,6 +31,33 @@ def test_library_exports_every_declared_symbol():
     assert sorted(SYMBOLS) == declared_symbols()
 
 
+def test_channels_rule_is_rank_consistent():
+    """the automatic RCCL channels-per-peer rule
+    (gcmx_comm_channels_rule, a pure function: no GPU call with an explicit CU
+    count) must give every rank of one grid the same count -- both ends of a
+    p2p connection use it -- however ragged the split: each rank calls it with
+    its OWN slab width, and the multi-rank form depends only on the shared
+    global X extent (the thinnest slab of an even split)."""
+    from gcm_amd import gcmx
+    splits = [([9, 6, 7], 40, 64), ([7, 5, 9, 3], 40, 64), ([5, 8, 3], 24, 64),
+              ([256, 256], 512, 512), ([128] * 4, 512, 512), ([64] * 8, 512, 512),
+              ([60, 68, 64, 64, 64, 64, 64, 64], 512, 512)]
+    for xs, Y, Z in splits:
+        gx, n = sum(xs), len(xs)
+        vals = {gcmx.channels_rule(gx, n, x, Y, Z) for x in xs}
+        assert len(vals) == 1, (xs, vals)
+        # = the one-rank rule on the thinnest slab of an even split
+        assert vals == {gcmx.channels_rule(0, 1, gx // n, Y, Z)}, (xs, vals)
+    # 512^3 on 256 CUs (DESIGN.md §5): 64-plane slabs leave 16 CUs beside the
+    # interior (4 channels), 128-plane slabs 8 (2), 256-plane slabs 4 (RCCL's default)
+    assert gcmx.channels_rule(512, 8, 64, 512, 512) == 4
+    assert gcmx.channels_rule(512, 4, 128, 512, 512) == 2
+    assert gcmx.channels_rule(512, 2, 256, 512, 512) == 0
+    # without the global extent a multi-rank rule cannot be rank-consistent: RCCL's default
+    assert gcmx.channels_rule(0, 3, 9, 40, 64) == 0
+    assert gcmx.channels_rule(512, 0, 64, 512, 512) == -1  # invalid
+
+
 def test_cpu_only_calls_fail_loudly():
     """No silent fallback: without a GPU, creating a context is an error."""
     import torch

@@ -337,16 +337,61 @@ def test_rccl_stalled_exchange_fails_instead_of_hanging(G):
     a.close()
 
 
-def test_rccl_channels_rule_is_rank_consistent(G):
-    """The automatic channels-per-peer rule uses only inputs every rank holds
-    alike: with global_x the thinnest slab of an even split decides, so ragged
-    ranks of one grid derive the same count (checked here on the rule's
-    one-rank form: a slab of global_x / nranks planes)."""
+def test_rccl_channels_fixed_per_process_is_checked(G):
+    """RCCL reads NCCL_NCHANNELS_PER_PEER once per process,
+    so the library fixes the count at the process's first communicator and
+    REFUSES (GCMX_ERR_STATE, before any RCCL call) a later communicator that
+    needs another count, instead of letting it run silently with the first
+    one's; asking for the fixed count explicitly works."""
     import gcm_amd
-    # one-rank communicator: its own slab (64 x 512 x 512 leaves 16 CUs: 4 channels)
     a = _whole(G, 8, 24, 64, 1)
     a.comm_init(gcm_amd.unique_id(), 1, 0, -1, -1)
-    assert a.comm_channels_per_peer >= 0
+    fixed = a.comm_channels_per_peer
+    assert fixed >= 0
+    b = _whole(G, 8, 24, 64, 1)
+    with pytest.raises(gcm_amd.GcmxError) as e:
+        b.comm_init(gcm_amd.unique_id(), 1, 0, -1, -1, channels_per_peer=fixed + 1)
+    assert e.value.status == 5 and "fixed" in str(e.value), str(e.value)  # GCMX_ERR_STATE
+    b.comm_init(gcm_amd.unique_id(), 1, 0, -1, -1, channels_per_peer=fixed)
+    assert b.comm_channels_per_peer == fixed
+    for c in (a, b):
+        c.close()
+
+
+def test_rccl_self_exchange_timings(G):
+    """the exchange is timed.  A one-rank self-exchange (the
+    real ncclSend / ncclRecv group every step) with profiling on: every post is
+    one `halo_rccl` bucket entry (comm stream, data-ready -> last kernel) whose
+    bytes are what one link direction carries, every wait of the compute stream
+    one `halo_wait` entry, and bench.py's rank_record turns them into the
+    per_rank fields of an N > 1 line.  Every group posted all its calls."""
+    import gcm_amd
+    import bench
+    X, Y, Z, steps = 16, 24, 64, 6
+    a = _whole(G, X, Y, Z, 0x5EED)
+    a.comm_init(gcm_amd.unique_id(), 1, 0, 0, 0)
+    a.step(0.9)
+    a.sync()
+    calls0 = a.comm_posted_calls
+    a.profile(True)
+    a.profile_reset()
+    for _ in range(steps):
+        a.step(0.9)
+    a.sync()
+    k = a.profile_read()
+    a.profile(False)
+    assert "halo_rccl" in k and "halo_wait" in k, sorted(k)
+    assert k["halo_rccl"]["launches"] == steps
+    comps = 6  # the X stage reads 6 of the 9 components at its neighbours
+    plane = (Y + 4) * (((2 + 14) + Z + 2 + 15) // 16 * 16)  # ghost-padded y rows x padded z row
+    assert k["halo_rccl"]["bytes_per_launch"] == 8.0 * 2 * plane * comps
+    rec = bench.rank_record(a, 0, k, steps, 1.0)
+    assert rec["halo_ms"] > 0 and rec["GBps_per_direction"] > 0
+    assert rec["halo_posts_per_step"] == 1.0 and rec["transport"] == "halo_rccl"
+    assert rec["exposed_wait_ms"] >= 0 and rec["interior_ms"] > 0 and rec["boundary_ms"] > 0
+    assert rec["channels_per_peer"] == a.comm_channels_per_peer
+    # every group: a send and a receive per halo component and neighbour (left = right = self)
+    assert a.comm_posted_calls - calls0 == steps * comps * 2 * 2
     a.close()
 
 

@@ -13,6 +13,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <ctime>
 
 #define CK(x)                                                                           \
 	do {                                                                                \
@@ -91,15 +92,18 @@ __global__ __launch_bounds__(512 / VEC * PL) void k_probe(const double* __restri
 // Each thread: TX adjacent planes at one z; 6 components at TX+4 planes, 3 at the TX nodes.
 // BAR: the fused kernel's Z exchange per row -- two barriers around 12 LDS row
 // writes (6 components x 2 nodes), then 4 neighbour reads per component.
-template <int TX, bool STORE, int KOPS = 0, bool BAR = false>
-__global__ __launch_bounds__(512, 2) void k_probe_tx(const double* __restrict__ in,
+// ZT < 512: a block covers z [zp*ZT, zp*ZT + ZT) of the row (one wave per SIMD
+// at one block per CU: the VGPR budget of a 512-register lane).
+template <int TX, bool STORE, int KOPS = 0, bool BAR = false, int ZT = 512>
+__global__ __launch_bounds__(ZT, ZT == 512 ? 2 : 1) void k_probe_tx(const double* __restrict__ in,
                                                      double* __restrict__ out, int chunk) {
 	extern __shared__ double dyn_lds[];
 	__shared__ double zl[BAR ? TX : 1][6][BAR ? 516 : 1];
-	const int z = threadIdx.x;
-	if (z == 1023) dyn_lds[0] = 0.0;  // never true: keeps the dynamic LDS request
+	constexpr int NZ = 512 / ZT;
+	if (threadIdx.x == 1023) dyn_lds[0] = 0.0;  // never true: keeps the dynamic LDS request
 	const int T_ = gridDim.x, b = blockIdx.x;
-	const int p = (T_ % 8 == 0) ? (b % 8) * (T_ / 8) + b / 8 : b;
+	const int p0 = (T_ % 8 == 0) ? (b % 8) * (T_ / 8) + b / 8 : b;
+	const int z = threadIdx.x + (p0 % NZ) * ZT, p = p0 / NZ;
 	const int np = N / TX;
 	const int x = (p % np) * TX, yb = (p / np) * chunk;
 	const unsigned base = (unsigned)(ORIGIN + x * STX + z);
@@ -230,6 +234,117 @@ __global__ __launch_bounds__(64 * (TY + 2 * BS)) void k_probe_xm(const double* _
 	}
 }
 
+
+// Generalised two/four-plane pattern (VERDICT r4 item 1 follow-up): ZT threads
+// per block, each lane holding ZR groups of VEC adjacent z columns (VEC = 2:
+// 16-byte loads) at TX adjacent x planes; a block covers ZT * ZR * VEC columns
+// of a row.  One block per CU when launched with 96 KB of dynamic LDS.
+template <int TX, int KOPS, int ZT, int ZR, int VEC>
+__global__ __launch_bounds__(ZT, ZT == 512 ? 2 : 1) void k_probe_tz(const double* __restrict__ in,
+                                                                   double* __restrict__ out, int chunk) {
+	typedef typename V<VEC>::T T;
+	extern __shared__ double dyn_lds[];
+	constexpr int ZB = ZT * ZR * VEC, NZ = 512 / ZB;
+	if (threadIdx.x == 1023) dyn_lds[0] = 0.0;
+	const int T_ = gridDim.x, b = blockIdx.x;
+	const int p0 = (T_ % 8 == 0) ? (b % 8) * (T_ / 8) + b / 8 : b;
+	const int zb = (p0 % NZ) * ZB, p = p0 / NZ;
+	const int np = N / TX;
+	const int x = (p % np) * TX, yb = (p / np) * chunk;
+	auto ld = [&](int c, long long o) { return *reinterpret_cast<const T*>(in + c * CS + o); };
+	for (int y = yb; y < yb + chunk; y++) {
+#pragma unroll
+		for (int r = 0; r < ZR; r++) {
+			const int z = zb + r * ZT * VEC + (int)threadIdx.x * VEC;
+			const long long o = ORIGIN + x * STX + (long long)y * STY + z;
+			T v[TX][9];
+#pragma unroll
+			for (int c = 0; c < 9; c++) {
+				if (c < 6) {
+					T w[TX + 4];
+#pragma unroll
+					for (int k = 0; k < TX + 4; k++) w[k] = ld(c, o + (long long)(k - BS) * STX);
+#pragma unroll
+					for (int t = 0; t < TX; t++) v[t][c] = w[t] + w[t + 1] + w[t + 2] + w[t + 3] + w[t + 4];
+				} else {
+#pragma unroll
+					for (int t = 0; t < TX; t++) v[t][c] = ld(c, o + (long long)t * STX);
+				}
+			}
+			if constexpr (KOPS > 0) {
+#pragma unroll
+				for (int t = 0; t < TX; t++)
+#pragma unroll 1
+					for (int k = 0; k < KOPS / 18; k++)
+#pragma unroll
+						for (int c = 0; c < 9; c++) v[t][c] = v[t][c] * 0.999 + 0.001;
+			}
+#pragma unroll
+			for (int t = 0; t < TX; t++)
+#pragma unroll
+				for (int c = 0; c < 9; c++)
+					__builtin_nontemporal_store(v[t][c], reinterpret_cast<T*>(out + c * CS + o + (long long)t * STX));
+		}
+	}
+}
+
+template <int TX, int KOPS, int ZT, int ZR, int VEC>
+void tz(const double* in, double* out, int chunk, size_t shm) {
+	const double nodes = (double)N * N * N;
+	constexpr int ZB = ZT * ZR * VEC;
+	dim3 grid((N / chunk) * (N / TX) * (512 / ZB));
+	hipEvent_t a, b;
+	CK(hipEventCreate(&a));
+	CK(hipEventCreate(&b));
+	// PROBE_REPS (default 10) timed launches; the CLOCK_MONOTONIC span of the
+	// timed launches is printed so that a power sampler (tools/power_probe.py)
+	// can attribute its samples to the variant
+	static const int reps = std::getenv("PROBE_REPS") ? std::atoi(std::getenv("PROBE_REPS")) : 10;
+	hipLaunchKernelGGL((k_probe_tz<TX, KOPS, ZT, ZR, VEC>), grid, dim3(ZT), shm, 0, in, out, chunk);
+	CK(hipDeviceSynchronize());
+	timespec t0, t1;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	CK(hipEventRecord(a));
+	for (int r = 0; r < reps; r++)
+		hipLaunchKernelGGL((k_probe_tz<TX, KOPS, ZT, ZR, VEC>), grid, dim3(ZT), shm, 0, in, out, chunk);
+	CK(hipEventRecord(b));
+	CK(hipEventSynchronize(b));
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	float ms = 0;
+	CK(hipEventElapsedTime(&ms, a, b));
+	ms /= reps;
+	std::printf("TZ: %d planes x %d z-groups x %d adjacent z per lane, %d threads/block%s, chunk %3d, + %d fp64 ops/node: "
+	            "%.3f ms (%.0f GB/s) [mono %.6f %.6f]\n",
+	            TX, ZR, VEC, ZT, shm ? " (1 block/CU)" : "", chunk, KOPS, ms, 144.0 * nodes / (ms * 1e6),
+	            t0.tv_sec + 1e-9 * t0.tv_nsec, t1.tv_sec + 1e-9 * t1.tv_nsec);
+	std::fflush(stdout);
+}
+
+// the flat 16-B copy of the layout (k_probe MODE 0, VEC 2) with its monotonic span
+void copy_span(const double* in, double* out) {
+	const double nodes = (double)N * N * N;
+	static const int reps = std::getenv("PROBE_REPS") ? std::atoi(std::getenv("PROBE_REPS")) : 10;
+	dim3 grid((N / 128) * N), block(256);
+	hipEvent_t a, b;
+	CK(hipEventCreate(&a));
+	CK(hipEventCreate(&b));
+	hipLaunchKernelGGL((k_probe<0, 2, 1>), grid, block, 0, 0, in, out, 128);
+	CK(hipDeviceSynchronize());
+	timespec t0, t1;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	CK(hipEventRecord(a));
+	for (int r = 0; r < reps; r++) hipLaunchKernelGGL((k_probe<0, 2, 1>), grid, block, 0, 0, in, out, 128);
+	CK(hipEventRecord(b));
+	CK(hipEventSynchronize(b));
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	float ms = 0;
+	CK(hipEventElapsedTime(&ms, a, b));
+	ms /= reps;
+	std::printf("copy (16-B lanes, layout planes): %.3f ms (%.0f GB/s) [mono %.6f %.6f]\n", ms,
+	            144.0 * nodes / (ms * 1e6), t0.tv_sec + 1e-9 * t0.tv_nsec, t1.tv_sec + 1e-9 * t1.tv_nsec);
+	std::fflush(stdout);
+}
+
 template <int TY, int XC>
 void xmarch(const double* in, double* out) {
 	const double nodes = (double)N * N * N;
@@ -253,24 +368,25 @@ void xmarch(const double* in, double* out) {
 	            loads, ms, 144.0 * nodes / (ms * 1e6));
 }
 
-template <int TX, int KOPS, bool BAR = false>
+template <int TX, int KOPS, bool BAR = false, int ZT = 512>
 void ops_tx(const double* in, double* out, int chunk, size_t shm = 0) {
 	const double nodes = (double)N * N * N;
-	dim3 grid((N / chunk) * (N / TX));
+	dim3 grid((N / chunk) * (N / TX) * (512 / ZT));
 	hipEvent_t a, b;
 	CK(hipEventCreate(&a));
 	CK(hipEventCreate(&b));
 	for (int r = 0; r < 11; r++) {
 		if (r == 1) CK(hipEventRecord(a));
-		hipLaunchKernelGGL((k_probe_tx<TX, true, KOPS, BAR>), grid, dim3(512), shm, 0, in, out, chunk);
+		hipLaunchKernelGGL((k_probe_tx<TX, true, KOPS, BAR, ZT>), grid, dim3(ZT), shm, 0, in, out, chunk);
 	}
 	CK(hipEventRecord(b));
 	CK(hipEventSynchronize(b));
 	float ms = 0;
 	CK(hipEventElapsedTime(&ms, a, b));
 	ms /= 10;
-	std::printf("TX %d planes/thread chunk %3d + %d fp64 ops/node%s%s: %.3f ms (%.0f GB/s)\n", TX, chunk, KOPS,
-	            BAR ? " + Z exchange (2 barriers/row)" : "", shm ? " (1 block/CU)" : "", ms,
+	std::printf("TX %d planes/thread chunk %3d + %d fp64 ops/node%s%s%s: %.3f ms (%.0f GB/s)\n", TX, chunk, KOPS,
+	            BAR ? " + Z exchange (2 barriers/row)" : "", shm ? " (1 block/CU)" : "",
+	            ZT == 512 ? "" : ZT == 256 ? " (256-thread blocks: 1 wave/SIMD)" : " (ZT?)", ms,
 	            144.0 * nodes / (ms * 1e6));
 }
 
@@ -335,6 +451,41 @@ int main() {
 	CK(hipMalloc(&out, bytes));
 	CK(hipMemset(in, 0, bytes));
 	CK(hipMemset(out, 0, bytes));
+	if (std::getenv("TZ_ONLY")) {  // two planes x two z groups per lane at one wave per SIMD
+		copy_span(in, out);
+		tz<2, 0, 512, 1, 1>(in, out, 128, 96 * 1024);   // = the shipped pattern, 1 block/CU
+		tz<4, 0, 256, 1, 1>(in, out, 128, 96 * 1024);   // = TX4 half rows, 1 wave/SIMD
+		tz<2, 0, 256, 2, 1>(in, out, 128, 96 * 1024);   // z and z+256 per lane, whole row, 1 wave/SIMD
+		tz<2, 0, 256, 1, 2>(in, out, 128, 96 * 1024);   // z, z+1 (16-B loads), whole row, 1 wave/SIMD
+		tz<2, 0, 256, 2, 1>(in, out, 512, 96 * 1024);
+		tz<2, 0, 256, 1, 2>(in, out, 512, 96 * 1024);
+		tz<2, 0, 512, 1, 1>(in, out, 512, 0);
+		ops_tx<2, 540>(in, out, 128);
+		tz<2, 540, 256, 2, 1>(in, out, 128, 96 * 1024);
+		tz<2, 540, 256, 1, 2>(in, out, 128, 96 * 1024);
+		tz<4, 540, 256, 1, 1>(in, out, 128, 96 * 1024);
+		tz<2, 900, 512, 1, 1>(in, out, 512, 0);
+		tz<2, 900, 256, 2, 1>(in, out, 512, 96 * 1024);
+		tz<2, 900, 256, 1, 2>(in, out, 512, 96 * 1024);
+		tz<4, 900, 256, 1, 1>(in, out, 512, 96 * 1024);
+		return 0;
+	}
+	if (std::getenv("TX4_ONLY")) {  // four planes per thread at one wave per SIMD
+		family<1, 1>(in, out, 128);
+		family<2, 1>(in, out, 128);
+		ops_tx<2, 0>(in, out, 128);
+		ops_tx<2, 0>(in, out, 128, 96 * 1024);
+		ops_tx<4, 0>(in, out, 128);
+		ops_tx<4, 0>(in, out, 128, 96 * 1024);
+		ops_tx<4, 0, false, 256>(in, out, 128, 96 * 1024);
+		ops_tx<2, 0, false, 256>(in, out, 128, 96 * 1024);
+		ops_tx<2, 540>(in, out, 128);
+		ops_tx<4, 540>(in, out, 128, 96 * 1024);
+		ops_tx<4, 540, false, 256>(in, out, 128, 96 * 1024);
+		ops_tx<2, 0>(in, out, 512);
+		ops_tx<4, 0, false, 256>(in, out, 512, 96 * 1024);
+		return 0;
+	}
 	if (std::getenv("XM_ONLY")) {  // the x-marching family beside the copy and the 2-plane pattern
 		family<1, 1>(in, out, 128);
 		family_tx<2>(in, out, 128);
