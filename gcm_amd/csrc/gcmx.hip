@@ -316,6 +316,8 @@ gcmx_status build_tables(gcmx_ctx* c, double tau) {
 			}
 			A.kf1 = t.kf[0];
 			A.kf2 = t.kf[2];
+			lagrange_weights(A.c1, A.kf1 == 0 ? bs : 0, A.w1);
+			lagrange_weights(A.c2, A.kf2 == 0 ? bs : 0, A.w2);
 		}
 	}
 	HIP_TRY(hipMemcpyAsync(c->tabs_d, h.data(), h.size() * sizeof(AxisTable),
@@ -341,6 +343,8 @@ gcmx_status build_tables(gcmx_ctx* c, double tau) {
 				}
 				A[s].kf1 = t.kf[0];
 				A[s].kf2 = t.kf[2];
+				lagrange_weights(A[s].c1, A[s].kf1 == 0 ? bs : 0, A[s].w1);
+				lagrange_weights(A[s].c2, A[s].kf2 == 0 ? bs : 0, A[s].w2);
 				ok = ok && A[s].kf1 == 0 && A[s].kf2 == 0;
 			}
 			ok = ok && std::memcmp(&A[0], &A[1], sizeof(IsoAxis)) == 0 && std::memcmp(&A[0], &A[2], sizeof(IsoAxis)) == 0;

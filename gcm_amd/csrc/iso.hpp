@@ -134,18 +134,42 @@ __host__ __device__ constexpr int pair_sig(int S, int P) {
 	return P == 0 ? sig3(S, S) : P == 1 ? sig3(tang1(S), S) : sig3(tang2(S), S);
 }
 
+// GCMX_LAGRANGE (the one-pass step's FMA build, kernels_xyz.hip compiled with
+// GCMX_FMA=1): with floor(q) = 0 and bs <= 2 a foot's interpolant is evaluated
+// in Lagrange form, w0 s0 + w1 s1 + w2 s2 with the host's weights
+// (lagrange_weights), as one multiply and bs fused multiply-adds: the same
+// polynomial as minMaxInterpolate's Newton form (EqualDistanceLineInterpolator.hpp:56-71)
+// with other roundings, ~1e-16 relative, inside the north star's 1e-10 of the
+// reference; the min-max limiter is unchanged.  The exact build
+// keeps the reference's Newton operations.
+#ifndef GCMX_FMA
+#define GCMX_FMA 0
+#endif
+#ifndef GCMX_LAGRANGE
+#define GCMX_LAGRANGE GCMX_FMA
+#endif
+template <int BS>
+__device__ __forceinline__ double lagrange_minmax(const double (&s)[BS + 1], const double* __restrict__ w) {
+	double ans = s[0] * w[0];
+#pragma unroll
+	for (int i = 1; i <= BS; i++) ans = __builtin_fma(w[i], s[i], ans);
+	return vlimit(ans, s[0], s[1]);
+}
+
 // Rows 2P (foot on the -S side, L > 0) and 2P+1 (+S side) of r = diag(U * V):
 // the two interpolations per component (minMaxInterpolate) and the U row sums.
 // W(j, o): component j at offset o along S (|o| <= BS).
 template <int S, int BS, bool KF0, int P, class WF>
 __device__ __forceinline__ void pair_update(const IsoAxis& A, WF W, double& ra, double& rb) {
 	const double* coef = (P == 0) ? A.c1 : A.c2;
+	const double* wts = (P == 0) ? A.w1 : A.w2;
 	const int kf = (P == 0) ? A.kf1 : A.kf2;
 	auto interp = [&](int j, int sh) {
 		double sv[BS + 1];
 #pragma unroll
 		for (int i = 0; i <= BS; i++) sv[i] = W(j, sh * i);
-		return newton_minmax<BS, KF0>(sv, kf, coef);
+		if constexpr (GCMX_LAGRANGE && KF0 && BS <= 2) return lagrange_minmax<BS>(sv, wts);
+		else return newton_minmax<BS, KF0>(sv, kf, coef);
 	};
 	ra = RowSum<S, false, 2 * P>::go(A, [&](int j) { return interp(j, -1); }, 0.0, true);
 	rb = RowSum<S, false, 2 * P + 1>::go(A, [&](int j) { return interp(j, 1); }, 0.0, true);

@@ -310,19 +310,18 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #endif
 
 
-// Runs f(k) once for every distinct key among the active lanes, with k uniform
-// (an SGPR value: per-material tables indexed by it are scalar loads), every lane
-// inside the call whose key is k.  One pass when the wave's key is uniform.
-template <class F>
-__device__ __forceinline__ void waterfall(unsigned key, F f) {
-	for (;;) {
-		const unsigned k = __builtin_amdgcn_readfirstlane(key);
-		if (key == k) {
-			f(k);
-			break;
-		}
-	}
-}
+// Per-node materials: every lane applies ITS OWN material's table, read from
+// the LDS copy with a per-lane address.  (Rounds 3-4 wrapped this in a
+// readfirstlane "waterfall" loop, `for (;;) { k = readfirstlane(key); if (key
+// == k) { f(k); break; } }`, meant to keep k wave-uniform.  Inside `key == k`
+// the compiler replaces k by the lane's own key, after which the loop carries
+// nothing uniform and is deleted: every lane runs f once with its own key, all
+// lanes active.  With tables read per lane that is still correct (and is what
+// the shipped round-4 ISA does: ds_read at a per-lane address, no loop); the
+// mid-round-4 variant that also passed the table fields through readfirstlane
+// (cb6938f) then broadcast the FIRST lane's table to the whole wave -- wrong
+// for every lane of another material (relative L2 0.687 on random material
+// ids, green on layered ids where a wave holds one material).  DESIGN.md §3.1.)
 
 // Component held in window slot q of a stage whose window mask is `mask`.
 __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
@@ -382,9 +381,9 @@ __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 // Every node's stages use its own material's tables mtab[mat[node]] (per material
 // the three axes' tables are identical and floor(q) = 0, checked on the host), as
 // GridCharacteristicMethod::stage takes each node's own matrices.  The tables are
-// applied through `waterfall` over the materials present in a wave, so they stay
-// scalar operands; where the two nodes of a lane differ in material, their X
-// stages run without the shared differences (pair_update per node).
+// read per lane from their LDS copy; where the two nodes of a lane differ in
+// material, their X stages run without the shared differences (pair_update per
+// node).
 template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET>
 __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
     const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY_,
@@ -501,9 +500,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	auto ldc = [&](int j, int k, int r) { return ldx(j, k, r); };
 	auto stz = [&](int c, int t, int y, double v) { out_p.st_nt(c, plane + (unsigned)y * sty + zo + (unsigned)t * stx, v); };
 #endif
-	// per-material table k (k wave-uniform: waterfall), from the LDS copy made at
-	// kernel start
-	// per-material table k (k wave-uniform: waterfall), from the LDS copy made at
+	// per-material table k (the lane's own material), from the LDS copy made at
 	// kernel start.  Measured alternatives: scalar loads through
 	// the constant address space spill VGPRs; separate one-table / two-table X
 	// paths double the X stage's code; both are slower.
@@ -588,7 +585,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				pair_update<0, BS, true, P>(
 				    t ? A1 : A0, [&](int j, int o) { return j == pair_vel(0, P) ? w[0][t + BS + o] : w[1][t + BS + o]; },
 				    rr[t][2 * P], rr[t][2 * P + 1]);
-		} else if constexpr (KF0) {
+		} else if constexpr (KF0 && !GCMX_LAGRANGE) {
 			const IsoAxis& AS = A0;  // one table for both nodes
 			const double* c = (P == 0) ? AS.c1 : AS.c2;
 			double im[2][2], ip[2][2];  // [vel/sig][node]
@@ -697,10 +694,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		cv_load(cv, r);
 		sched_fence();
 		if constexpr (HET) {
-			waterfall(key, [&](unsigned k) {
-				const unsigned m0 = k & 255u, m1 = k >> 8;
-				x_compute(pre, wc, cv, xr, mt(m0), mt(m1), m0 == m1);
-			});
+			const unsigned m0 = key & 255u, m1 = key >> 8;
+			x_compute(pre, wc, cv, xr, mt(m0), mt(m1), m0 == m1);
 		} else {
 			x_compute(pre, wc, cv, xr, AX, AX, true);
 		}
@@ -815,7 +810,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				    [&](int j) { return ((WMY >> j) & 1u) ? win[t][wslot(WMY, j)][BS] : cp[(t * NCY + wslot(CMY, j)) * ZT]; },
 				    yv[t]);
 			};
-			if constexpr (HET) waterfall(t ? hk[BS] >> 8 : hk[BS] & 255u, [&](unsigned k) { go(mt(k)); });
+			if constexpr (HET) go(mt(t ? hk[BS] >> 8 : hk[BS] & 255u));
 			else go(AY);
 		}
 	};
@@ -929,7 +924,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				    A, [&](int j, int o) { return zl[t][wslot(WMZ, j)][BS + z + o]; },
 				    [&](int j) { return ((WMZ >> j) & 1u) ? zl[t][wslot(WMZ, j)][BS + z] : yv[t][j]; }, zv);
 		};
-		if constexpr (HET) waterfall(t ? hk[BS] >> 8 : hk[BS] & 255u, [&](unsigned k) { go(mt(k)); });
+		if constexpr (HET) go(mt(t ? hk[BS] >> 8 : hk[BS] & 255u));
 		else go(AZ);
 		if (fb.ode_on) {  // MaxwellViscosityOde: sigma *= exp(-tau / tau0), the stored product (Ode.hpp:34-35)
 			double f = fb.ode;
@@ -1022,7 +1017,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 // ------------------------------------------------------------- launchers --
 
 static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
-	static_assert(sizeof(IsoAxis) == 12 * 8 + 2 * 4, "IsoAxis has padding");
+	static_assert(sizeof(IsoAxis) == 18 * 8 + 2 * 4, "IsoAxis has padding");
 	return std::memcmp(&p, &q, sizeof(IsoAxis)) == 0;
 }
 

@@ -53,8 +53,24 @@ struct IsoAxis {
 	double a, b, g;      // U:  sigma_ss of rows 0/1, sigma_ts of rows 2..5, sigma_ss of row 8
 	double p1, p2, s;    // U1: sigma_ss / sigma_tt of columns 0/1, sigma_st of columns 2..5
 	double c1[3], c2[3]; // ((q - i) + 1) / i, i = 1..bs
+	double w1[3], w2[3]; // the same interpolant's Lagrange weights (floor(q) = 0, bs <= 2; else 0):
+	                     // sum_i w[i] s_i == Newton's s0 + c0 D1 + c0 c1 D2 (lagrange_weights)
 	int kf1, kf2;        // floor(q)
 };
+// Lagrange weights w[0..bs] of the Newton interpolant with coefficients c
+// (EqualDistanceLineInterpolator.hpp:56-71: ans = s0 + c0 (s1 - s0) + c0 c1 (s2 - 2 s1 + s0))
+inline void lagrange_weights(const double* c, int bs, double* w) {
+	w[0] = w[1] = w[2] = 0.0;
+	if (bs == 1) {
+		w[0] = 1.0 - c[0];
+		w[1] = c[0];
+	} else if (bs == 2) {
+		const double c01 = c[0] * c[1];
+		w[0] = (1.0 - c[0]) + c01;
+		w[1] = c[0] - 2.0 * c01;
+		w[2] = c01;
+	}
+}
 bool iso_axis_extract(int s, const double* U, const double* U1, const double* L, IsoAxis& A);
 bool fast_layout_ok(const Geo& g);
 bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const IsoAxis& A,

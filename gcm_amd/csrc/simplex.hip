@@ -44,6 +44,14 @@ gcmx_status fail(gcmx_status s, const std::string& msg) {
 			return fail(GCMX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
 	} while (0)
 
+// Every kernel launch on a context's stream, counted (gsx_launch_count: the
+// dependent launches of a step, for its launch-floor model).
+#define SX_LAUNCH(ctx, ...)                \
+	do {                                   \
+		++(ctx)->launches;                 \
+		hipLaunchKernelGGL(__VA_ARGS__);   \
+	} while (0)
+
 struct BorderArgs {  // static per-condition data passed by value with every launch
 	int type[GSX_MAX_BORDER_CONDITIONS];
 	double minDet[GSX_MAX_BORDER_CONDITIONS][3];
@@ -124,6 +132,7 @@ struct gsx_ctx {
 	int epoch = 0;
 	unsigned gTarget = 0;
 	unsigned tickets = 0;  // work tickets k_sx_stage_l8 launches have handed out (device counter ready[N + 2])
+	long long launches = 0;  // kernel launches on this context's stream (gsx_launch_count)
 	int fuseMode = 1;  // gsx_set_stage_fusion: 0 never, 1 border + inner, 2 gradient + border + inner,
 	                   // 3 border + inner without the grid-size cap (tuning)
 	bool lastFused = false;  // the last gsx_stage ran as one launch
@@ -1504,7 +1513,7 @@ gcmx_status prep_border(gsx_ctx* c) {
 	BorderDev& bd = c->bd;
 	if (!c->matsSet || !bd.set || bd.n == 0) return GCMX_OK;
 	if (!bd.md) SX_TRY(hipMalloc(&bd.md, (size_t)bd.n * 60 * sizeof(double)));
-	hipLaunchKernelGGL(k_sx_border_prep, dim3(((size_t)bd.n * 6 + 255) / 256), dim3(256), 0, c->stream,
+	SX_LAUNCH(c, k_sx_border_prep, dim3(((size_t)bd.n * 6 + 255) / 256), dim3(256), 0, c->stream,
 	                   bd.B, c->mats, bd.n, bd.md);
 	SX_TRY(hipGetLastError());
 	for (int s = 0; s < 3; s++) {
@@ -1515,7 +1524,7 @@ gcmx_status prep_border(gsx_ctx* c) {
 			SX_TRY(hipMalloc(&st.recB, (size_t)st.nBorder * 27 * sizeof(double)));
 			SX_TRY(hipMalloc(&st.recMd, (size_t)st.nBorder * 20 * sizeof(double)));
 		}
-		hipLaunchKernelGGL(k_sx_border_rec, dim3((st.nBorder + 255) / 256), dim3(256), 0, c->stream,
+		SX_LAUNCH(c, k_sx_border_rec, dim3((st.nBorder + 255) / 256), dim3(256), 0, c->stream,
 		                   st.border, st.nBorder, c->corrOf, bd.cond, bd.outer, bd.n, bd.B, bd.md, s,
 		                   bd.argsDev, st.rec, st.recB, st.recMd);
 		SX_TRY(hipGetLastError());
@@ -1902,7 +1911,7 @@ gcmx_status gsx_set_border_values(gsx_ctx* c, const double* b) {
 		BorderValues v{};
 		for (int i = 0; i < 3 * c->bd.nCond; i++) v.b[i] = b[i];
 		if (!c->bd.valuesSet || std::memcmp(v.b, c->bd.lastValues, sizeof(v.b)) != 0) {
-			hipLaunchKernelGGL(k_sx_set_border_values, dim3(1), dim3(64), 0, c->stream, c->bvals, v,
+			SX_LAUNCH(c, k_sx_set_border_values, dim3(1), dim3(64), 0, c->stream, c->bvals, v,
 			                   3 * c->bd.nCond);
 			SX_TRY(hipGetLastError());
 			std::memcpy(c->bd.lastValues, v.b, sizeof(v.b));
@@ -1918,11 +1927,11 @@ gcmx_status gsx_plain_correction(gsx_ctx* c) {
 	const BorderDev& bd = c->bd;
 	if (!bd.set || !bd.valuesSet) return fail(GCMX_ERR_STATE, "border plan / values not set");
 	if (c->matsSet) {  // fused with the first stage's beforeStage (the next call is stage 0)
-		hipLaunchKernelGGL(k_sx_begin, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->u, c->w,
+		SX_LAUNCH(c, k_sx_begin, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->u, c->w,
 		                   c->mats, bd.n ? bd.nodeRec : nullptr, bd.S, c->N, bd.argsDev);
 		c->wStage = 0;
 	} else if (bd.n) {
-		hipLaunchKernelGGL(k_sx_plain, dim3((bd.n + 63) / 64), dim3(64), 0, c->stream, bd.nodes,
+		SX_LAUNCH(c, k_sx_plain, dim3((bd.n + 63) / 64), dim3(64), 0, c->stream, bd.nodes,
 		                   bd.cond, bd.S, c->u, bd.n, c->N, bd.argsDev);
 		c->wStage = -1;
 	}
@@ -1964,7 +1973,7 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 	// beforeStage: the invariants come from the previous stage's final writers when
 	// chained, otherwise from a transform pass
 	if (c->wStage != stage)
-		hipLaunchKernelGGL(k_sx_transform<true>, grd, blk, 0, c->stream, c->u, c->w,
+		SX_LAUNCH(c, k_sx_transform<true>, grd, blk, 0, c->stream, c->u, c->w,
 		                   c->mats + stage * 81, N);
 	c->wStage = -1;
 	// one-launch stage (k_sx_stage_l8: gradient, border and inner groups side by side)
@@ -1997,11 +2006,11 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 		                   c->ready + N + 1, c->waitBudget,
 		                   reinterpret_cast<unsigned*>(c->ready + N + 2), c->tickets};
 		if (!withGrad)
-			hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
+			SX_LAUNCH(c, k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
 			                   c->stream, c->w, c->grad, c->gOff, c->gNb, c->coords, c->gW, c->gM, c->gDet, N);
 		const int nbBlk = (int)(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block);
 		const int niBlk = (int)(((size_t)st.nInner * kL + kL8Block - 1) / kL8Block);
-		hipLaunchKernelGGL(k_sx_stage_l8, dim3(ngBlk + nbBlk + niBlk), dim3(kL8Block), 0, c->stream, st.border,
+		SX_LAUNCH(c, k_sx_stage_l8, dim3(ngBlk + nbBlk + niBlk), dim3(kL8Block), 0, c->stream, st.border,
 		                   st.nBorder, st.inner, st.nInner, nbBlk, st.fv, st.flam, st.fmeta, st.shift, c->coords,
 		                   c->w, c->grad, c->wn, c->deferred, bp, bd.argsDev, c->mats + stage * 81,
 		                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, sw, ngBlk,
@@ -2014,11 +2023,11 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 		return GCMX_OK;
 	}
 	if (l8)
-		hipLaunchKernelGGL(k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
+		SX_LAUNCH(c, k_sx_gradient_l8, dim3(((size_t)N * kL + kL8Block - 1) / kL8Block), dim3(kL8Block), 0,
 		                   c->stream, c->w,
 		                   c->grad, c->gOff, c->gNb, c->coords, c->gW, c->gM, c->gDet, N);
 	else
-		hipLaunchKernelGGL(k_sx_gradient, grd, blk, 0, c->stream, c->w, c->grad, c->gOff, c->gNb,
+		SX_LAUNCH(c, k_sx_gradient, grd, blk, 0, c->stream, c->w, c->grad, c->gOff, c->gNb,
 		                   c->coords, c->gW, c->gM, c->gDet, N);
 	if (st.nBorder) {
 		const BorderDevArgs bp = {c->corrOf, (bd.set && bd.n) ? bd.cond : nullptr, bd.B, bd.S,
@@ -2029,13 +2038,13 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 #endif
 #ifdef GCMX_SX_DIAG_ASINNER  // tuning builds only: time the inner kernel over the border list
 			if (true)
-				hipLaunchKernelGGL(k_sx_inner_l8, dim3(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block),
+				SX_LAUNCH(c, k_sx_inner_l8, dim3(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block),
 			                   dim3(kL8Block), 0, c->stream, st.border, st.nBorder, st.fv, st.flam, st.fmeta,
 			                   st.shift, c->coords, c->w, c->grad, c->wn, c->mats + 3 * 81 + stage * 81,
 			                   nextU(c, stage), c->un, c->wnext, N, 0, st.nBorder + st.nInner);
 			else
 #endif
-			hipLaunchKernelGGL(k_sx_border_l8, dim3(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block),
+			SX_LAUNCH(c, k_sx_border_l8, dim3(((size_t)st.nBorder * kL + kL8Block - 1) / kL8Block),
 			                   dim3(kL8Block), 0, c->stream,
 			                   st.border, st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w,
 			                   c->grad, c->wn, c->deferred, bp, bd.argsDev, c->mats + stage * 81,
@@ -2043,7 +2052,7 @@ gcmx_status stage_nodes(gsx_ctx* c, int stage, bool fuse, bool* fused) {
 			                   st.nBorder + st.nInner);
 		}
 		else  // border lists are short (a surface): 64-thread blocks spread them over the CUs
-			hipLaunchKernelGGL(k_sx_border, dim3((st.nBorder + 63) / 64), dim3(64), 0, c->stream, st.border,
+			SX_LAUNCH(c, k_sx_border, dim3((st.nBorder + 63) / 64), dim3(64), 0, c->stream, st.border,
 			                   st.nBorder, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
 			                   c->wn, c->deferred, bp, bd.argsDev, c->mats + stage * 81,
 			                   c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, stage, N, 0,
@@ -2064,13 +2073,13 @@ gcmx_status stage_finish(gsx_ctx* c, int stage, bool inner_done) {
 	const StageDev& st = c->st[stage];
 	if (inner_done) {
 	} else if (st.nInner && node_lanes(c) == kL)
-		hipLaunchKernelGGL(k_sx_inner_l8, dim3(((size_t)st.nInner * kL + kL8Block - 1) / kL8Block),
+		SX_LAUNCH(c, k_sx_inner_l8, dim3(((size_t)st.nInner * kL + kL8Block - 1) / kL8Block),
 		                   dim3(kL8Block), 0, c->stream,
 		                   st.inner, st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
 		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N,
 		                   st.nBorder, st.nBorder + st.nInner);
 	else if (st.nInner)
-		hipLaunchKernelGGL(k_sx_inner, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
+		SX_LAUNCH(c, k_sx_inner, dim3((st.nInner + 255) / 256), blk, 0, c->stream, st.inner,
 		                   st.nInner, st.fv, st.flam, st.fmeta, st.shift, c->coords, c->w, c->grad,
 		                   c->wn, c->mats + 3 * 81 + stage * 81, nextU(c, stage), c->un, c->wnext, N,
 		                   st.nBorder, st.nBorder + st.nInner);
@@ -2099,6 +2108,12 @@ gcmx_status gsx_set_stage_fusion(gsx_ctx* c, int on) {
 	if (s) return s;
 	if (on < 0 || on > 3) return fail(GCMX_ERR_INVALID_ARG, "stage fusion must be 0..3");
 	c->fuseMode = on;
+	return GCMX_OK;
+}
+
+gcmx_status gsx_launch_count(const gsx_ctx* c, long long* launches) {
+	if (!c || !launches) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	*launches = c->launches;
 	return GCMX_OK;
 }
 
@@ -2207,7 +2222,7 @@ gcmx_status gsx_contact_plain(gsx_contact* c) {
 	if (!c->n) return GCMX_OK;
 	c->a->wStage = c->b->wStage = -1;  // u changes under any prepared invariants
 	return onBothStreams(c, [&] {
-		hipLaunchKernelGGL(k_sx_contact_plain, dim3((c->n + 255) / 256), dim3(256), 0, c->a->stream,
+		SX_LAUNCH(c->a, k_sx_contact_plain, dim3((c->n + 255) / 256), dim3(256), 0, c->a->stream,
 		                   c->na, c->nb, c->S, c->a->u, c->b->u, c->a->N, c->b->N, c->n);
 	});
 }
@@ -2222,7 +2237,7 @@ gcmx_status gsx_contact_correct(gsx_contact* c, int stage) {
 	const double* mA = c->a->mats;
 	const double* mB = c->b->mats;
 	return onBothStreams(c, [&] {
-		hipLaunchKernelGGL(k_sx_contact, dim3((c->n + 63) / 64), dim3(64), 0, c->a->stream, c->na,
+		SX_LAUNCH(c->a, k_sx_contact, dim3((c->n + 63) / 64), dim3(64), 0, c->a->stream, c->na,
 		                   c->nb, c->normal, c->S, c->codeA, c->codeB, mA + stage * 81,
 		                   mA + 3 * 81 + stage * 81, mB + stage * 81, mB + 3 * 81 + stage * 81,
 		                   c->a->wn, c->b->wn, c->a->N, c->b->N, c->n, stage, c->minDet[stage][0],

@@ -57,7 +57,8 @@ SYMBOLS = [
     "gsx_plain_correction", "gsx_upload", "gsx_download", "gsx_stage", "gsx_sync",
     "gsx_stage_nodes", "gsx_stage_finish", "gsx_contact_create", "gsx_contact_destroy",
     "gsx_contact_plain", "gsx_contact_correct", "gsx_step", "gsx_set_node_lanes",
-    "gsx_set_stage_fusion", "gsx_last_stage_fused", "gsx_stage_plan_info", "gsx_set_wait_budget",
+    "gsx_set_stage_fusion", "gsx_last_stage_fused", "gsx_launch_count", "gsx_stage_plan_info",
+    "gsx_set_wait_budget",
     "gsx_test_interpolate",
 ]
 
@@ -148,10 +149,13 @@ def lib() -> ctypes.CDLL:
                                       ctypes.c_int, ctypes.c_int, ctypes.POINTER(CommOptions)]
     L.gcmx_comm_channels_per_peer.argtypes = [vp]
     L.gcmx_comm_channels_per_peer.restype = ctypes.c_int
-    L.gcmx_comm_channels_rule.argtypes = [ctypes.c_int] * 8
-    L.gcmx_comm_channels_rule.restype = ctypes.c_int
-    L.gcmx_comm_posted_calls.argtypes = [vp]
-    L.gcmx_comm_posted_calls.restype = ctypes.c_longlong
+    # (ABI additions of round 5: bound when present, so that A/B timing runs can
+    # load an older build; tests/test_abi.py checks this build exports them)
+    if hasattr(L, "gcmx_comm_channels_rule"):
+        L.gcmx_comm_channels_rule.argtypes = [ctypes.c_int] * 8
+        L.gcmx_comm_channels_rule.restype = ctypes.c_int
+        L.gcmx_comm_posted_calls.argtypes = [vp]
+        L.gcmx_comm_posted_calls.restype = ctypes.c_longlong
     L.gcmx_comm_test_stall.argtypes = [vp, ctypes.c_int]
     L.gcmx_halo_exchange.argtypes = [vp]
     L.gcmx_halo_exchange_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int]

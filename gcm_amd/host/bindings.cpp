@@ -588,8 +588,12 @@ PYBIND11_MODULE(_gcm_host, m) {
 	    .def("set_node_lanes", [](PySimplexEngine& p, int lanes) { p.e->setNodeLanes(lanes); },
 	         "node-kernel layout: 0 automatic, 1 thread per node, 8 lanes per node", py::arg("lanes"))
 	    .def("set_stage_fusion", [](PySimplexEngine& p, int mode) { p.e->setStageFusion(mode); },
-	         "one launch per stage for a body without contacts: 0 off, 1 border + inner (default), "
-	         "2 with the gradient", py::arg("mode"))
+	         "one launch per stage for a body without contacts: 0 off, 1 border + inner, "
+	         "2 with the gradient, -1 (default) measured per mesh on the first steps", py::arg("mode"))
+	    .def_property_readonly("stage_fusion", [](PySimplexEngine& p) { return p.e->stageFusion(); })
+	    .def_property_readonly("fusion_tuning", [](PySimplexEngine& p) { return p.e->fusionTuning(); })
+	    .def_property_readonly("fusion_times_ms", [](PySimplexEngine& p) { return p.e->fusionTimes(); })
+	    .def_property_readonly("launches", [](PySimplexEngine& p) { return p.e->launches(); })
 	    .def_property_readonly("fused_stages", [](PySimplexEngine& p) { return p.e->fusedStages(); })
 	    .def_property_readonly("steps", [](PySimplexEngine& p) { return p.e->stepsDone(); })
 	    .def_property_readonly("time_step", [](PySimplexEngine& p) { return p.e->timeStepValue(); })

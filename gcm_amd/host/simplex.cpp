@@ -1243,7 +1243,25 @@ void Engine::setNodeLanes(int lanes) {
 }
 
 void Engine::setStageFusion(int mode) {
+	if (mode < 0) {  // measured per mesh on the next steps (nextTimeStep)
+		autoFusion_ = true;
+		tunePhase_ = 0;
+		mode = 1;
+	} else {
+		autoFusion_ = false;
+	}
 	for (auto& b : bodies) gcmxCheck(gsx_set_stage_fusion(b.ctx, mode), "gsx_set_stage_fusion");
+	fusionMode_ = mode;
+}
+
+long long Engine::launches() const {
+	long long n = 0;
+	for (const auto& b : bodies) {
+		long long k = 0;
+		gcmxCheck(gsx_launch_count(b.ctx, &k), "gsx_launch_count");
+		n += k;
+	}
+	return n;
 }
 
 Engine::~Engine() {
@@ -1257,7 +1275,43 @@ real Engine::estimateTimeStep() { return tau; }
 // basis: plain corrections at the next time layer, then gcmStage (:119-143) for
 // every stage: beforeStage + contactAndBorderStage of every body, the contact
 // correctors, then (per body) its border correctors, innerStage, afterStage, swap.
+// The automatic stage-fusion choice (setStageFusion(-1)) is made on the first
+// steps: one warm-up step, kTuneSteps in mode 1, kTuneSteps in mode 2, each
+// block between stream synchronisations; mode 2 is kept only if >= 3 % faster
+// (faster on the fracture layer, slower on the cube).  Every
+// mode gives the same results (test_one_launch_stage_equals_two_launches), so
+// the timed steps are the run's own steps.
 void Engine::nextTimeStep() {
+	const bool tuning = autoFusion_ && tunePhase_ < 3 && contacts.empty() && !replaySteps;
+	if (tuning && tunePhase_ > 0 && tuneLeft_ == kTuneSteps) {
+		sync();
+		tuneT0_ = std::chrono::steady_clock::now();
+	}
+	stepCalls();
+	if (!tuning) return;
+	if (tunePhase_ == 0) {
+		tunePhase_ = 1;
+		tuneLeft_ = kTuneSteps;
+		return;
+	}
+	if (--tuneLeft_ > 0) return;
+	sync();
+	tuneMs_[tunePhase_ - 1] =
+	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tuneT0_).count() / kTuneSteps;
+	if (tunePhase_ == 1) {
+		tunePhase_ = 2;
+		tuneLeft_ = kTuneSteps;
+		for (auto& b : bodies) gcmxCheck(gsx_set_stage_fusion(b.ctx, 2), "gsx_set_stage_fusion");
+		fusionMode_ = 2;
+	} else {
+		tunePhase_ = 3;
+		const int best = tuneMs_[1] < 0.97 * tuneMs_[0] ? 2 : 1;
+		for (auto& b : bodies) gcmxCheck(gsx_set_stage_fusion(b.ctx, best), "gsx_set_stage_fusion");
+		fusionMode_ = best;
+	}
+}
+
+void Engine::stepCalls() {
 	setBorderValues(Clock::Time() + Clock::TimeStep());
 	if (replaySteps) {  // the same calls, captured once per layer state and replayed
 		std::vector<gsx_ctx*> ctxs;

@@ -19,6 +19,7 @@
 #pragma once
 
 #include <array>
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <utility>
@@ -266,8 +267,22 @@ public:
 	/// Thread layout of every body's node kernels (gsx_set_node_lanes: 0 auto, 1, 8).
 	void setNodeLanes(int lanes);
 	/// One launch per stage for the border and inner halves of a body without
-	/// contacts (gsx_set_stage_fusion: 0 off, 1 default, 2 with the gradient).
+	/// contacts (gsx_set_stage_fusion: 0 off, 1 border + inner, 2 with the
+	/// gradient; -1, the default: measured per mesh -- the engine's first steps
+	/// run kTuneSteps in mode 1 and kTuneSteps in mode 2 between stream
+	/// synchronisations and keep mode 2 only where it is >= 3 % faster; the
+	/// modes give identical results, so the measured steps are ordinary steps).
 	void setStageFusion(int mode);
+	/// the mode in effect (1 or 2 while / after measuring in mode -1), and
+	/// whether the automatic choice is still being measured
+	int stageFusion() const { return fusionMode_; }
+	bool fusionTuning() const { return autoFusion_ && tunePhase_ < 3; }
+	/// measured ms per step of modes 1 and 2 (automatic mode; 0 before)
+	std::pair<double, double> fusionTimes() const { return {tuneMs_[0], tuneMs_[1]}; }
+	/// kernel launches made on the bodies' streams since construction
+	/// (gsx_launch_count): the dependent launches of the steps
+	long long launches() const;
+	static constexpr int kTuneSteps = 8;
 	/// stages run as one launch since construction
 	long long fusedStages() const { return fusedStages_; }
 	/// (plan admits the one launch, inner feet that wait there) of a body's stage
@@ -282,6 +297,14 @@ protected:
 	void writeSnapshots(const int step) override;
 
 private:
+	bool autoFusion_ = true;  // stage fusion mode measured per mesh (setStageFusion(-1))
+	int fusionMode_ = 1;
+	int tunePhase_ = 0;       // 0: warm-up step, 1 / 2: timing mode 1 / 2, 3: chosen
+	int tuneLeft_ = 0;
+	double tuneMs_[2] = {0.0, 0.0};
+	std::chrono::steady_clock::time_point tuneT0_;
+	void stepCalls();
+
 	struct Body {
 		size_t id = 0;
 		int materialNumber = 0;

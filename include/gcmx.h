@@ -454,18 +454,20 @@ gcmx_status gsx_set_node_lanes(gsx_ctx* ctx, int lanes);
  * space-time with border nodes' new invariants waits, on the device, for exactly
  * those nodes): on = 1 (default) border + inner, 2 also the gradient groups in
  * the same launch, 0 separate launches, 3 (tuning only) mode 1 without the
- * 4096-block cap on the fused grid.  Results are identical.  The one launch
- * relies on workgroups being dispatched in id order (how the hardware behaves,
- * not a HIP guarantee); every device-side wait is bounded and a timed-out wait
- * is reported by gsx_sync / gsx_download / the engine's run_steps.
+ * 4096-block cap on the fused grid.  Results are identical.  In the one
+ * launch a block takes its work index from an atomic ticket when it starts, so
+ * it waits only on work that blocks already running took (no assumption on
+ * dispatch order); every device-side wait is bounded and a timed-out wait is
+ * reported by gsx_sync / gsx_download / the engine's run_steps.
  * gsx_last_stage_fused reports whether the last gsx_stage ran as one launch. */
 gcmx_status gsx_set_stage_fusion(gsx_ctx* ctx, int on);
 gcmx_status gsx_last_stage_fused(const gsx_ctx* ctx, int* fused);
-/* Tuning only: on = 3 is mode 1 without the 4096-block grid cap.  The one
- * launch relies on workgroups being dispatched in block-id order (each block
- * waits only on blocks with lower ids); every device wait is bounded: a wait
- * that gives up sets the context's error word, which gsx_sync and gsx_download
- * report (GCMX_ERR_STATE, "results invalid") and clear.
+/* Kernel launches made on the context's stream so far (each a dependent
+ * kernel boundary of its step: the launch-floor model). */
+gcmx_status gsx_launch_count(const gsx_ctx* ctx, long long* launches);
+/* Tuning only: on = 3 is mode 1 without the 4096-block grid cap.  Every device
+ * wait is bounded: a wait that gives up sets the context's error word, which
+ * gsx_sync and gsx_download report (GCMX_ERR_STATE, "results invalid") and clear.
  * gsx_stage_plan_info: whether stage `stage`'s plan admits the one launch and
  * how many inner feet wait there for border nodes' new invariants.
  * gsx_set_wait_budget: polls per device wait (default 2^20); < 0 makes every

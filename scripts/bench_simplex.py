@@ -20,6 +20,10 @@ two stream synchronisations, inputs resident on the device.  Prints one JSON lin
 per workload.
 
     python scripts/bench_simplex.py [--workloads cubetask,cube,fracture,layered] [--n 64]
+
+Each line carries the step's dependent launches (launches_per_step, counted by
+gsx_launch_count) and the launch floor they imply (floor_ms: 1.45-1.9 us per
+kernel boundary, MI355X_MICROARCH.md) beside the measured ms_per_step.
 """
 import argparse
 import json
@@ -57,8 +61,9 @@ def main():
                     help="node-kernel layout (gsx_set_node_lanes): 0 automatic, 1, 8")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from a gsx_step HIP graph instead of the stage calls")
-    ap.add_argument("--fusion", type=int, default=1,
-                    help="gsx_set_stage_fusion: 0 separate launches, 1 border + inner in one, 2 with the gradient")
+    ap.add_argument("--fusion", type=int, default=-1,
+                    help="gsx_set_stage_fusion: 0 separate launches, 1 border + inner in one, 2 with the "
+                         "gradient, -1 (the engine's default) measured per mesh on the first steps")
     a = ap.parse_args()
     from gcm_amd import _gcm_host as H
     for name in a.workloads.split(","):
@@ -71,12 +76,16 @@ def main():
         e.set_stage_fusion(a.fusion)
         setup = time.perf_counter() - t0
         nv = sum(e.number_of_vertices(b) for b in range(e.number_of_bodies))
-        e.run_steps(a.warmup)
+        # the automatic fusion choice is made on the first 1 + 2 * 8 steps: warm past it
+        warm = max(a.warmup, 20) if a.fusion < 0 else a.warmup
+        e.run_steps(warm)
         e.sync()
+        l0 = e.launches
         t1 = time.perf_counter()
         e.run_steps(a.steps)
         e.sync()
         dt = time.perf_counter() - t1
+        lps = (e.launches - l0) / a.steps
         print(json.dumps({
             "metric": "simplex Mnode-steps/s", "workload": name, "mesh": desc,
             "value": round(nv * a.steps / dt / 1e6, 2), "unit": "Mnode-steps/s",
@@ -84,7 +93,15 @@ def main():
             "bodies": e.number_of_bodies, "contact_pairs": e.number_of_contact_pairs,
             "steps": a.steps, "warmup": a.warmup, "setup_s": round(setup, 1), "dtype": "f64",
             "graph": a.graph, "lanes": a.lanes, "fusion": a.fusion,
+            "fusion_in_effect": e.stage_fusion,
+            "fusion_times_ms": [round(v, 4) for v in e.fusion_times_ms] if a.fusion < 0 else None,
             "fused_stages": e.fused_stages,
+            # the launch floor: every launch of a step is a dependent kernel boundary on
+            # the body's stream; MI355X_MICROARCH.md's price list puts one at 1.45 us
+            # (trivial kernels) to 1.7-1.9 us (real streaming kernels)
+            "launches_per_step": round(lps, 2),
+            "floor_ms": [round(lps * 1.45e-3, 4), round(lps * 1.9e-3, 4)],
+            "floor_frac": round(lps * 1.45e-3 / (dt / a.steps * 1e3), 3),
         }), flush=True)
 
 

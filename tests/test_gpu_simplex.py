@@ -230,6 +230,33 @@ def test_one_launch_stage_equals_two_launches(H, case, mode):
     assert np.abs(fused).max() > 0
 
 
+def test_automatic_stage_fusion_equals_fixed_mode(H):
+    """the engine's default fusion mode (-1) measures modes 1
+    and 2 on its first steps (one warm-up step, 8 steps each between stream
+    synchronisations) and keeps the faster; the modes give identical results, so
+    a run through the choice equals a run in mode 1, bitwise.  The engine also
+    counts every launch of a step (gsx_launch_count) for the launch floor."""
+    mk = lambda: fracture_task((12, 12, 6), 1.0)  # noqa: E731
+    steps = 1 + 2 * 8 + 3
+    out = []
+    for fuse in (-1, 1):
+        e = H.SimplexEngine(mk())
+        e.set_node_lanes(8)
+        e.set_stage_fusion(fuse)
+        assert e.fusion_tuning == (fuse < 0)
+        l0 = e.launches
+        e.run_steps(steps)
+        e.sync()
+        out.append((e.pde(), e.stage_fusion, e.fusion_tuning, e.fusion_times_ms, e.launches - l0))
+    (auto, mode, tuning, times, launches), (fixed, mode1, _, _, launches1) = out
+    assert not tuning and mode in (1, 2) and mode1 == 1
+    assert times[0] > 0 and times[1] > 0
+    assert (mode == 2) == (times[1] < 0.97 * times[0])
+    assert launches > 0 and launches1 > 0 and launches1 % steps == 0
+    assert np.array_equal(auto, fixed), f"{int((auto != fixed).sum())} values differ"
+    assert np.abs(fixed).max() > 0
+
+
 @pytest.mark.timeout(300)
 def test_one_launch_stage_above_block_cap_completes(H):
     """k_sx_stage_l8 takes its work index from an atomic
