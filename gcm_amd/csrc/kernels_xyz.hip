@@ -308,6 +308,9 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_HET_AB
 #define GCMX_HET_AB 0
 #endif
+#ifndef GCMX_TX2_UNROLL  // timing knob: row-loop unroll (5 = the window period: no window moves)
+#define GCMX_TX2_UNROLL 1
+#endif
 
 
 // Per-node materials: every lane applies ITS OWN material's table, read from
@@ -1002,6 +1005,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		x_enter(y, pre, kn);
 		TX2_T(5);
 	};
+#if GCMX_TX2_UNROLL > 1
+#pragma unroll GCMX_TX2_UNROLL
+#endif
 	for (int it = 0; it < ye - yb; it++) row(REV ? ye - 1 - it : yb + it, it);
 #if GCMX_TX2_DIAG
 	if ((threadIdx.x & 63) == 0) {

@@ -320,6 +320,60 @@ void tz(const double* in, double* out, int chunk, size_t shm) {
 	std::fflush(stdout);
 }
 
+
+// Box characterisation: an fp64-FMA-only kernel on random
+// operands, no memory traffic in the loop -- the clock a box holds when the VALU
+// alone draws the power.  Eight independent chains per lane, ITERS iterations;
+// 4 cycles per wave64 fp64 FMA per SIMD, so the effective clock is
+// (waves per SIMD x ITERS x 8 x 4 cycles) / time.
+template <int ITERS>
+__global__ __launch_bounds__(256) void k_valu_fp64(double* __restrict__ out, unsigned long long seed) {
+	unsigned long long s = seed ^ (0x9E3779B97F4A7C15ull * (blockIdx.x * 256 + threadIdx.x + 1));
+	double a[8], b[8];
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		s = s * 6364136223846793005ull + 1442695040888963407ull;
+		a[i] = 0.5 + (double)(s >> 11) * 0x1.0p-54;
+		b[i] = 1.0 - (double)((s >> 7) & 0xffff) * 0x1.0p-20;
+	}
+	const double c = 0.999999 + (double)(s & 0xff) * 1e-12;
+	for (int k = 0; k < ITERS; k++) {
+#pragma unroll
+		for (int i = 0; i < 8; i++) a[i] = __builtin_fma(a[i], b[i], c * 1e-3);
+	}
+	double acc = 0;
+#pragma unroll
+	for (int i = 0; i < 8; i++) acc += a[i];
+	if (acc == 1234.5) out[0] = acc;
+}
+
+void valu_span(double* out, int cus) {
+	constexpr int ITERS = 1 << 16;
+	static const int reps = std::getenv("PROBE_REPS") ? std::atoi(std::getenv("PROBE_REPS")) : 10;
+	const int blocks = cus * 8;  // 8 waves per SIMD... 8 blocks of 4 waves per CU
+	hipEvent_t a, b;
+	CK(hipEventCreate(&a));
+	CK(hipEventCreate(&b));
+	hipLaunchKernelGGL((k_valu_fp64<ITERS>), dim3(blocks), dim3(256), 0, 0, out, 1ull);
+	CK(hipDeviceSynchronize());
+	timespec t0, t1;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	CK(hipEventRecord(a));
+	for (int r = 0; r < reps; r++) hipLaunchKernelGGL((k_valu_fp64<ITERS>), dim3(blocks), dim3(256), 0, 0, out, 2ull + r);
+	CK(hipEventRecord(b));
+	CK(hipEventSynchronize(b));
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	float ms = 0;
+	CK(hipEventElapsedTime(&ms, a, b));
+	ms /= reps;
+	// per SIMD: 8 waves (8 blocks x 4 waves / 4 SIMDs) x ITERS x 8 FMAs x 4 cycles
+	const double cycles = 8.0 * ITERS * 8 * 4;
+	std::printf("fp64 FMA only (8 waves/SIMD, random operands): %.3f ms, effective clock %.0f MHz "
+	            "[mono %.6f %.6f]\n", ms, cycles / (ms * 1e-3) / 1e6, t0.tv_sec + 1e-9 * t0.tv_nsec,
+	            t1.tv_sec + 1e-9 * t1.tv_nsec);
+	std::fflush(stdout);
+}
+
 // the flat 16-B copy of the layout (k_probe MODE 0, VEC 2) with its monotonic span
 void copy_span(const double* in, double* out) {
 	const double nodes = (double)N * N * N;
@@ -451,6 +505,16 @@ int main() {
 	CK(hipMalloc(&out, bytes));
 	CK(hipMemset(in, 0, bytes));
 	CK(hipMemset(out, 0, bytes));
+	if (std::getenv("BOX_ONLY")) {  // box characterisation: HBM copy and fp64 VALU, each alone
+		int dev = 0, cus = 256;
+		CK(hipGetDevice(&dev));
+		CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+		copy_span(in, out);
+		valu_span(out, cus);
+		copy_span(in, out);
+		valu_span(out, cus);
+		return 0;
+	}
 	if (std::getenv("TZ_ONLY")) {  // two planes x two z groups per lane at one wave per SIMD
 		copy_span(in, out);
 		tz<2, 0, 512, 1, 1>(in, out, 128, 96 * 1024);   // = the shipped pattern, 1 block/CU
