@@ -445,6 +445,22 @@ def test_face_map_refuses_bad_maps(G):
     ctx.close()
 
 
+def test_context_close_closes_its_face_maps_and_node_lists(G):
+    """gcmx_face_map_destroy / gcmx_border_nodes_destroy read their
+    context (device, stream), so a FaceMap or BorderNodes outliving an explicit
+    Context.close() must not call them afterwards.  The context closes its
+    children first; their later close() (or collection) is then a no-op."""
+    b = partial_body(2, [6, 12, 64], PARTIAL_CASES["bs1"][2])
+    ctx = context_for(b)
+    fmap = ctx.face_map([None, None, np.zeros(6 * 64, dtype=np.uint8), None, None, None])
+    nodes = ctx.border_nodes(1, -1, np.array([[0, 0, 0], [1, 0, 3]], dtype=np.int32))
+    ctx.close()
+    assert not fmap.ptr.value and not nodes.ptr.value  # closed with their context
+    fmap.close()
+    nodes.close()
+    del fmap, nodes
+
+
 def test_engine_partial_faces_one_pass(G):
     """A titan-like body through the C++ engine: border conditions whose areas
     cover parts of faces -> HipBorderConditions builds the per-node face map and

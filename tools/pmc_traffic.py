@@ -32,7 +32,7 @@ def readable(rocprof_name):
     return f"{m.group(1)}<{', '.join(out)}>"
 
 
-def main(prof_dir, out, n=512, lib_path="gcm_amd/lib/libgcmx.so"):
+def main(prof_dir, out, n=512, lib_path="gcm_amd/lib/libgcmx.so", calib_json=None):
     f = agg(f"{prof_dir}/fetch/run_counter_collection.csv", "FETCH_SIZE")
     w = agg(f"{prof_dir}/write/run_counter_collection.csv", "WRITE_SIZE")
     true = 8 * (1 << 30)
@@ -42,12 +42,13 @@ def main(prof_dir, out, n=512, lib_path="gcm_amd/lib/libgcmx.so"):
         r8 = [v for k, v in cf.items() if k.startswith("read8")][0] * 1024
         w8 = [v for k, v in cw.items() if k.startswith("write8")][0] * 1024
     except (FileNotFoundError, IndexError):  # reuse the stored calibration run
-        old = json.load(open(out))["calibration"]
+        old = json.load(open(calib_json or out))["calibration"]
         r8, w8 = old["read8_fetch_bytes"], old["write8_write_bytes"]
     ff, wf = true / r8, true / w8
     alg = 144 * n ** 3
     import hashlib
     sha = hashlib.sha256(open(lib_path, "rb").read()).hexdigest()
+    z = min(t for t in (64, 128, 256, 512, 1024) if t >= n)  # the launch's ZT
     res = {"n": n, "ranks": 1, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, {prof_dir}",
            "lib_sha256": sha,
            "calibration": {"tool": "tools/calib_fetch.hip", "true_bytes": true,
@@ -55,8 +56,8 @@ def main(prof_dir, out, n=512, lib_path="gcm_amd/lib/libgcmx.so"):
                            "write8_write_bytes": w8, "write_factor": wf},
            "kernels": {}}
     # bench.py's bucket "fused_xyz" is the one-pass step: k_step_tx2 (default) or k_fused_xyz
-    for short, frag in (("march_x", "k_march<0, 2"), ("fused_yz", "k_fused_yz<2, 512"),
-                        ("fused_xyz", "k_fused_xyz<2, 512"), ("fused_xyz", "k_step_tx2<2, 512")):
+    for short, frag in (("march_x", "k_march<0, 2"), ("fused_yz", f"k_fused_yz<2, {z}"),
+                        ("fused_xyz", f"k_fused_xyz<2, {z}"), ("fused_xyz", f"k_step_tx2<2, {z}")):
         fks = [v for k, v in f.items() if frag in k]
         wks = [v for k, v in w.items() if frag in k]
         if not fks or not wks:
@@ -74,4 +75,6 @@ def main(prof_dir, out, n=512, lib_path="gcm_amd/lib/libgcmx.so"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    # pmc_traffic.py PROF_DIR OUT.json [N] [CALIBRATION.json: reuse its stored calibration]
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 512,
+         calib_json=sys.argv[4] if len(sys.argv) > 4 else None)
