@@ -35,5 +35,5 @@ tot = a.sum(axis=1)
 print("per wave-in-block: share of cycles by phase")
 for w in range(8):
     print(f"wave {w}: " + "  ".join(f"{names[i]} {a[w, i] / tot[w]:.3f}" for i in range(7)))
-blocks = (N // 128) * (N // 2)
-print(f"mean cycles per wave per row: {tot[:8].mean() / (blocks * 128 * steps):.0f}")
+pair_rows = (N // 2) * N  # every (x pair, row) once, whatever the chunking
+print(f"mean cycles per wave per row: {tot[:8].mean() / (pair_rows * steps):.0f}")
