@@ -240,6 +240,16 @@ def rank_record(ctx, rank, kernels, steps_total, step_ms):
             "channels_per_peer": ctx.comm_channels_per_peer}
 
 
+def box_summary(box, sampled):
+    """The few box fields that tell ranks' GPUs apart (tools/box_state.py)."""
+    import statistics
+    box = box or {}
+    sampled = sampled or {}
+    sc = [int(k[:-3]) for k, n in (sampled.get("sclk") or {}).items() if k.endswith("Mhz") for _ in range(n)]
+    return {"unique_id": box.get("unique_id"), "vbios": box.get("vbios_version"),
+            "power_w": sampled.get("power_w"), "sclk_mhz_median": statistics.median(sc) if sc else None}
+
+
 def multi_gpu_parity(dist, world, rank, device, U, U1, L, channels):
     """N > 1 self-check of the RCCL X-slab path (halo exchange overlapped with the
     interior X stage): 3 steps on a 12*N x 40 x 64 grid split into N slabs must
@@ -410,7 +420,7 @@ def main():
     tau = 0.9 * 1.0 / 1.0  # Courant * h / max|lambda| (Engine.cpp:124-140)
 
     box = None
-    if rank == 0 and not a.no_box_state:
+    if not a.no_box_state:  # every rank reads its own GPU's state (per_rank for N > 1)
         try:
             box = box_state.static_state(device)
         except Exception as e:  # reported context, never required
@@ -466,7 +476,7 @@ def main():
         ctx.profile(True)
         ctx.profile_reset()
     sampler = None
-    if rank == 0 and not a.no_box_state:
+    if not a.no_box_state:
         try:
             sampler = box_state.Sampler(device).start()
         except Exception as e:  # reported context, never required
@@ -505,6 +515,7 @@ def main():
     per_rank = None
     if (world > 1 or a.rccl_self) and kernels:
         rec = rank_record(ctx, rank, kernels, a.steps * max(1, a.reps), el / a.steps * 1e3)
+        rec["box"] = box_summary(box, sampled)
         if dist is not None:
             recs = [None] * world if rank == 0 else None
             dist.gather_object(rec, recs, dst=0)

@@ -19,3 +19,29 @@ def test_copy_ceiling_reports_a_plausible_rate():
             c.copy_ceiling_ms(nbytes, 0)
     finally:
         c.close()
+
+
+@pytest.mark.timeout(240)
+def test_bench_prints_one_json_line_with_rccl_self():
+    """The driver reads ONE JSON line from bench.py's stdout.  With an RCCL
+    communicator in the process (RCCL prints a version banner on stdout when one
+    is created) the line must still be the only stdout output, and an exchange
+    run carries per_rank with the exchange timings and the rank's box summary."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--n", "64", "--steps", "3",
+                        "--warmup", "1", "--reps", "2", "--rccl-self", "--no-cpu-baseline",
+                        "--no-copy-ceiling", "--no-clock-probe"],
+                       capture_output=True, text=True, timeout=200, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["roofline"]["kernel"] == "fused_xyz"
+    pr = d["per_rank"]
+    assert len(pr) == 1 and pr[0]["halo_ms"] > 0 and pr[0]["transport"] == "halo_rccl"
+    assert pr[0]["halo_posts_per_step"] == 1.0 and pr[0]["bytes_per_direction"] > 0
+    assert "box" in pr[0] and "process_state" in d
