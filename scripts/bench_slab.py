@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 import gcm_amd  # noqa: E402
 from gcm_amd import gcmx  # noqa: E402
 from gcm_amd.host import isotropic_elastic_matrices  # noqa: E402
-from bench import rank_record  # noqa: E402
+from bench import rank_record, stdout_to_stderr  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--sched", default="bfirst", choices=["single", "xslab", "bfirst"])
@@ -65,7 +65,8 @@ def make(X, path=gcmx.PATH_AUTO, x0=0, loop=False):
     c.set_schedule(SCHED, args.rows)
     c.fill_random([N, N, N], 0x5EED)
     if loop and args.rccl_self:
-        c.comm_init(gcm_amd.unique_id(), 1, 0, 0, 0)
+        with stdout_to_stderr():  # RCCL's banner stays off the JSON lines
+            c.comm_init(gcm_amd.unique_id(), 1, 0, 0, 0)
     elif loop and args.loop_gbps >= 0:
         c.comm_init_loopback(args.loop_gbps, args.loop_blocks)
     return c
