@@ -128,6 +128,7 @@ struct gcmx_ctx {
 	AxisTable* tabs_d = nullptr;   // [mat][D]
 	double tabs_tau = NAN;
 	bool iso_fast = false;         // fast kernels admissible (3-D, homogeneous, iso structure)
+	bool iso2_fast = false;        // the 2-D one-pass step may run its isotropic kernel
 	IsoAxis iso[3] = {};           // per-axis values for the fast kernels (tau part in build_tables)
 	bool iso_het = false;          // per-node materials, every material of the iso structure (k_step_tx2 HET)
 	bool het_ok = false;           // this tau: floor(q) = 0 and equal axes for every material
@@ -300,12 +301,13 @@ gcmx_status build_tables(gcmx_ctx* c, double tau) {
 				for (int i = 1; i <= bs; i++) t.coef[k][i - 1] = ((q - i) + 1) / i;
 			}
 		}
-	if (c->iso_fast) {
+	if (c->iso_fast || c->iso2_fast) {
+		const int nfeet = D == 3 ? 6 : 4;
 		for (int s = 0; s < D; s++) {
 			const AxisTable& t = h[s];
 			IsoAxis& A = c->iso[s];
-			// feet k and k^1 share q; feet 2..5 share q (|L| equal, checked at extraction)
-			for (int k = 1; k < 6; k++) {
+			// feet k and k^1 share q; feet 2..5 (2-D: 2, 3) share q (|L| equal, checked at extraction)
+			for (int k = 1; k < nfeet; k++) {
 				const int ref = (k < 2) ? 0 : 2;
 				if (t.kf[k] != t.kf[ref] || std::memcmp(t.coef[k], t.coef[ref], sizeof(t.coef[k])) != 0)
 					return fail(GCMX_ERR_STATE, "inconsistent foot data");
@@ -741,6 +743,12 @@ void refresh_fast(gcmx_ctx* c) {
 		fits = iso_axis_extract(sx, &c->U[(size_t)sx * M * M], &c->U1[(size_t)sx * M * M],
 		                        &c->L[(size_t)sx * M], c->iso[sx]);
 	c->iso_fast = fits;
+	// the 2-D one-pass step's isotropic kernel: one material, the ElasticModel<2> structure
+	bool fits2 = D == 2 && c->mat_d == nullptr && c->n_mat == 1 && step2d_iso_supported(c->geo);
+	for (int sx = 0; fits2 && sx < D; sx++)
+		fits2 = iso2_axis_extract(sx, &c->U[(size_t)sx * M * M], &c->U1[(size_t)sx * M * M], &c->L[(size_t)sx * M],
+		                          c->iso[sx]);
+	c->iso2_fast = fits2;
 	// heterogeneous one-pass step: per-node ids and every material of the structure
 	bool het = !fits && D == 3 && c->mat_d != nullptr && c->n_mat >= 1 && c->n_mat <= kHetMaxMaterials &&
 	           fast_layout_ok(c->geo) && het_supported(c->geo);
@@ -755,11 +763,21 @@ void refresh_fast(gcmx_ctx* c) {
 	c->tabs_tau = NAN;
 }
 
+// The one-pass 2-D step (k_step2d) runs where its preconditions hold: one
+// material, no ghost ever written (so every ghost of both layers is zero and
+// the two layers' ghosts agree, whichever one the step leaves the state in),
+// no X-slab exchange, a borderSize it is built for, and no forced per-stage path.
+bool step2d_admissible(const gcmx_ctx* c) {
+	return c->D == 2 && step2d_supported(c->geo) && c->mat_d == nullptr && c->n_mat == 1 && !c->ghosts_touched &&
+	       c->faces_written == 0 && !has_halo(c) && c->path != GCMX_PATH_GENERIC && c->path != GCMX_PATH_SPLIT;
+}
+
 gcmx_path effective_path(gcmx_ctx* c) {
 	if (c->iso_het) {  // per-node materials: the one-pass step or the generic stages
 		if (c->path == GCMX_PATH_GENERIC || c->path == GCMX_PATH_SPLIT || c->ghosts_touched) return GCMX_PATH_GENERIC;
 		return GCMX_PATH_FUSED;
 	}
+	if (c->D == 2) return step2d_admissible(c) ? GCMX_PATH_FUSED : GCMX_PATH_GENERIC;
 	if (c->D != 3 || !c->iso_fast || c->bs > 3) return GCMX_PATH_GENERIC;
 	if (c->path == GCMX_PATH_GENERIC) return GCMX_PATH_GENERIC;
 	if (c->path == GCMX_PATH_SPLIT) return GCMX_PATH_SPLIT;
@@ -806,7 +824,8 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	}
 	const Geo& g = c->geo;
 	const double bytes = node_stage_bytes(c) * (double)g.n_inner;
-	const gcmx_path p = c->iso_het ? GCMX_PATH_GENERIC : effective_path(c);  // no per-stage het kernels
+	// no per-stage het kernels; the per-stage kernels of the split path are 3-D only
+	const gcmx_path p = (c->iso_het || c->D != 3) ? GCMX_PATH_GENERIC : effective_path(c);
 	bool ok;
 	if (p == GCMX_PATH_GENERIC) {
 		Timed t(c, "stage_generic", bytes, c->stream);
@@ -1235,6 +1254,20 @@ struct SlabJoin {
 	}
 };
 
+// One 2-D step in one pass (k_step2d, cur -> nxt, then swap): the caller
+// checked step2d_admissible.
+gcmx_status step2d(gcmx_ctx* c) {
+	const Geo& g = c->geo;
+	Timed t(c, "step2d", node_stage_bytes(c) * (double)g.n_inner, c->stream);
+	if (!launch_step2d(c->cur, c->nxt, g, c->tabs_d, c->iso2_fast ? c->iso : nullptr, c->stream, &t.kname))
+		return fail(GCMX_ERR_UNSUPPORTED, "no 2-D step variant for this configuration");
+	HIP_TRY(hipGetLastError());
+	std::swap(c->cur, c->nxt);
+	touch_layer(c);
+	c->last_path = GCMX_PATH_FUSED;
+	return GCMX_OK;
+}
+
 // One fused step (k_step_tx2 / k_fused_xyz): the caller checked the path.
 // `fb`: y/z face conditions (x faces already filled in memory), or null.
 // `final`: the step's result is the new state (no separate ODE pass follows).
@@ -1425,6 +1458,11 @@ gcmx_status step_body(gcmx_ctx* c, double tau, const StepOde& ode) {
 	gcmx_status s = build_tables(c, tau);
 	if (s) return s;
 	c->last_ode_fused = false;
+	if (c->D == 2 && effective_path(c) == GCMX_PATH_FUSED) {
+		s = step2d(c);
+		if (s) return s;
+		return ode.on ? ode_apply(c, ode.f) : GCMX_OK;
+	}
 	if (effective_path(c) != GCMX_PATH_FUSED || c->faces_written != 0 || (c->iso_het && !c->het_ok)) {
 		for (int a = 0; a < c->D; a++) {
 			s = stage_impl(c, a, tau);

@@ -72,6 +72,16 @@ inline void lagrange_weights(const double* c, int bs, double* w) {
 	}
 }
 bool iso_axis_extract(int s, const double* U, const double* U1, const double* L, IsoAxis& A);
+// kernels_2d.hip: the one-pass 2-D step.  One material: tabs = its X and Y
+// tables; iso = its two IsoAxis (the isotropic structure, iso2_axis_extract) or
+// null.  borderSize 1..kStep2dMaxBs (the isotropic kernel up to 3), y ghost
+// columns of both layers zero.
+constexpr int kStep2dMaxBs = 5;
+bool iso2_axis_extract(int s, const double* U, const double* U1, const double* L, IsoAxis& A);
+bool step2d_supported(const Geo& g);
+bool step2d_iso_supported(const Geo& g);
+bool launch_step2d(const double* cur, double* nxt, const Geo& g, const AxisTable* tabs, const IsoAxis* iso,
+                   hipStream_t st, const char** kname);
 bool fast_layout_ok(const Geo& g);
 bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const IsoAxis& A,
                   int x0, int x1, hipStream_t st);

@@ -131,7 +131,10 @@ gcmx_status gcmx_stage(gcmx_ctx* ctx, int axis, double tau);
 /* All `dim` stages of one time step with no border or contact work between
  * them (cubic::Engine::nextTimeStep, Engine.cpp:90-121, for a body without
  * border conditions, contacts or ODEs).  May run fused kernels; results are
- * identical to dim consecutive gcmx_stage calls. */
+ * identical to dim consecutive gcmx_stage calls.  3-D: the one-pass step
+ * (k_step_tx2 / k_fused_xyz); 2-D: the one-pass step k_step2d_iso / k_step2d
+ * with one material, untouched ghosts and no X-slab exchange (else the
+ * per-stage kernels); 1-D: the one stage. */
 gcmx_status gcmx_step(gcmx_ctx* ctx, double tau);
 gcmx_status gcmx_set_kernel_path(gcmx_ctx* ctx, gcmx_path path);
 /* Step schedule of the fused path and the fused kernel's y rows per block
