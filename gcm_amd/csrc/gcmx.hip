@@ -771,6 +771,15 @@ bool step2d_admissible(const gcmx_ctx* c) {
 	return c->D == 2 && step2d_supported(c->geo) && c->mat_d == nullptr && c->n_mat == 1 && !c->ghosts_touched &&
 	       c->faces_written == 0 && !has_halo(c) && c->path != GCMX_PATH_GENERIC && c->path != GCMX_PATH_SPLIT;
 }
+// The same with whole-face border conditions `on` (bit 2*axis + side): the
+// isotropic kernel, the y ghost columns formed in the pass from the mirrored
+// inner columns (Y >= bs + 1), and every face whose ghosts an earlier step wrote
+// refreshed now.
+bool step2d_faces_admissible(const gcmx_ctx* c, unsigned on) {
+	return c->D == 2 && c->iso2_fast && step2d_iso_supported(c->geo) && c->mat_d == nullptr && c->n_mat == 1 &&
+	       !c->ghosts_touched && (c->faces_written & ~on) == 0 && !has_halo(c) && c->path != GCMX_PATH_GENERIC &&
+	       c->path != GCMX_PATH_SPLIT && c->geo.sizes[1] >= c->bs + 1;
+}
 
 gcmx_path effective_path(gcmx_ctx* c) {
 	if (c->iso_het) {  // per-node materials: the one-pass step or the generic stages
@@ -1256,10 +1265,10 @@ struct SlabJoin {
 
 // One 2-D step in one pass (k_step2d, cur -> nxt, then swap): the caller
 // checked step2d_admissible.
-gcmx_status step2d(gcmx_ctx* c) {
+gcmx_status step2d(gcmx_ctx* c, const Face2* faces = nullptr) {
 	const Geo& g = c->geo;
 	Timed t(c, "step2d", node_stage_bytes(c) * (double)g.n_inner, c->stream);
-	if (!launch_step2d(c->cur, c->nxt, g, c->tabs_d, c->iso2_fast ? c->iso : nullptr, c->stream, &t.kname))
+	if (!launch_step2d(c->cur, c->nxt, g, c->tabs_d, c->iso2_fast ? c->iso : nullptr, c->stream, &t.kname, faces))
 		return fail(GCMX_ERR_UNSUPPORTED, "no 2-D step variant for this configuration");
 	HIP_TRY(hipGetLastError());
 	std::swap(c->cur, c->nxt);
@@ -1542,6 +1551,45 @@ gcmx_status step_faces_body(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 	}
 	s = build_tables(c, tau);
 	if (s) return s;
+	auto fill = [&](int f) -> gcmx_status {
+		s = halo_wait(c);
+		if (s) return s;
+		Timed t(c, "face_fill", 0.0, c->stream);
+		launch_face_fill(c->cur, c->geo, f / 2, (f & 1) ? 1 : -1, bq[f], c->stream);
+		HIP_TRY(hipGetLastError());
+		c->faces_written |= 1u << f;
+		return GCMX_OK;
+	};
+	if (D == 2 && step2d_faces_admissible(c, on)) {
+		// One 2-D pass: x faces in memory, y faces formed in the pass (Face2); a
+		// y face with PRESSURE (its trace needs components the pass does not form
+		// at ghosts) keeps the per-stage path.
+		Face2 f2{};
+		bool ok = true;
+		for (int f = 2; f < 4 && ok; f++) {
+			if (!((on >> f) & 1u)) continue;
+			f2.on |= 1u << (f - 2);
+			for (int k = 0; k < bq[f].n; k++) {
+				const int comp = quantity_comp(D, bq[f].q[k]);
+				if (comp < 0) {
+					ok = false;
+					break;
+				}
+				f2.mask[f - 2] |= 1u << comp;
+				f2.two_v[f - 2][comp] = 2 * bq[f].v[k];  // the last setting of a component wins
+			}
+		}
+		if (ok) {
+			for (int f = 0; f < 2; f++)
+				if ((on >> f) & 1u) {
+					s = fill(f);
+					if (s) return s;
+				}
+			s = step2d(c, &f2);
+			if (s) return s;
+			return ode.on ? ode_apply(c, ode.f) : GCMX_OK;
+		}
+	}
 	// One pass: x faces in memory, y/z faces as FaceBC; the y/z faces must be
 	// free of PRESSURE (its trace needs components the fused ghosts do not form)
 	// and no face may hold ghosts written earlier but not refreshed now.
@@ -1561,15 +1609,6 @@ gcmx_status step_faces_body(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 			fb.two_v[f - 2][comp] = 2 * bq[f].v[k];  // the last setting of a component wins
 		}
 	}
-	auto fill = [&](int f) -> gcmx_status {
-		s = halo_wait(c);
-		if (s) return s;
-		Timed t(c, "face_fill", 0.0, c->stream);
-		launch_face_fill(c->cur, c->geo, f / 2, (f & 1) ? 1 : -1, bq[f], c->stream);
-		HIP_TRY(hipGetLastError());
-		c->faces_written |= 1u << f;
-		return GCMX_OK;
-	};
 	if (fused) {
 		for (int f = 0; f < 2; f++)
 			if ((on >> f) & 1u) {

@@ -153,9 +153,17 @@ __device__ __forceinline__ void node_update2(const IsoAxis& A, WF W, CF C, doubl
 #ifndef GCMX_2D_PF  // rows the loads run ahead of the row computed
 #define GCMX_2D_PF 1
 #endif
-template <int BS, int T, bool KF0>
+//
+// FACES: border conditions on the y faces (Face2).  A lane whose column is a
+// ghost of a face with a condition loads the MIRRORED inner column (ghost -a <->
+// inner +a, BorderConditions.hpp:94-114) and forms that column's X stage itself
+// -- the same operations on the same data as the lane that owns it, so the same
+// bits -- then stores the ghost value (the mirrored X result, -inner + 2 f(t) in
+// the overridden components) in its LDS slot: the Y stage reads ghost columns
+// like any other, with no extra barrier and no divergent branch.
+template <int BS, int T, bool KF0, bool FACES>
 __global__ __launch_bounds__(T) void k_step2d_iso(const double* __restrict__ cur, double* __restrict__ nxt, Geo g,
-                                                  IsoAxis AX, IsoAxis AY, int chunk) {
+                                                  IsoAxis AX, IsoAxis AY, int chunk, Face2 fc) {
 	constexpr unsigned WMX = iso2_window(0), CMX = iso2_center_only(0);
 	constexpr unsigned WMY = iso2_window(1);
 	constexpr int NWX = popc9(WMX), NWY = popc9(WMY);
@@ -167,10 +175,16 @@ __global__ __launch_bounds__(T) void k_step2d_iso(const double* __restrict__ cur
 	const int y = (int)blockIdx.x * (T - 2 * BS) - BS + l;
 	const int xb = (int)blockIdx.y * chunk;
 	const int xe = min(xb + chunk, X);
-	const bool col = y >= 0 && y < Y;
-	const bool out = col && l >= BS && l < T - BS;
+	const bool inner = y >= 0 && y < Y;
+	const bool out = inner && l >= BS && l < T - BS;
+	// FACES: a ghost column of a face with a condition forms its mirror's X stage
+	const int face = y < 0 ? 0 : 1;
+	const bool ghost = FACES && !inner && y >= -BS && y < Y + BS && ((fc.on >> face) & 1u);
+	const int ysrc = inner ? y : ghost ? (y < 0 ? -y : 2 * (Y - 1) - y) : 0;
+	const bool col = inner || ghost;  // the lane loads a column and forms its X stage
 	const unsigned sx = (unsigned)g.stride[0];
-	const unsigned off = (unsigned)(g.origin + (col ? y : 0));  // + x * sx: node (x, y)
+	const unsigned off = (unsigned)(g.origin + ysrc);  // + x * sx: node (x, ysrc)
+	const unsigned fmask = ghost ? fc.mask[face] : 0u;
 	const Planes src(cur, g.cs);
 	const PlanesW dst(nxt, g.cs);
 
@@ -207,7 +221,12 @@ __global__ __launch_bounds__(T) void k_step2d_iso(const double* __restrict__ cur
 		double (*buf)[T] = lds[x & 1];
 #pragma unroll
 		for (int c = 0; c < 5; c++)
-			if ((WMY >> c) & 1u) buf[wslot(WMY, c)][l] = col ? xo[c] : 0.0;  // ghost columns: 0
+			if ((WMY >> c) & 1u) {
+				double v = col ? xo[c] : 0.0;  // ghost columns without a condition: 0
+				if constexpr (FACES)
+					if ((fmask >> c) & 1u) v = -v + fc.two_v[face][c];
+				buf[wslot(WMY, c)][l] = v;
+			}
 		__syncthreads();
 		if (out) {
 			double yo[5];
@@ -403,9 +422,16 @@ static int step2d_chunk(int X, int ny) {
 	return chunk;
 }
 
+template <int BS, int T, bool KF0, bool FACES>
+static const char* step2d_iso_name() {
+	static const std::string s = "k_step2d_iso<" + std::to_string(BS) + ", " + std::to_string(T) + ", " +
+	                             (KF0 ? "KF0" : "!KF0") + (FACES ? ", FACES" : "") + ">";
+	return s.c_str();
+}
+
 template <int BS, int T>
 static void launch_step2d_t(const double* cur, double* nxt, const Geo& g, const AxisTable* tabs,
-                            const IsoAxis* iso, hipStream_t st, const char** kname) {
+                            const IsoAxis* iso, hipStream_t st, const char** kname, const Face2* faces) {
 	const int X = g.sizes[0], Y = g.sizes[1];
 	const int ny = (Y + (T - 2 * BS) - 1) / (T - 2 * BS);
 	const int chunk = step2d_chunk(X, ny);
@@ -413,13 +439,18 @@ static void launch_step2d_t(const double* cur, double* nxt, const Geo& g, const 
 	if constexpr (BS <= 3) {
 		if (iso) {
 			const bool kf0 = iso[0].kf1 == 0 && iso[0].kf2 == 0 && iso[1].kf1 == 0 && iso[1].kf2 == 0;
-			if (kf0)
-				hipLaunchKernelGGL((k_step2d_iso<BS, T, true>), grid, dim3(T), 0, st, cur, nxt, g, iso[0], iso[1], chunk);
-			else
-				hipLaunchKernelGGL((k_step2d_iso<BS, T, false>), grid, dim3(T), 0, st, cur, nxt, g, iso[0], iso[1], chunk);
-			static const std::string n0 = "k_step2d_iso<" + std::to_string(BS) + ", " + std::to_string(T) + ", KF0>";
-			static const std::string n1 = "k_step2d_iso<" + std::to_string(BS) + ", " + std::to_string(T) + ", !KF0>";
-			if (kname) *kname = kf0 ? n0.c_str() : n1.c_str();
+			const Face2 none{};
+			auto go = [&](auto K, const char* name) {
+				hipLaunchKernelGGL(K, grid, dim3(T), 0, st, cur, nxt, g, iso[0], iso[1], chunk, faces ? *faces : none);
+				if (kname) *kname = name;
+			};
+			if (faces && faces->on) {
+				if (kf0) go(k_step2d_iso<BS, T, true, true>, step2d_iso_name<BS, T, true, true>());
+				else go(k_step2d_iso<BS, T, false, true>, step2d_iso_name<BS, T, false, true>());
+			} else {
+				if (kf0) go(k_step2d_iso<BS, T, true, false>, step2d_iso_name<BS, T, true, false>());
+				else go(k_step2d_iso<BS, T, false, false>, step2d_iso_name<BS, T, false, false>());
+			}
 			return;
 		}
 	}
@@ -430,11 +461,11 @@ static void launch_step2d_t(const double* cur, double* nxt, const Geo& g, const 
 
 template <int BS>
 static void launch_step2d_bs(const double* cur, double* nxt, const Geo& g, const AxisTable* tabs,
-                             const IsoAxis* iso, hipStream_t st, const char** kname) {
+                             const IsoAxis* iso, hipStream_t st, const char** kname, const Face2* faces) {
 	if (g.sizes[1] + 2 * BS <= 64)
-		launch_step2d_t<BS, 64>(cur, nxt, g, tabs, iso, st, kname);
+		launch_step2d_t<BS, 64>(cur, nxt, g, tabs, iso, st, kname, faces);
 	else
-		launch_step2d_t<BS, 256>(cur, nxt, g, tabs, iso, st, kname);
+		launch_step2d_t<BS, 256>(cur, nxt, g, tabs, iso, st, kname, faces);
 }
 
 bool step2d_supported(const Geo& g) {
@@ -446,15 +477,16 @@ bool step2d_iso_supported(const Geo& g) {
 }
 
 bool launch_step2d(const double* cur, double* nxt, const Geo& g, const AxisTable* tabs, const IsoAxis* iso,
-                   hipStream_t st, const char** kname) {
+                   hipStream_t st, const char** kname, const Face2* faces) {
 	if (!step2d_supported(g)) return false;
 	if (iso && !step2d_iso_supported(g)) iso = nullptr;
+	if (faces && faces->on && (!iso || g.sizes[1] < g.bs + 1)) return false;  // y faces: isotropic kernel only
 	switch (g.bs) {
-	case 1: launch_step2d_bs<1>(cur, nxt, g, tabs, iso, st, kname); return true;
-	case 2: launch_step2d_bs<2>(cur, nxt, g, tabs, iso, st, kname); return true;
-	case 3: launch_step2d_bs<3>(cur, nxt, g, tabs, iso, st, kname); return true;
-	case 4: launch_step2d_bs<4>(cur, nxt, g, tabs, iso, st, kname); return true;
-	case 5: launch_step2d_bs<5>(cur, nxt, g, tabs, iso, st, kname); return true;
+	case 1: launch_step2d_bs<1>(cur, nxt, g, tabs, iso, st, kname, faces); return true;
+	case 2: launch_step2d_bs<2>(cur, nxt, g, tabs, iso, st, kname, faces); return true;
+	case 3: launch_step2d_bs<3>(cur, nxt, g, tabs, iso, st, kname, faces); return true;
+	case 4: launch_step2d_bs<4>(cur, nxt, g, tabs, iso, st, kname, faces); return true;
+	case 5: launch_step2d_bs<5>(cur, nxt, g, tabs, iso, st, kname, faces); return true;
 	default: return false;
 	}
 }

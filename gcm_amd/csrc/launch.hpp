@@ -80,8 +80,18 @@ constexpr int kStep2dMaxBs = 5;
 bool iso2_axis_extract(int s, const double* U, const double* U1, const double* L, IsoAxis& A);
 bool step2d_supported(const Geo& g);
 bool step2d_iso_supported(const Geo& g);
+// Cubic border conditions on the two y faces of the 2-D step (face f: 0 y-,
+// 1 y+), as the one pass forms them: the Y stage's ghost columns are the
+// mirrored X results with the components in mask[f] set to -inner + two_v[f][c]
+// (BorderConditions.hpp:94-114); the x faces are filled in memory before the
+// launch.  Isotropic kernel only; needs Y >= bs + 1.
+struct Face2 {
+	unsigned on;       // bit f: face f has a condition
+	unsigned mask[2];  // overridden components
+	double two_v[2][5];
+};
 bool launch_step2d(const double* cur, double* nxt, const Geo& g, const AxisTable* tabs, const IsoAxis* iso,
-                   hipStream_t st, const char** kname);
+                   hipStream_t st, const char** kname, const Face2* faces = nullptr);
 bool fast_layout_ok(const Geo& g);
 bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const IsoAxis& A,
                   int x0, int x1, hipStream_t st);

@@ -3,7 +3,8 @@
 # full GPU suite, smoke, the default bench line, bare and traced bench runs,
 # 256^3 (steady: 100 steps), the RCCL self-exchange lines (whole grid and the
 # N = 8 slab), the simplex lines, 512^3 physical runs, and rocprofv3 evidence
-# (trace + FETCH_SIZE + WRITE_SIZE) for profiles/pmc_traffic.json of this build.
+# (trace + FETCH_SIZE + WRITE_SIZE) for profiles/pmc_traffic.json of this build;
+# the 2-D step lines and a 1024^3 line.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/r5/${LEASE:-final}
@@ -25,6 +26,11 @@ timeout -k 10 300 python bench.py --rccl-self --steps 20 --reps 5 --no-cpu-basel
 timeout -k 10 300 python scripts/bench_slab.py --rccl-self --ranks 8 --no-check > $OUT/slab8_rccl_self.json 2> $OUT/slab8_rccl_self.err || exit 1
 tail -1 $OUT/slab8_rccl_self.json
 timeout -k 10 300 python scripts/bench_simplex.py --workloads cubetask,fracture --n 16 --steps 200 > $OUT/simplex16.jsonl 2> $OUT/simplex16.err || exit 1
+timeout -k 10 300 python scripts/bench_2d.py --steps 100 > $OUT/bench_2d.jsonl 2> $OUT/bench_2d.err || exit 1
+cat $OUT/bench_2d.jsonl
+# 1024^3 on one GPU (2 x 80 GB layers; Z = 1024: the one-plane k_fused_xyz)
+timeout -k 10 400 python bench.py --n 1024 --steps 5 --warmup 2 --reps 3 --no-cpu-baseline --no-copy-ceiling > $OUT/bench_1024.json 2> $OUT/bench_1024.err || exit 1
+python3 -c "import json;d=json.load(open('$OUT/bench_1024.json'));r=d['roofline'];print('1024',d['ms_per_step'],r['kernel_avg_ms'],r['frac'],r['kernel'])"
 for a in "free512:--n 512 --steps 10" "het512:--n 512 --steps 10 --layers" "hetmax512:--n 512 --steps 10 --layers --maxwell"; do
   n=${a%%:*}; args=${a#*:}
   timeout -k 10 300 python3 scripts/bench_physics.py $args > $OUT/phys_$n.json 2> $OUT/phys_$n.err || { echo "$n rc=$?"; exit 1; }

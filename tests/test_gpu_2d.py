@@ -8,6 +8,8 @@ so the result is IEEE-equal to two oracle stages.  The cases cover borderSize
 single column / row, grids narrower than one 64-lane block, and grids needing
 several 256-lane column blocks (whose halo columns each block forms itself).
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -151,4 +153,98 @@ def test_step2d_table_kernel_for_other_matrices(G, bs):
         else:
             ctx.step(tau)
         assert_same(ctx, b, f"table kernel bs={bs} step {step}")
+    ctx.close()
+
+
+# ------------------------------------------------------------- y/x faces --
+
+QCODE = {"Vx": 2, "Vy": 3, "Sxx": 5, "Sxy": 6, "Syy": 8, "PRESSURE": 12}
+FREE2 = {0: ("Sxx", "Sxy"), 1: ("Syy", "Sxy")}  # free surface of a 2-D face (ndi.hpp:30-55)
+
+
+def free2(axis, normal=lambda t: 0.0):
+    q = FREE2[axis]
+    return {q[0]: normal, q[1]: lambda t: 0.0}
+
+
+def face_body2(bs, sizes, conditions):
+    """conditions: (axis, side or 0 for both faces, {quantity: f(t)}), h = 1."""
+    from oracle import oracle as O
+    bcs = []
+    for axis, side, vals in conditions:
+        if side == 0:
+            area = ("infinite",)
+        else:
+            lo, hi = [-1e3] * 3, [1e3] * 3
+            c = 0.0 if side < 0 else float(sizes[axis] - 1)
+            lo[axis], hi[axis] = c - 0.5, c + 0.5
+            area = ("box", tuple(lo), tuple(hi))
+        bcs.append(O.BorderCondition(axis, area, vals))
+    t = O.Task(D=2, border_size=bs, h=[1.0, 1.0], cubics={0: (list(sizes), [0, 0])}, courant=0.9,
+               default_material=O.Material(4.0, 2.0, 1.0), number_of_snaps=1, border_conditions={0: bcs})
+    return O.Engine(t).bodies[0]
+
+
+def faces_at2(conditions, time):
+    from oracle import oracle as O
+    faces = [None] * 4
+    for axis, side, vals in conditions:
+        lst = sorted(vals.items(), key=lambda kv: O.QUANTITY_ORDER.index(kv[0]))
+        entry = [(QCODE[q], f(time)) for q, f in lst]
+        for s in ((0, 1) if side == 0 else ((0,) if side < 0 else (1,))):
+            faces[2 * axis + s] = entry
+    return faces
+
+
+FACE2_CASES = {
+    "free_all": (2, [30, 70], [(0, 0, free2(0)), (1, 0, free2(1))], 0.9, "fused"),
+    "some_faces": (2, [25, 40], [(1, 1, free2(1, lambda t: 0.3 * math.sin(2 * t))),
+                                 (0, -1, {"Vx": lambda t: 0.05})], 0.9, "fused"),
+    "override": (2, [12, 22], [(1, 0, free2(1)), (1, -1, {"Vy": lambda t: 0.1, "Sxy": lambda t: 0.0})],
+                 0.9, "fused"),
+    "bs1_narrow": (1, [9, 2], [(0, 0, free2(0)), (1, 0, free2(1))], 0.9, "fused"),
+    "bs3_courant25": (3, [14, 33], [(0, 0, free2(0)), (1, 0, free2(1, lambda t: -0.2))], 2.5, "fused"),
+    "column_blocks": (2, [10, 600], [(1, 0, free2(1)), (0, 1, free2(0))], 0.9, "fused"),
+    "pressure_y": (2, [8, 20], [(1, -1, {"PRESSURE": lambda t: 0.25}), (0, 0, free2(0))], 0.9, "generic"),
+    "pressure_x": (2, [8, 20], [(0, 1, {"PRESSURE": lambda t: 0.25}), (1, 0, free2(1))], 0.9, "fused"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FACE2_CASES))
+def test_step2d_faces_matches_oracle(G, name):
+    """gcmx_step_faces in 2-D: x faces filled in memory, the y faces' ghost
+    columns formed in the one pass from the mirrored columns; inner nodes equal
+    the reference's apply_border + stage sequence bitwise (the ghosts of the
+    intermediate layer exist only on the chip)."""
+    from tests.helpers import assert_same_inner
+    bs, sizes, conds, courant, path = FACE2_CASES[name]
+    b = face_body2(bs, sizes, conds)
+    random_state(b, seed=len(name) + sizes[1], ghosts=False)
+    ctx = context_for(b)
+    tau, t = courant, 0.0  # h = 1, c1 = 1
+    for step in range(3):
+        for s in range(2):
+            b.apply_border(s, t)
+            b.stage(s, tau)
+        ctx.step_faces(tau, faces_at2(conds, t))
+        assert ctx.last_path == path, f"{name}: ran {ctx.last_path}"
+        assert_same_inner(ctx, b, f"2-D faces {name} step {step}")
+        t += tau
+    ctx.close()
+
+
+def test_step2d_faces_kernel_and_plain_step_after(G):
+    """The faces step names its FACES instance; a plain gcmx_step after it (x face
+    ghosts written in memory, not refreshed) takes the per-stage path."""
+    conds = [(0, 0, free2(0)), (1, 0, free2(1))]
+    b = face_body2(2, [16, 300], conds)
+    random_state(b, seed=2, ghosts=False)
+    ctx = context_for(b)
+    ctx.profile(True)
+    ctx.profile_reset()
+    ctx.step_faces(0.9, faces_at2(conds, 0.0))
+    ctx.sync()
+    assert ctx.profile_read()["step2d"]["kernel"] == "k_step2d_iso<2, 256, KF0, FACES>"
+    ctx.profile(False)
+    assert ctx.effective_path == "generic"
     ctx.close()
