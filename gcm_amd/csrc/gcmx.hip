@@ -738,7 +738,7 @@ gcmx_status halo_ensure(gcmx_ctx* c) {
 // Fast kernels: 3-D, one material, no per-node ids, isotropic zero pattern.
 void refresh_fast(gcmx_ctx* c) {
 	const int D = c->D, M = c->M;
-	bool fits = (D == 3) && (c->mat_d == nullptr) && (c->n_mat == 1) && fast_layout_ok(c->geo);
+	bool fits = (D == 3) && (c->mat_d == nullptr) && (c->n_mat == 1) && onepass_layout_ok(c->geo);
 	for (int sx = 0; fits && sx < D; sx++)
 		fits = iso_axis_extract(sx, &c->U[(size_t)sx * M * M], &c->U1[(size_t)sx * M * M],
 		                        &c->L[(size_t)sx * M], c->iso[sx]);
@@ -751,7 +751,7 @@ void refresh_fast(gcmx_ctx* c) {
 	c->iso2_fast = fits2;
 	// heterogeneous one-pass step: per-node ids and every material of the structure
 	bool het = !fits && D == 3 && c->mat_d != nullptr && c->n_mat >= 1 && c->n_mat <= kHetMaxMaterials &&
-	           fast_layout_ok(c->geo) && het_supported(c->geo);
+	           onepass_layout_ok(c->geo) && het_supported(c->geo);
 	for (int m = 0; het && m < c->n_mat; m++)
 		for (int sx = 0; het && sx < D; sx++) {
 			IsoAxis tmp{};
@@ -789,8 +789,10 @@ gcmx_path effective_path(gcmx_ctx* c) {
 	if (c->D == 2) return step2d_admissible(c) ? GCMX_PATH_FUSED : GCMX_PATH_GENERIC;
 	if (c->D != 3 || !c->iso_fast || c->bs > 3) return GCMX_PATH_GENERIC;
 	if (c->path == GCMX_PATH_GENERIC) return GCMX_PATH_GENERIC;
-	if (c->path == GCMX_PATH_SPLIT) return GCMX_PATH_SPLIT;
-	if (c->ghosts_touched || !fused_supported(c->geo)) return GCMX_PATH_SPLIT;
+	// the per-stage kernels address whole layers with 32-bit offsets
+	const gcmx_path split = fast_layout_ok(c->geo) ? GCMX_PATH_SPLIT : GCMX_PATH_GENERIC;
+	if (c->path == GCMX_PATH_SPLIT) return split;
+	if (c->ghosts_touched || !fused_supported(c->geo)) return split;
 	return GCMX_PATH_FUSED;
 }
 
@@ -834,7 +836,8 @@ gcmx_status stage_impl(gcmx_ctx* c, int axis, double tau) {
 	const Geo& g = c->geo;
 	const double bytes = node_stage_bytes(c) * (double)g.n_inner;
 	// no per-stage het kernels; the per-stage kernels of the split path are 3-D only
-	const gcmx_path p = (c->iso_het || c->D != 3) ? GCMX_PATH_GENERIC : effective_path(c);
+	const gcmx_path p =
+	    (c->iso_het || c->D != 3 || !fast_layout_ok(c->geo)) ? GCMX_PATH_GENERIC : effective_path(c);
 	bool ok;
 	if (p == GCMX_PATH_GENERIC) {
 		Timed t(c, "stage_generic", bytes, c->stream);

@@ -262,8 +262,16 @@ bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& 
 	}
 }
 
+// The one-pass kernels address each block's planes from SGPR bases at its own
+// plane x: the 32-bit relative offsets cover the 2*bs+2 planes a block reads
+// (plus the origin's bs planes), not the whole layer -- grids of any size that
+// fits in HBM (1024^3: 9 GB per component plane).
+bool onepass_layout_ok(const Geo& g) {
+	return g.D == 3 && g.bs >= 1 && g.bs <= 3 && (long long)(3 * g.bs + 3) * g.stride[0] * 8 < (1LL << 31);
+}
+
 bool fused_supported(const Geo& g) {
-	return fast_layout_ok(g) && g.sizes[2] <= 1024 && g.sizes[2] >= 2 * g.bs;
+	return onepass_layout_ok(g) && g.sizes[2] <= 1024 && g.sizes[2] >= 2 * g.bs;
 }
 
 }  // namespace gcmx

@@ -102,10 +102,13 @@ __global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
 	const int zc = live ? z : Z - 1;  // idle lanes shadow a valid column
 	const unsigned stx = (unsigned)g.stride[0];
 	const unsigned sty = (unsigned)g.stride[1];
-	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
+	// Plane bases in SGPRs at this block's plane x, element offsets relative to
+	// them: 32-bit offsets whatever the layer's size (onepass_layout_ok)
+	const long long pbase = (long long)x * g.stride[0];
+	const unsigned plane = (unsigned)g.origin;  // node (x, 0, 0) from the bases
 	const unsigned base = plane + zc;
-	const Planes src(in, g.cs);
-	const PlanesW out_p(outl, g.cs);
+	const Planes src(in + pbase, g.cs);
+	const PlanesW out_p(outl + pbase, g.cs);
 
 	if (z < 2 * BS) {  // ghost slots of both LDS row buffers: zero, never overwritten
 		const int gslot = (z < BS) ? z : (Z + z);
@@ -460,14 +463,17 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const int zc = live ? z : Z - 1;
 	const unsigned stx = (unsigned)g.stride[0];
 	const unsigned sty = (unsigned)g.stride[1];
-	const unsigned plane = (unsigned)(g.origin + x * g.stride[0]);
+	// plane bases at this block's plane x (SGPRs), offsets relative to them:
+	// 32-bit whatever the layer's size (onepass_layout_ok)
+	const long long pbase = (long long)x * g.stride[0];
+	const unsigned plane = (unsigned)g.origin;  // node (x, 0, 0) from the bases
 	const unsigned zo = live ? (unsigned)z : (unsigned)Z;
 	// Memory accessors.  ldx(j, k, r): component j of plane x - BS + k (the last
 	// plane clamped when x + 1 is not ours), row r, this lane's column;
 	// stz(c, t, y, v): component c of node (x + t, y) of the output layer.
 #if GCMX_TX2_BUF
-	const Planes src(in, g.cs);
-	const PlanesW out_p(outl, g.cs);
+	const Planes src(in + pbase, g.cs);
+	const PlanesW out_p(outl + pbase, g.cs);
 	const unsigned lv = (unsigned)zc * 8u, sv = zo * 8u;  // per-lane byte offsets
 	const unsigned pxm = plane - (unsigned)BS * stx;      // plane x - BS, row 0, column 0
 	auto ldx = [&](int j, int k, int r) {
@@ -494,8 +500,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 #else
 	const unsigned base = plane + zc;
-	const Planes src(in, g.cs);
-	const PlanesW out_p(outl, g.cs);
+	const Planes src(in + pbase, g.cs);
+	const PlanesW out_p(outl + pbase, g.cs);
 	auto ldx = [&](int j, int k, int r) {
 		const int d = (k == WX - 1 && !two) ? BS : (k == 0 && !one) ? 1 - BS : k - BS;
 		return src.ld(j, base + (unsigned)r * sty + (unsigned)d * stx);

@@ -92,7 +92,8 @@ struct Face2 {
 };
 bool launch_step2d(const double* cur, double* nxt, const Geo& g, const AxisTable* tabs, const IsoAxis* iso,
                    hipStream_t st, const char** kname, const Face2* faces = nullptr);
-bool fast_layout_ok(const Geo& g);
+bool fast_layout_ok(const Geo& g);     // the per-stage kernels: layer planes < 2^32 bytes
+bool onepass_layout_ok(const Geo& g);  // the one-pass kernels: 32-bit offsets within a block's planes
 bool launch_march(const double* cur, double* nxt, const Geo& g, int s, const IsoAxis& A,
                   int x0, int x1, hipStream_t st);
 bool launch_line_z(const double* cur, double* nxt, const Geo& g, const IsoAxis& A, int x0,
