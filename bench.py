@@ -619,7 +619,7 @@ def main():
                               "alloc_order": (f"torch buffer {a.prealloc_gb} GiB, " if hold is not None else "")
                                              + ("layers A+gap+B in one allocation" if placement["one_allocation"]
                                                 else "layer A, layer B, tables"),
-                              "env": {k: os.environ[k] for k in ("GCMX_LAYER_GAP", "GCMX_STREAM_PRIO", "GCMX_FP")
+                              "env": {k: os.environ[k] for k in ("GCMX_LAYER_GAP", "GCMX_STREAM_PRIO", "GCMX_FP", "GCMX_ALLOC")
                                       if k in os.environ},
                               "under_profiler": bool(os.environ.get("ROCPROF_OUTPUT_PATH") or
                                                      "rocprof" in os.environ.get("LD_PRELOAD", ""))},
