@@ -172,7 +172,7 @@ def layer_placement(ctx) -> dict:
     a, b = li["a"], li["b"]
     mods = {"4K": 1 << 12, "64K": 1 << 16, "2M": 1 << 21, "1G": 1 << 30}
     return {"a": hex(a), "b": hex(b), "b_minus_a": b - a, "layer_bytes": li["layer_bytes"],
-            "one_allocation": li["one_allocation"],
+            "one_allocation": li["one_allocation"], "alloc": li.get("alloc"),
             "a_mod": {k: a % m for k, m in mods.items()},
             "b_mod": {k: b % m for k, m in mods.items()},
             "b_minus_a_mod": {k: (b - a) % m for k, m in mods.items()}}
@@ -617,8 +617,8 @@ def main():
                               # levels / power / temperatures sampled during the reps
                               "box": box, "box_during_reps": sampled,
                               "alloc_order": (f"torch buffer {a.prealloc_gb} GiB, " if hold is not None else "")
-                                             + ("layers A+gap+B in one allocation" if placement["one_allocation"]
-                                                else "layer A, layer B, tables"),
+                                             + (f"layers A+gap+B in one block ({placement['alloc']})"
+                                                if placement["one_allocation"] else "layer A, layer B, tables"),
                               "env": {k: os.environ[k] for k in ("GCMX_LAYER_GAP", "GCMX_STREAM_PRIO", "GCMX_FP", "GCMX_ALLOC")
                                       if k in os.environ},
                               "under_profiler": bool(os.environ.get("ROCPROF_OUTPUT_PATH") or

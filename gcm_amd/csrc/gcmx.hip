@@ -116,6 +116,13 @@ struct gcmx_ctx {
 	double* layer_a = nullptr;   // the two layers as allocated (cur / nxt swap every step)
 	double* layer_b = nullptr;
 	void* layers_block = nullptr;  // both layers in one allocation (GCMX_LAYER_GAP), else null
+	// layers_block mapped from physical chunks in shuffled order (vmm_map): the
+	// reserved range, its size and the chunks' handles (empty: hipMalloc'd)
+	size_t vmm_bytes = 0;
+	std::vector<hipMemGenericAllocationHandle_t> vmm_chunks;
+	// gcmx_layer_info out[3]: 0 two allocations, 1 one hipMalloc'd block, 2 one
+	// physically contiguous block, else the shuffled mapping's chunk bytes
+	uint64_t alloc_kind = 0;
 	// clock sampler (gcmx_clock_probe_*): its own stream and sample buffer
 	hipStream_t probe_stream = nullptr;
 	unsigned long long* probe_d = nullptr;
@@ -884,6 +891,74 @@ const char* gcmx_status_string(gcmx_status s) {
 	return "unknown";
 }
 
+// Default chunk of the shuffled mapping: 512^3 runs alike from 64 MiB to 1 GiB
+// chunks (3.64-3.66 ms), 256^3 best at 256 MiB (0.508 ms; 64 MiB 0.518), 32 MiB
+// and below lose (2 MiB: 4.80 ms) -- profiles/r5/r, profiles/r5/s.
+constexpr long long kShuffleChunkMiB = 256;
+
+// The layers' block as physical chunks of `chunk` bytes mapped into one
+// virtual range in a shuffled order (HIP virtual memory management): whatever
+// the physical free space looks like, consecutive virtual chunks land in
+// unrelated physical places.  A large hipMalloc on a box whose VRAM is one free
+// region comes back physically contiguous, and then the one-pass step's
+// concurrent streams (9 components x 2*bs+2 planes x every CU's block) meet the
+// HBM in a regular pattern: 512^3 4.14-4.17 ms from a contiguous block, 3.88-3.91
+// where hipMalloc happened to scatter it, 3.58-3.65 ms from shuffled 64 MiB - 1 GiB
+// chunks.  Returns false (nothing held) on failure.
+static bool vmm_map(gcmx_ctx* c, size_t bytes, size_t chunk_req) {
+	hipMemAllocationProp prop{};
+	prop.type = hipMemAllocationTypePinned;
+	prop.location.type = hipMemLocationTypeDevice;
+	prop.location.id = c->device;
+	size_t gran = 0;
+	if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || gran == 0)
+		return false;
+	const size_t chunk = (chunk_req + gran - 1) / gran * gran;
+	const size_t n = (bytes + chunk - 1) / chunk, total = n * chunk;
+	void* va = nullptr;
+	if (hipMemAddressReserve(&va, total, chunk, nullptr, 0) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	std::vector<hipMemGenericAllocationHandle_t> h;
+	h.reserve(n);
+	bool ok = true;
+	for (size_t i = 0; i < n && ok; i++) {
+		hipMemGenericAllocationHandle_t x{};
+		ok = hipMemCreate(&x, chunk, &prop, 0) == hipSuccess;
+		if (ok) h.push_back(x);
+	}
+	// a fixed pseudo-random permutation (Fisher-Yates over a 64-bit LCG)
+	std::vector<size_t> perm(h.size());
+	for (size_t i = 0; i < perm.size(); i++) perm[i] = i;
+	unsigned long long st = 0x9E3779B97F4A7C15ULL;
+	for (size_t i = perm.size(); i > 1; i--) {
+		st = st * 6364136223846793005ULL + 1442695040888963407ULL;
+		std::swap(perm[i - 1], perm[(size_t)((st >> 33) % i)]);
+	}
+	size_t mapped = 0;
+	for (size_t i = 0; i < h.size() && ok; i++, mapped++)
+		ok = hipMemMap(static_cast<char*>(va) + i * chunk, chunk, 0, h[perm[i]], 0) == hipSuccess;
+	if (ok) {
+		hipMemAccessDesc acc{};
+		acc.location = prop.location;
+		acc.flags = hipMemAccessFlagsProtReadWrite;
+		ok = hipMemSetAccess(va, total, &acc, 1) == hipSuccess;
+	}
+	if (!ok) {
+		(void)hipGetLastError();
+		for (size_t i = 0; i < mapped; i++) (void)hipMemUnmap(static_cast<char*>(va) + i * chunk, chunk);
+		for (auto x : h) (void)hipMemRelease(x);
+		(void)hipMemAddressFree(va, total);
+		(void)hipGetLastError();
+		return false;
+	}
+	c->layers_block = va;
+	c->vmm_bytes = total;
+	c->vmm_chunks = std::move(h);
+	return true;
+}
+
 gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 	if (!d || !out) return fail(GCMX_ERR_INVALID_ARG, "null argument");
 	*out = nullptr;
@@ -958,9 +1033,43 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 		const long long v = std::atoll(e);
 		gap = v < 0 ? -1 : round_up(v, 256);
 	}
+	// Placement of the layers' block in physical memory (measured):
+	// by default physical chunks of kShuffleChunkMiB mapped in a shuffled order
+	// (vmm_map) once the block spans two chunks; GCMX_ALLOC=malloc (one
+	// hipMalloc), =contiguous (hipDeviceMallocContiguous) or =shuffle:<MiB>
+	// chooses explicitly.  Any failure falls back to hipMalloc.
+	static const long long shuffle_mb = [] {
+		const char* e = std::getenv("GCMX_ALLOC");
+		if (!e || !*e) return kShuffleChunkMiB;
+		if (std::strncmp(e, "shuffle:", 8) == 0) return std::max(1LL, std::atoll(e + 8));
+		return 0LL;
+	}();
+	static const bool alloc_contig = [] {
+		const char* e = std::getenv("GCMX_ALLOC");
+		return e && std::strcmp(e, "contiguous") == 0;
+	}();
 	bool alloc_ok;
 	if (gap >= 0) {
-		alloc_ok = hipMalloc(&c->layers_block, 2 * bytes + (size_t)gap) == hipSuccess;
+		const size_t block = 2 * bytes + (size_t)gap;
+		alloc_ok = false;
+		if (shuffle_mb > 0 && block >= 2 * ((size_t)shuffle_mb << 20)) {
+			alloc_ok = vmm_map(c, block, (size_t)shuffle_mb << 20);
+			if (alloc_ok) c->alloc_kind = c->vmm_bytes / c->vmm_chunks.size();
+			else std::fprintf(stderr, "gcmx: shuffled chunk mapping failed, using hipMalloc\n");
+		}
+		if (!alloc_ok && alloc_contig) {
+			alloc_ok = hipExtMallocWithFlags(&c->layers_block, block, hipDeviceMallocContiguous) == hipSuccess;
+			if (alloc_ok) {
+				c->alloc_kind = 2;
+			} else {
+				(void)hipGetLastError();
+				std::fprintf(stderr, "gcmx: contiguous allocation of %zu bytes failed, using hipMalloc\n", block);
+			}
+		}
+		if (!alloc_ok) {
+			alloc_ok = hipMalloc(&c->layers_block, block) == hipSuccess;
+			c->alloc_kind = 1;
+		}
 		if (alloc_ok) {
 			c->cur = static_cast<double*>(c->layers_block);
 			c->nxt = reinterpret_cast<double*>(static_cast<char*>(c->layers_block) + bytes + (size_t)gap);
@@ -1043,7 +1152,13 @@ void gcmx_destroy(gcmx_ctx* c) {
 						(void)hipEventSynchronize(L.done[t][sd][pr]);
 		L.ctx[c->lrank] = nullptr;
 	}
-	if (c->layers_block) {
+	if (c->layers_block && c->vmm_bytes) {
+		const size_t chunk = c->vmm_bytes / c->vmm_chunks.size();
+		for (size_t i = 0; i < c->vmm_chunks.size(); i++)
+			(void)hipMemUnmap(static_cast<char*>(c->layers_block) + i * chunk, chunk);
+		for (auto x : c->vmm_chunks) (void)hipMemRelease(x);
+		(void)hipMemAddressFree(c->layers_block, c->vmm_bytes);
+	} else if (c->layers_block) {
 		(void)hipFree(c->layers_block);
 	} else {
 		(void)hipFree(c->layer_a);
@@ -2456,7 +2571,7 @@ gcmx_status gcmx_layer_info(gcmx_ctx* c, uint64_t out[4]) {
 	out[0] = (uint64_t)(uintptr_t)c->layer_a;
 	out[1] = (uint64_t)(uintptr_t)c->layer_b;
 	out[2] = (uint64_t)(c->layer_elems * sizeof(double));
-	out[3] = c->layers_block ? 1 : 0;
+	out[3] = c->alloc_kind;
 	return GCMX_OK;
 }
 

@@ -440,8 +440,11 @@ class Context:
         """gcmx_layer_info: the two time layers' device addresses (measurement)."""
         out = (ctypes.c_uint64 * 4)()
         _check(lib().gcmx_layer_info(self._ptr, out))
+        k = int(out[3])
+        alloc = {0: "two hipMalloc", 1: "one hipMalloc", 2: "one contiguous block"}.get(
+            k, f"shuffled {k >> 20} MiB chunks")
         return {"a": int(out[0]), "b": int(out[1]), "layer_bytes": int(out[2]),
-                "one_allocation": bool(out[3])}
+                "one_allocation": k != 0, "alloc": alloc}
 
     def clock_probe_start(self, seconds: float, period_us: float = 200.0):
         """gcmx_clock_probe_start: one co-resident wave samples the shader clock."""

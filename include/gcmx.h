@@ -552,9 +552,13 @@ size_t      gcmx_device_bytes(gcmx_ctx* ctx);
 gcmx_status gcmx_copy_ceiling(gcmx_ctx* ctx, size_t bytes, int reps, float* ms_out);
 /* Measurement only: out[0], out[1] = device addresses of the two time layers as
  * allocated (layer A holds the state after an even number of steps), out[2] =
- * bytes per layer, out[3] = 1 when both live in one allocation (the default:
- * layer A, a 2 MiB gap, layer B; environment GCMX_LAYER_GAP = bytes of the gap
- * at gcmx_create, < 0 = two separate allocations), else 0. */
+ * bytes per layer, out[3] = how they are allocated: both live in one block
+ * (the default: layer A, a 2 MiB gap, layer B; environment GCMX_LAYER_GAP =
+ * bytes of the gap at gcmx_create, < 0 = two separate allocations: out[3] = 0)
+ * which is, by default once it spans two 256 MiB chunks, physical chunks mapped
+ * in a shuffled order (out[3] = the chunk bytes); GCMX_ALLOC=malloc gives one
+ * hipMalloc (1), =contiguous a physically contiguous block (2), =shuffle:<MiB>
+ * another chunk size.  DESIGN.md §2 has the measurements. */
 gcmx_status gcmx_layer_info(gcmx_ctx* ctx, uint64_t out[4]);
 /* Measurement only: the shader clock under load.  _start launches ONE wave on
  * a stream of its own that records (s_memrealtime, s_memtime) pairs every
