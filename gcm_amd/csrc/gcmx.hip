@@ -891,10 +891,12 @@ const char* gcmx_status_string(gcmx_status s) {
 	return "unknown";
 }
 
-// Default chunk of the shuffled mapping: 512^3 runs alike from 64 MiB to 1 GiB
-// chunks (3.64-3.66 ms), 256^3 best at 256 MiB (0.508 ms; 64 MiB 0.518), 32 MiB
-// and below lose (2 MiB: 4.80 ms) -- profiles/r5/r, profiles/r5/s.
-constexpr long long kShuffleChunkMiB = 256;
+// Default chunk of the shuffled mapping (profiles/r5/r, s, t, u): 512^3 runs
+// alike from 64 MiB to 1 GiB chunks (3.64-3.66 ms), 32 MiB and below lose
+// (2 MiB: 4.80 ms); the 2-D 8192^2 block (5.4 GB) gains with 64 MiB chunks
+// (1.11 against 1.27 ms) and not with 256 MiB ones; 256^3 and the N = 8 slab
+// are alike with either.  256 MiB chunks for blocks of 8 GiB and more, 64 MiB below.
+static long long shuffle_chunk_mib(size_t block) { return block >= (8ULL << 30) ? 256 : 64; }
 
 // The layers' block as physical chunks of `chunk` bytes mapped into one
 // virtual range in a shuffled order (HIP virtual memory management): whatever
@@ -1034,13 +1036,13 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 		gap = v < 0 ? -1 : round_up(v, 256);
 	}
 	// Placement of the layers' block in physical memory (measured):
-	// by default physical chunks of kShuffleChunkMiB mapped in a shuffled order
+	// by default physical chunks (shuffle_chunk_mib) mapped in a shuffled order
 	// (vmm_map) once the block spans two chunks; GCMX_ALLOC=malloc (one
 	// hipMalloc), =contiguous (hipDeviceMallocContiguous) or =shuffle:<MiB>
 	// chooses explicitly.  Any failure falls back to hipMalloc.
-	static const long long shuffle_mb = [] {
+	static const long long shuffle_env = [] {  // -1: the default rule, 0: no shuffling
 		const char* e = std::getenv("GCMX_ALLOC");
-		if (!e || !*e) return kShuffleChunkMiB;
+		if (!e || !*e) return -1LL;
 		if (std::strncmp(e, "shuffle:", 8) == 0) return std::max(1LL, std::atoll(e + 8));
 		return 0LL;
 	}();
@@ -1051,6 +1053,7 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 	bool alloc_ok;
 	if (gap >= 0) {
 		const size_t block = 2 * bytes + (size_t)gap;
+		const long long shuffle_mb = shuffle_env < 0 ? shuffle_chunk_mib(block) : shuffle_env;
 		alloc_ok = false;
 		if (shuffle_mb > 0 && block >= 2 * ((size_t)shuffle_mb << 20)) {
 			alloc_ok = vmm_map(c, block, (size_t)shuffle_mb << 20);

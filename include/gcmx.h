@@ -555,8 +555,9 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* ctx, size_t bytes, int reps, float* ms_o
  * bytes per layer, out[3] = how they are allocated: both live in one block
  * (the default: layer A, a 2 MiB gap, layer B; environment GCMX_LAYER_GAP =
  * bytes of the gap at gcmx_create, < 0 = two separate allocations: out[3] = 0)
- * which is, by default once it spans two 256 MiB chunks, physical chunks mapped
- * in a shuffled order (out[3] = the chunk bytes); GCMX_ALLOC=malloc gives one
+ * which is, by default once it spans two chunks (256 MiB from an 8 GiB block
+ * up, else 64 MiB), physical chunks mapped in a shuffled order (out[3] = the
+ * chunk bytes); GCMX_ALLOC=malloc gives one
  * hipMalloc (1), =contiguous a physically contiguous block (2), =shuffle:<MiB>
  * another chunk size.  DESIGN.md §2 has the measurements. */
 gcmx_status gcmx_layer_info(gcmx_ctx* ctx, uint64_t out[4]);
