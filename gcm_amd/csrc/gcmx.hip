@@ -942,10 +942,29 @@ static bool vmm_map(gcmx_ctx* c, size_t bytes, size_t chunk_req) {
 	for (size_t i = 0; i < h.size() && ok; i++, mapped++)
 		ok = hipMemMap(static_cast<char*>(va) + i * chunk, chunk, 0, h[perm[i]], 0) == hipSuccess;
 	if (ok) {
-		hipMemAccessDesc acc{};
-		acc.location = prop.location;
-		acc.flags = hipMemAccessFlagsProtReadWrite;
-		ok = hipMemSetAccess(va, total, &acc, 1) == hipSuccess;
+		// read-write for this device and every peer that can reach it (the
+		// in-process X-slab group copies between devices, gcmx_halo_exchange_group)
+		std::vector<hipMemAccessDesc> acc;
+		int ndev = 0;
+		if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+		for (int dv = 0; dv < ndev; dv++) {
+			int can = dv == c->device;
+			if (!can && hipDeviceCanAccessPeer(&can, dv, c->device) != hipSuccess) can = 0;
+			if (!can) continue;
+			hipMemAccessDesc a{};
+			a.location.type = hipMemLocationTypeDevice;
+			a.location.id = dv;
+			a.flags = hipMemAccessFlagsProtReadWrite;
+			acc.push_back(a);
+		}
+		ok = !acc.empty() && hipMemSetAccess(va, total, acc.data(), acc.size()) == hipSuccess;
+		if (!ok && acc.size() > 1) {  // peers refused: this device alone
+			(void)hipGetLastError();
+			hipMemAccessDesc a{};
+			a.location = prop.location;
+			a.flags = hipMemAccessFlagsProtReadWrite;
+			ok = hipMemSetAccess(va, total, &a, 1) == hipSuccess;
+		}
 	}
 	if (!ok) {
 		(void)hipGetLastError();
