@@ -97,6 +97,14 @@ struct LocalComm {
 	}
 };
 
+// A virtual range backed by physical chunks (vmm_map): its base, size and the
+// chunks' handles in mapping order (empty: not in use).
+struct VmmBlock {
+	void* va = nullptr;
+	size_t bytes = 0;
+	std::vector<hipMemGenericAllocationHandle_t> chunks;
+};
+
 struct gcmx_ctx {
 	int device = 0;
 	hipStream_t stream = nullptr;
@@ -116,10 +124,9 @@ struct gcmx_ctx {
 	double* layer_a = nullptr;   // the two layers as allocated (cur / nxt swap every step)
 	double* layer_b = nullptr;
 	void* layers_block = nullptr;  // both layers in one allocation (GCMX_LAYER_GAP), else null
-	// layers_block mapped from physical chunks in shuffled order (vmm_map): the
-	// reserved range, its size and the chunks' handles (empty: hipMalloc'd)
-	size_t vmm_bytes = 0;
-	std::vector<hipMemGenericAllocationHandle_t> vmm_chunks;
+	// layers_block mapped from physical chunks in shuffled order (vmm_map); empty
+	// when hipMalloc'd
+	VmmBlock vmm;
 	// gcmx_layer_info out[3]: 0 two allocations, 1 one hipMalloc'd block, 2 one
 	// physically contiguous block, else the shuffled mapping's chunk bytes
 	uint64_t alloc_kind = 0;
@@ -907,11 +914,11 @@ static long long shuffle_chunk_mib(size_t block) { return block >= (8ULL << 30) 
 // HBM in a regular pattern: 512^3 4.14-4.17 ms from a contiguous block, 3.88-3.91
 // where hipMalloc happened to scatter it, 3.58-3.65 ms from shuffled 64 MiB - 1 GiB
 // chunks.  Returns false (nothing held) on failure.
-static bool vmm_map(gcmx_ctx* c, size_t bytes, size_t chunk_req) {
+static bool vmm_map(int device, size_t bytes, size_t chunk_req, VmmBlock& out) {
 	hipMemAllocationProp prop{};
 	prop.type = hipMemAllocationTypePinned;
 	prop.location.type = hipMemLocationTypeDevice;
-	prop.location.id = c->device;
+	prop.location.id = device;
 	size_t gran = 0;
 	if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || gran == 0)
 		return false;
@@ -948,8 +955,8 @@ static bool vmm_map(gcmx_ctx* c, size_t bytes, size_t chunk_req) {
 		int ndev = 0;
 		if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
 		for (int dv = 0; dv < ndev; dv++) {
-			int can = dv == c->device;
-			if (!can && hipDeviceCanAccessPeer(&can, dv, c->device) != hipSuccess) can = 0;
+			int can = dv == device;
+			if (!can && hipDeviceCanAccessPeer(&can, dv, device) != hipSuccess) can = 0;
 			if (!can) continue;
 			hipMemAccessDesc a{};
 			a.location.type = hipMemLocationTypeDevice;
@@ -974,10 +981,38 @@ static bool vmm_map(gcmx_ctx* c, size_t bytes, size_t chunk_req) {
 		(void)hipGetLastError();
 		return false;
 	}
-	c->layers_block = va;
-	c->vmm_bytes = total;
-	c->vmm_chunks = std::move(h);
+	out.va = va;
+	out.bytes = total;
+	out.chunks = std::move(h);
 	return true;
+}
+
+static void vmm_free(VmmBlock& b) {
+	if (!b.va) return;
+	const size_t chunk = b.bytes / b.chunks.size();
+	for (size_t i = 0; i < b.chunks.size(); i++) (void)hipMemUnmap(static_cast<char*>(b.va) + i * chunk, chunk);
+	for (auto x : b.chunks) (void)hipMemRelease(x);
+	(void)hipMemAddressFree(b.va, b.bytes);
+	b = VmmBlock{};
+}
+
+// The allocation policy of large device blocks (the layers, the copy-ceiling
+// buffers): the shuffled mapping's chunk in MiB for a block of `block` bytes,
+// 0 for none; `contig`: GCMX_ALLOC=contiguous.
+static long long shuffle_policy_mib(size_t block, bool* contig) {
+	static const long long env = [] {  // -1: the default rule, 0: no shuffling
+		const char* e = std::getenv("GCMX_ALLOC");
+		if (!e || !*e) return -1LL;
+		if (std::strncmp(e, "shuffle:", 8) == 0) return std::max(1LL, std::atoll(e + 8));
+		return 0LL;
+	}();
+	static const bool cont = [] {
+		const char* e = std::getenv("GCMX_ALLOC");
+		return e && std::strcmp(e, "contiguous") == 0;
+	}();
+	if (contig) *contig = cont;
+	const long long mib = env < 0 ? shuffle_chunk_mib(block) : env;
+	return (mib > 0 && block >= 2 * ((size_t)mib << 20)) ? mib : 0;
 }
 
 gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
@@ -1059,25 +1094,20 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 	// (vmm_map) once the block spans two chunks; GCMX_ALLOC=malloc (one
 	// hipMalloc), =contiguous (hipDeviceMallocContiguous) or =shuffle:<MiB>
 	// chooses explicitly.  Any failure falls back to hipMalloc.
-	static const long long shuffle_env = [] {  // -1: the default rule, 0: no shuffling
-		const char* e = std::getenv("GCMX_ALLOC");
-		if (!e || !*e) return -1LL;
-		if (std::strncmp(e, "shuffle:", 8) == 0) return std::max(1LL, std::atoll(e + 8));
-		return 0LL;
-	}();
-	static const bool alloc_contig = [] {
-		const char* e = std::getenv("GCMX_ALLOC");
-		return e && std::strcmp(e, "contiguous") == 0;
-	}();
 	bool alloc_ok;
 	if (gap >= 0) {
 		const size_t block = 2 * bytes + (size_t)gap;
-		const long long shuffle_mb = shuffle_env < 0 ? shuffle_chunk_mib(block) : shuffle_env;
+		bool alloc_contig = false;
+		const long long shuffle_mb = shuffle_policy_mib(block, &alloc_contig);
 		alloc_ok = false;
-		if (shuffle_mb > 0 && block >= 2 * ((size_t)shuffle_mb << 20)) {
-			alloc_ok = vmm_map(c, block, (size_t)shuffle_mb << 20);
-			if (alloc_ok) c->alloc_kind = c->vmm_bytes / c->vmm_chunks.size();
-			else std::fprintf(stderr, "gcmx: shuffled chunk mapping failed, using hipMalloc\n");
+		if (shuffle_mb > 0) {
+			alloc_ok = vmm_map(c->device, block, (size_t)shuffle_mb << 20, c->vmm);
+			if (alloc_ok) {
+				c->layers_block = c->vmm.va;
+				c->alloc_kind = c->vmm.bytes / c->vmm.chunks.size();
+			} else {
+				std::fprintf(stderr, "gcmx: shuffled chunk mapping failed, using hipMalloc\n");
+			}
 		}
 		if (!alloc_ok && alloc_contig) {
 			alloc_ok = hipExtMallocWithFlags(&c->layers_block, block, hipDeviceMallocContiguous) == hipSuccess;
@@ -1174,12 +1204,8 @@ void gcmx_destroy(gcmx_ctx* c) {
 						(void)hipEventSynchronize(L.done[t][sd][pr]);
 		L.ctx[c->lrank] = nullptr;
 	}
-	if (c->layers_block && c->vmm_bytes) {
-		const size_t chunk = c->vmm_bytes / c->vmm_chunks.size();
-		for (size_t i = 0; i < c->vmm_chunks.size(); i++)
-			(void)hipMemUnmap(static_cast<char*>(c->layers_block) + i * chunk, chunk);
-		for (auto x : c->vmm_chunks) (void)hipMemRelease(x);
-		(void)hipMemAddressFree(c->layers_block, c->vmm_bytes);
+	if (c->vmm.va) {
+		vmm_free(c->vmm);
 	} else if (c->layers_block) {
 		(void)hipFree(c->layers_block);
 	} else {
@@ -2554,7 +2580,13 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 	if (!ms_out || reps < 1 || bytes < 64) return fail(GCMX_ERR_INVALID_ARG, "bad copy-ceiling arguments");
 	const size_t half = bytes / 2 / 16 * 16;
 	void *a = nullptr, *b = nullptr;
-	if (hipMalloc(&a, half) != hipSuccess || hipMalloc(&b, half) != hipSuccess) {
+	// the buffers placed as the layers are (shuffle_policy_mib): one block, a | b
+	VmmBlock vb;
+	const long long mib = shuffle_policy_mib(2 * half, nullptr);
+	if (mib > 0 && vmm_map(c->device, 2 * half, (size_t)mib << 20, vb)) {
+		a = vb.va;
+		b = static_cast<char*>(vb.va) + half;
+	} else if (hipMalloc(&a, half) != hipSuccess || hipMalloc(&b, half) != hipSuccess) {
 		if (a) (void)hipFree(a);
 		return fail(GCMX_ERR_OOM, "copy-ceiling buffers");
 	}
@@ -2580,8 +2612,12 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 	}
 	if (e0) (void)hipEventDestroy(e0);
 	if (e1) (void)hipEventDestroy(e1);
-	(void)hipFree(a);
-	(void)hipFree(b);
+	if (vb.va) {
+		vmm_free(vb);
+	} else {
+		(void)hipFree(a);
+		(void)hipFree(b);
+	}
 	if (st) return st;
 	std::sort(ms.begin(), ms.end());
 	*ms_out = ms[ms.size() / 2] * (float)((double)bytes / (double)(2 * half));  // per `bytes`
