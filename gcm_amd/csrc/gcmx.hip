@@ -945,9 +945,11 @@ static bool vmm_map(int device, size_t bytes, size_t chunk_req, VmmBlock& out) {
 		st = st * 6364136223846793005ULL + 1442695040888963407ULL;
 		std::swap(perm[i - 1], perm[(size_t)((st >> 33) % i)]);
 	}
-	size_t mapped = 0;
-	for (size_t i = 0; i < h.size() && ok; i++, mapped++)
+	size_t mapped = 0;  // chunks mapped so far
+	for (size_t i = 0; i < h.size() && ok; i++) {
 		ok = hipMemMap(static_cast<char*>(va) + i * chunk, chunk, 0, h[perm[i]], 0) == hipSuccess;
+		if (ok) mapped++;
+	}
 	if (ok) {
 		// read-write for this device and every peer that can reach it (the
 		// in-process X-slab group copies between devices, gcmx_halo_exchange_group)
@@ -1205,6 +1207,9 @@ void gcmx_destroy(gcmx_ctx* c) {
 		L.ctx[c->lrank] = nullptr;
 	}
 	if (c->vmm.va) {
+		// unmapping does not wait for the device (hipFree does): another context's
+		// stream may still read these layers (gcmx_copy_box, an in-process group)
+		(void)hipDeviceSynchronize();
 		vmm_free(c->vmm);
 	} else if (c->layers_block) {
 		(void)hipFree(c->layers_block);
@@ -2613,6 +2618,7 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 	if (e0) (void)hipEventDestroy(e0);
 	if (e1) (void)hipEventDestroy(e1);
 	if (vb.va) {
+		(void)hipStreamSynchronize(c->stream);
 		vmm_free(vb);
 	} else {
 		(void)hipFree(a);
