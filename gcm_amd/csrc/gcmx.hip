@@ -951,29 +951,10 @@ static bool vmm_map(int device, size_t bytes, size_t chunk_req, VmmBlock& out) {
 		if (ok) mapped++;
 	}
 	if (ok) {
-		// read-write for this device and every peer that can reach it (the
-		// in-process X-slab group copies between devices, gcmx_halo_exchange_group)
-		std::vector<hipMemAccessDesc> acc;
-		int ndev = 0;
-		if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
-		for (int dv = 0; dv < ndev; dv++) {
-			int can = dv == device;
-			if (!can && hipDeviceCanAccessPeer(&can, dv, device) != hipSuccess) can = 0;
-			if (!can) continue;
-			hipMemAccessDesc a{};
-			a.location.type = hipMemLocationTypeDevice;
-			a.location.id = dv;
-			a.flags = hipMemAccessFlagsProtReadWrite;
-			acc.push_back(a);
-		}
-		ok = !acc.empty() && hipMemSetAccess(va, total, acc.data(), acc.size()) == hipSuccess;
-		if (!ok && acc.size() > 1) {  // peers refused: this device alone
-			(void)hipGetLastError();
-			hipMemAccessDesc a{};
-			a.location = prop.location;
-			a.flags = hipMemAccessFlagsProtReadWrite;
-			ok = hipMemSetAccess(va, total, &a, 1) == hipSuccess;
-		}
+		hipMemAccessDesc a{};
+		a.location = prop.location;
+		a.flags = hipMemAccessFlagsProtReadWrite;
+		ok = hipMemSetAccess(va, total, &a, 1) == hipSuccess;
 	}
 	if (!ok) {
 		(void)hipGetLastError();
@@ -987,6 +968,19 @@ static bool vmm_map(int device, size_t bytes, size_t chunk_req, VmmBlock& out) {
 	out.bytes = total;
 	out.chunks = std::move(h);
 	return true;
+}
+
+// Read-write access to a mapped block for another device (the in-process X-slab
+// group copies between devices); false if the peer cannot be granted it.
+static bool vmm_grant(const VmmBlock& b, int peer) {
+	if (!b.va) return true;
+	hipMemAccessDesc a{};
+	a.location.type = hipMemLocationTypeDevice;
+	a.location.id = peer;
+	a.flags = hipMemAccessFlagsProtReadWrite;
+	if (hipMemSetAccess(b.va, b.bytes, &a, 1) == hipSuccess) return true;
+	(void)hipGetLastError();
+	return false;
 }
 
 static void vmm_free(VmmBlock& b) {
@@ -2382,6 +2376,10 @@ gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n) {
 		if (s) return s;
 	}
 	if (n == 1) return GCMX_OK;
+	for (int i = 0; i + 1 < n; i++)
+		if (slabs[i]->device != slabs[i + 1]->device &&
+		    (!vmm_grant(slabs[i]->vmm, slabs[i + 1]->device) || !vmm_grant(slabs[i + 1]->vmm, slabs[i]->device)))
+			return fail(GCMX_ERR_HIP, "peer access to a neighbour's layers refused");
 	gcmx_ctx* lead = slabs[0];
 	HIP_TRY(hipSetDevice(lead->device));
 	for (int i = 0; i < n; i++) {
@@ -2435,6 +2433,11 @@ gcmx_status gcmx_comm_init_local(gcmx_ctx* const* ctxs, int n) {
 			if (!ok) return fail(GCMX_ERR_INVALID_ARG, "slabs are not X-adjacent with equal y/z extents");
 		}
 	}
+	// neighbours on other devices copy into / out of each other's layers
+	for (int i = 0; i + 1 < n; i++)
+		if (ctxs[i]->device != ctxs[i + 1]->device &&
+		    (!vmm_grant(ctxs[i]->vmm, ctxs[i + 1]->device) || !vmm_grant(ctxs[i + 1]->vmm, ctxs[i]->device)))
+			return fail(GCMX_ERR_HIP, "peer access to a neighbour's layers refused");
 	auto L = std::make_shared<LocalComm>();
 	L->n = n;
 	L->ctx.assign(ctxs, ctxs + n);
