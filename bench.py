@@ -3,16 +3,22 @@
 
 One step = one full time step of cubic::Engine::nextTimeStep (all three stages,
 engine/cubic/Engine.cpp:90-121) over the whole grid, inputs resident in HBM.
-`python bench.py --gpus N --steps K --warmup W`; for N > 1 the driver launches
-one rank per GPU (torch.distributed.run) and the 512^3 grid is split into
-N X-slabs with an RCCL halo exchange of the X ghost planes every step
-(strong scaling: the total work is fixed).
+`python bench.py --gpus N --steps K --warmup W`; for N > 1 the 512^3 grid is
+split into N X-slabs, one rank per GPU, with an RCCL halo exchange of the X
+ghost planes every step (strong scaling: the total work is fixed).  The ranks
+come from a launcher (torch.distributed.run sets RANK / WORLD_SIZE / ...) or,
+when none set WORLD_SIZE, from bench.py itself: the parent process counts the
+devices (no GPU call), starts N rank processes with the launcher's variables
+and relays rank 0's JSON line (`self_launch`).
 
 Prints ONE JSON line on rank 0 (see README/DESIGN for the fields).
 """
 import argparse
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,7 +41,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=512, help="global grid edge (nodes)")
+    # (--edge: the same under torch.distributed.run, whose argparse takes "--n" for an
+    # ambiguous abbreviation of its own options)
+    p.add_argument("--n", "--edge", dest="n", type=int, default=512, help="global grid edge (nodes)")
     p.add_argument("--path", default="auto", choices=["auto", "generic", "split", "fused"])
     p.add_argument("--reps", type=int, default=9,
                    help="repetitions of the K timed steps; value = median (BASELINE.md asks "
@@ -65,6 +73,82 @@ def parse():
                         "(gcmx_comm_init_local: the X-slab step schedule with its overlapped "
                         "in-step exchange, device copies instead of RCCL), one host thread each")
     return p.parse_args()
+
+
+def backend():
+    """(gcm_amd, gcm_amd.gcmx): the product library.  Tests only: GCM_BENCH_BACKEND
+    names a module whose `gcm_amd` / `gcmx` attributes stand in for them
+    (tests/bench_stub.py steps the oracle on the CPU, so the N > 1 orchestration
+    -- rank spawning, the unique-id broadcast, comm_init arguments, the MAX over
+    ranks, the per_rank gather -- runs under gloo without a GPU).  A line made
+    through it says so in `backend` and `data`; it is never a measurement."""
+    name = os.environ.get("GCM_BENCH_BACKEND")
+    if name:
+        mod = importlib.import_module(name)
+        return mod.gcm_amd, mod.gcmx
+    import gcm_amd
+    from gcm_amd import gcmx
+    return gcm_amd, gcmx
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N rank processes of this
+    script, each with RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT set as torch.distributed.run would, rank 0's stdout
+    (the JSON line) relayed to ours, the other ranks' to stderr.  The parent
+    touches no GPU (torch.cuda.device_count() does not initialise one on this
+    image) and refuses to run fewer ranks than asked: too few devices is an
+    error, not a one-rank run.  Returns the exit code (the first failing
+    rank's; the others are then terminated)."""
+    if not os.environ.get("GCM_BENCH_BACKEND"):
+        import torch
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            log(f"bench.py --gpus {a.gpus}: only {have} GPU(s) visible; refusing to run fewer ranks")
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), GCM_BENCH_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    log(f"bench.py: started {a.gpus} ranks (pids {[p.pid for p in procs]}), MASTER_PORT {port}")
+    import threading
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    while any(p.poll() is None for p in procs):  # a failed rank ends the others
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            log(f"bench.py: a rank exited with {rc}; terminating the others")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=60)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.2)
+    reader.join(timeout=60)
+    rc = rc or next((p.returncode for p in procs if p.returncode), 0)
+    sys.stdout.write(out[0].decode() if out else "")
+    sys.stdout.flush()
+    return rc
 
 
 def host_threads() -> int:
@@ -135,7 +219,7 @@ def copy_ceiling(ctx, step_bytes, achieved_gbps):
 def lib_sha256() -> str:
     """Digest of the libgcmx.so this process loaded (gcm_amd.gcmx.LIB_PATH)."""
     import hashlib
-    from gcm_amd import gcmx
+    gcmx = backend()[1]
     with open(gcmx.LIB_PATH, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()
 
@@ -250,13 +334,12 @@ def box_summary(box, sampled):
             "power_w": sampled.get("power_w"), "sclk_mhz_median": statistics.median(sc) if sc else None}
 
 
-def multi_gpu_parity(dist, world, rank, device, U, U1, L, channels):
+def multi_gpu_parity(dist, world, rank, device, U, U1, L, channels, gcm_amd):
     """N > 1 self-check of the RCCL X-slab path (halo exchange overlapped with the
     interior X stage): 3 steps on a 12*N x 40 x 64 grid split into N slabs must
     equal, bitwise, the same grid run whole on rank 0's GPU."""
     import numpy as np
     import torch
-    import gcm_amd
     Xs, Y, Z, bs, seed = 12, 40, 64, 2, 0x5EED
     Xg = Xs * world
     c = gcm_amd.Context(3, bs, [Xs, Y, Z], start=[rank * Xs, 0, 0], device=device)
@@ -383,6 +466,8 @@ def emulate_slabs(a):
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.emulate_slabs:
+        sys.exit(self_launch(a))
     # The ONE JSON line goes to the original stdout; everything else the
     # libraries write to fd 1 (RCCL prints a version banner when a communicator
     # is created) goes to stderr.
@@ -396,15 +481,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE (the launcher's rank count)")
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    import gcm_amd
-    from gcm_amd import gcmx
+    gcm_amd, gcmx = backend()
+    stub = os.environ.get("GCM_BENCH_BACKEND")
     paths = {"auto": gcmx.PATH_AUTO, "generic": gcmx.PATH_GENERIC, "split": gcmx.PATH_SPLIT,
              "fused": gcmx.PATH_FUSED}
 
@@ -415,7 +500,7 @@ def main():
     x0 = rank * X
     device = local if torch.cuda.device_count() > 1 else 0
     # material (4,2,1): ElasticModel<3> matrices built by the host mirror
-    from gcm_amd.host import isotropic_elastic_matrices
+    from gcm_amd.host import isotropic_elastic_matrices  # host C++ (ElasticModel), no GPU
     U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
     tau = 0.9 * 1.0 / 1.0  # Courant * h / max|lambda| (Engine.cpp:124-140)
 
@@ -448,7 +533,7 @@ def main():
     ctx.sync()
     parity = None
     if world > 1:
-        parity = multi_gpu_parity(dist, world, rank, device, U, U1, L, ctx.comm_channels_per_peer)
+        parity = multi_gpu_parity(dist, world, rank, device, U, U1, L, ctx.comm_channels_per_peer, gcm_amd)
         log(f"[rank {rank}] multi-GPU slab parity: {parity}")
     log(f"[rank {rank}] slab x[{x0},{x0 + X}) of {N}^3, {ctx.device_bytes / 1e9:.1f} GB, "
         f"path {ctx.effective_path}, setup {time.perf_counter() - t_setup:.1f}s")
@@ -555,7 +640,7 @@ def main():
                 "kernels": {k: {"avg_ms": round(v["total_ms"] / max(1, v["launches"]), 4),
                                 "GBps": round(v["bytes_per_launch"] /
                                               (v["total_ms"] / max(1, v["launches"]) * 1e-3) /
-                                              1e9, 1)}
+                                              1e9, 1) if v["total_ms"] > 0 else None}
                             for k, v in kernels.items()}}
 
     if roof is not None and not a.no_copy_ceiling:
@@ -574,7 +659,8 @@ def main():
     if rank == 0:
         step_bytes = 3 * BYTES_PER_NODE_STAGE * total_nodes  # three separate stage passes
         out = {
-            "metric": "Mnode-steps/sec + achieved HBM GB/s, 3D isotropic elastic 512³ CubicGrid",
+            # BASELINE.json's metric when N = 512; other grids name their own size
+            "metric": f"Mnode-steps/sec + achieved HBM GB/s, 3D isotropic elastic {N}³ CubicGrid",
             "value": round(value, 1),
             "unit": "Mnode-steps/s",
             "n_gpus": world,
@@ -587,7 +673,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic parity-random field (SplitMix64 seed 0x5EED), material (4,2,1)",
+            "data": ("STUB BACKEND (tests only, not a measurement): " if stub else "")
+                    + "synthetic parity-random field (SplitMix64 seed 0x5EED), material (4,2,1)",
+            **({"backend": f"{stub} (test stub)"} if stub else {}),
             "config": {"workload": f"3-D isotropic elastic CubicGrid {N}^3, borderSize 2, "
                                    f"Courant 0.9, tau 0.9, one full time step (3 stages)",
                        "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,

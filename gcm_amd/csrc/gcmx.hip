@@ -103,6 +103,7 @@ struct VmmBlock {
 	void* va = nullptr;
 	size_t bytes = 0;
 	std::vector<hipMemGenericAllocationHandle_t> chunks;
+	unsigned long long granted = 0;  // devices given read-write access (bit d; the owner's at mapping)
 };
 
 struct gcmx_ctx {
@@ -967,18 +968,26 @@ static bool vmm_map(int device, size_t bytes, size_t chunk_req, VmmBlock& out) {
 	out.va = va;
 	out.bytes = total;
 	out.chunks = std::move(h);
+	out.granted = device < 64 ? 1ULL << device : 0;
 	return true;
 }
 
 // Read-write access to a mapped block for another device (the in-process X-slab
 // group copies between devices); false if the peer cannot be granted it.
-static bool vmm_grant(const VmmBlock& b, int peer) {
+// Granted once per (block, device): the grant walks the whole multi-GB mapping,
+// so it is made at group set-up and cached, never per exchange.
+static bool vmm_grant(VmmBlock& b, int peer) {
 	if (!b.va) return true;
+	const unsigned long long bit = peer >= 0 && peer < 64 ? 1ULL << peer : 0;
+	if (bit && (b.granted & bit)) return true;
 	hipMemAccessDesc a{};
 	a.location.type = hipMemLocationTypeDevice;
 	a.location.id = peer;
 	a.flags = hipMemAccessFlagsProtReadWrite;
-	if (hipMemSetAccess(b.va, b.bytes, &a, 1) == hipSuccess) return true;
+	if (hipMemSetAccess(b.va, b.bytes, &a, 1) == hipSuccess) {
+		b.granted |= bit;
+		return true;
+	}
 	(void)hipGetLastError();
 	return false;
 }
@@ -2376,11 +2385,17 @@ gcmx_status gcmx_halo_exchange_group(gcmx_ctx* const* slabs, int n) {
 		if (s) return s;
 	}
 	if (n == 1) return GCMX_OK;
-	for (int i = 0; i + 1 < n; i++)
-		if (slabs[i]->device != slabs[i + 1]->device &&
-		    (!vmm_grant(slabs[i]->vmm, slabs[i + 1]->device) || !vmm_grant(slabs[i + 1]->vmm, slabs[i]->device)))
-			return fail(GCMX_ERR_HIP, "peer access to a neighbour's layers refused");
 	gcmx_ctx* lead = slabs[0];
+	// every pair's copies run on the lead's comm stream: the lead's device touches
+	// both sides of each pair, the pair's devices each other's layers (cached
+	// grants: the first call pays for them)
+	for (int i = 0; i < n; i++) {
+		gcmx_ctx* c = slabs[i];
+		const bool ok = vmm_grant(c->vmm, lead->device) &&
+		                (i == 0 || vmm_grant(c->vmm, slabs[i - 1]->device)) &&
+		                (i + 1 == n || vmm_grant(c->vmm, slabs[i + 1]->device));
+		if (!ok) return fail(GCMX_ERR_HIP, "peer access to a neighbour's layers refused");
+	}
 	HIP_TRY(hipSetDevice(lead->device));
 	for (int i = 0; i < n; i++) {
 		HIP_TRY(hipSetDevice(slabs[i]->device));
@@ -2435,8 +2450,7 @@ gcmx_status gcmx_comm_init_local(gcmx_ctx* const* ctxs, int n) {
 	}
 	// neighbours on other devices copy into / out of each other's layers
 	for (int i = 0; i + 1 < n; i++)
-		if (ctxs[i]->device != ctxs[i + 1]->device &&
-		    (!vmm_grant(ctxs[i]->vmm, ctxs[i + 1]->device) || !vmm_grant(ctxs[i + 1]->vmm, ctxs[i]->device)))
+		if (!vmm_grant(ctxs[i]->vmm, ctxs[i + 1]->device) || !vmm_grant(ctxs[i + 1]->vmm, ctxs[i]->device))
 			return fail(GCMX_ERR_HIP, "peer access to a neighbour's layers refused");
 	auto L = std::make_shared<LocalComm>();
 	L->n = n;

@@ -419,6 +419,8 @@ __global__ __launch_bounds__(T) void k_step2d(const double* __restrict__ cur, do
 static int step2d_chunk(int X, int ny) {
 	int chunk = X < 64 ? X : 64;
 	while (chunk > 4 && (long long)ny * ((X + chunk - 1) / chunk) < 1024) chunk = (chunk + 1) / 2;
+	// gridDim.y <= 65535: beyond ~4.19M x rows a block marches more rows (any chunk is valid)
+	while ((X + chunk - 1) / chunk > 65535) chunk *= 2;
 	return chunk;
 }
 

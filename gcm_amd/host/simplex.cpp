@@ -1276,13 +1276,19 @@ real Engine::estimateTimeStep() { return tau; }
 // every stage: beforeStage + contactAndBorderStage of every body, the contact
 // correctors, then (per body) its border correctors, innerStage, afterStage, swap.
 // The automatic stage-fusion choice (setStageFusion(-1)) is made on the first
-// steps: one warm-up step, kTuneSteps in mode 1, kTuneSteps in mode 2, each
+// steps: one warm-up step, kTuneSteps in mode 1, one warm-up step and kTuneSteps
+// in mode 2 (with contacts or replayed steps it is not timed: mode 1), each
 // block between stream synchronisations; mode 2 is kept only if >= 3 % faster
 // (faster on the fracture layer, slower on the cube).  Every
 // mode gives the same results (test_one_launch_stage_equals_two_launches), so
 // the timed steps are the run's own steps.
 void Engine::nextTimeStep() {
-	const bool tuning = autoFusion_ && tunePhase_ < 3 && contacts.empty() && !replaySteps;
+	if (autoFusion_ && tunePhase_ < 3 && (!contacts.empty() || replaySteps)) {
+		tunePhase_ = 3;  // no timing with contacts or replayed steps: the choice is mode 1
+		for (auto& b : bodies) gcmxCheck(gsx_set_stage_fusion(b.ctx, 1), "gsx_set_stage_fusion");
+		fusionMode_ = 1;
+	}
+	const bool tuning = autoFusion_ && tunePhase_ < 3;
 	if (tuning && tunePhase_ > 0 && tuneLeft_ == kTuneSteps) {
 		sync();
 		tuneT0_ = std::chrono::steady_clock::now();
@@ -1300,7 +1306,7 @@ void Engine::nextTimeStep() {
 	    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tuneT0_).count() / kTuneSteps;
 	if (tunePhase_ == 1) {
 		tunePhase_ = 2;
-		tuneLeft_ = kTuneSteps;
+		tuneLeft_ = kTuneSteps + 1;  // one untimed step in mode 2 first (its first-use costs)
 		for (auto& b : bodies) gcmxCheck(gsx_set_stage_fusion(b.ctx, 2), "gsx_set_stage_fusion");
 		fusionMode_ = 2;
 	} else {

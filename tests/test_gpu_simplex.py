@@ -232,8 +232,8 @@ def test_one_launch_stage_equals_two_launches(H, case, mode):
 
 def test_automatic_stage_fusion_equals_fixed_mode(H):
     """the engine's default fusion mode (-1) measures modes 1
-    and 2 on its first steps (one warm-up step, 8 steps each between stream
-    synchronisations) and keeps the faster; the modes give identical results, so
+    and 2 on its first steps (an untimed warm-up step before each mode's 8
+    steps between stream synchronisations) and keeps the faster; the modes give identical results, so
     a run through the choice equals a run in mode 1, bitwise.  The engine also
     counts every launch of a step (gsx_launch_count) for the launch floor."""
     mk = lambda: fracture_task((12, 12, 6), 1.0)  # noqa: E731
