@@ -265,6 +265,14 @@ void drain_timings(gcmx_ctx* c) {
 
 long long round_up(long long v, long long m) { return (v + m - 1) / m * m; }
 
+// GCMX_ROW_PAD and friends (gcmx_create): a non-negative element count rounded
+// up to `align`; 0 when unset.
+static long long layout_pad(const char* name, long long align) {
+	const char* e = std::getenv(name);
+	const long long v = (e && *e) ? std::atoll(e) : 0;
+	return v > 0 ? round_up(v, align) : 0;
+}
+
 // Element offset (device layout) of node `it` (multi-index incl. ghosts).
 long long dev_offset(const Geo& g, const int it[3]) {
 	long long o = g.origin;
@@ -1056,20 +1064,27 @@ gcmx_status gcmx_create(const gcmx_grid_desc* d, int device, gcmx_ctx** out) {
 	g.gx0 = d->start[0];
 	// fastest axis: `lead` unused elements, bs ghosts, inner, bs ghosts, padding
 	const int last = D - 1;
+	// Layout perturbation (tests only, GCMX_ROW_PAD / GCMX_PLANE_PAD / GCMX_CS_PAD:
+	// extra elements per row, per 3-D x plane, per component plane, rounded to
+	// keep the alignments): every kernel and host conversion must take its strides
+	// from Geo, and tests/test_gpu_layout.py runs the suites' cases with the strides
+	// no longer implied by the sizes.
+	const long long row_pad = layout_pad("GCMX_ROW_PAD", kRowAlign);
+	const long long plane_pad = D == 3 ? layout_pad("GCMX_PLANE_PAD", kRowAlign) : 0;
+	const long long cs_pad = layout_pad("GCMX_CS_PAD", 64);
 	g.lead = (int)round_up(bs, kRowAlign) - bs;
-	g.row = round_up(g.lead + bs + d->sizes[last] + bs, kRowAlign);
+	g.row = round_up(g.lead + bs + d->sizes[last] + bs, kRowAlign) + row_pad;
 	long long n_all_d[3] = {1, 1, 1};
 	for (int i = 0; i < D; i++) n_all_d[i] = d->sizes[i] + 2LL * bs;
 	for (int i = 0; i < 3; i++) g.stride[i] = 0;
 	g.stride[last] = 1;
 	long long st = g.row;
 	for (int i = last - 1; i >= 0; i--) {
-		g.stride[i] = st;
-		st *= n_all_d[i];
+		g.stride[i] = st + (i == 0 ? plane_pad : 0);
+		st = g.stride[i] * n_all_d[i];
 	}
-	long long total = g.row;
-	for (int i = 0; i < last; i++) total *= n_all_d[i];
-	g.cs = round_up(total, 64);
+	const long long total = st;
+	g.cs = round_up(total, 64) + cs_pad;
 	g.origin = (long long)(g.lead + bs);  // fastest-axis offset of inner index 0
 	for (int i = 0; i < last; i++) g.origin += (long long)bs * g.stride[i];
 	g.n_inner = (long long)g.sizes[0] * g.sizes[1] * g.sizes[2];
@@ -2644,6 +2659,16 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* c, size_t bytes, int reps, float* ms_out
 	if (st) return st;
 	std::sort(ms.begin(), ms.end());
 	*ms_out = ms[ms.size() / 2] * (float)((double)bytes / (double)(2 * half));  // per `bytes`
+	return GCMX_OK;
+}
+
+gcmx_status gcmx_geometry(gcmx_ctx* c, int64_t out[6]) {
+	if (!c || !out) return fail(GCMX_ERR_INVALID_ARG, "null argument");
+	const Geo& g = c->geo;
+	for (int i = 0; i < 3; i++) out[i] = g.stride[i];
+	out[3] = g.cs;
+	out[4] = g.origin;
+	out[5] = g.row;
 	return GCMX_OK;
 }
 

@@ -50,7 +50,7 @@ SYMBOLS = [
     "gcmx_sync", "gcmx_stream",
     "gcmx_profile_enable", "gcmx_profile_reset", "gcmx_profile_read", "gcmx_profile_kernel",
     "gcmx_inner_nodes",
-    "gcmx_all_nodes", "gcmx_device_bytes", "gcmx_copy_ceiling", "gcmx_layer_info",
+    "gcmx_all_nodes", "gcmx_device_bytes", "gcmx_copy_ceiling", "gcmx_layer_info", "gcmx_geometry",
     "gcmx_clock_probe_start", "gcmx_clock_probe_read",
     "gsx_create", "gsx_destroy", "gsx_set_matrices", "gsx_set_gradient_plan",
     "gsx_set_stage_plan", "gsx_set_border_plan", "gsx_set_border_values",
@@ -183,6 +183,7 @@ def lib() -> ctypes.CDLL:
     L.gsx_test_interpolate.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, dp]
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.gcmx_layer_info.argtypes = [vp, u64p]
+    L.gcmx_geometry.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
     L.gcmx_clock_probe_start.argtypes = [vp, ctypes.c_double, ctypes.c_double]
     L.gcmx_clock_probe_read.argtypes = [vp, u64p, ctypes.c_int]
     L.gcmx_clock_probe_read.restype = ctypes.c_int
@@ -435,6 +436,13 @@ class Context:
         ms = ctypes.c_float(0.0)
         _check(lib().gcmx_copy_ceiling(self._ptr, int(nbytes), int(reps), ctypes.byref(ms)))
         return float(ms.value)
+
+    def geometry(self) -> dict:
+        """gcmx_geometry: the device layout's element strides (tests)."""
+        out = (ctypes.c_int64 * 6)()
+        _check(lib().gcmx_geometry(self._ptr, out))
+        return {"stride": [int(out[0]), int(out[1]), int(out[2])], "cs": int(out[3]),
+                "origin": int(out[4]), "row": int(out[5])}
 
     def layer_info(self) -> dict:
         """gcmx_layer_info: the two time layers' device addresses (measurement)."""

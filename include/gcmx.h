@@ -561,6 +561,15 @@ gcmx_status gcmx_copy_ceiling(gcmx_ctx* ctx, size_t bytes, int reps, float* ms_o
  * hipMalloc (1), =contiguous a physically contiguous block (2), =shuffle:<MiB>
  * another chunk size.  DESIGN.md §2 has the measurements. */
 gcmx_status gcmx_layer_info(gcmx_ctx* ctx, uint64_t out[4]);
+/* The device layout of a layer (tests, tools): out[0..2] = the element strides
+ * of axes 0..2 (x plane, y row, z), out[3] = elements per component plane,
+ * out[4] = the element offset of inner node (0, 0, 0) in a plane, out[5] = the
+ * padded row length.  Host code never needs it (gcmx_upload / gcmx_download
+ * take the reference's all-nodes AoS order); GCMX_ROW_PAD / GCMX_PLANE_PAD /
+ * GCMX_CS_PAD (elements, read at gcmx_create, tests only) pad rows, 3-D x
+ * planes and component planes so a test can check that nothing derives a
+ * stride from the sizes. */
+gcmx_status gcmx_geometry(gcmx_ctx* ctx, int64_t out[6]);
 /* Measurement only: the shader clock under load.  _start launches ONE wave on
  * a stream of its own that records (s_memrealtime, s_memtime) pairs every
  * `period_us` for `seconds` (it co-resides with the kernels that run meanwhile);
