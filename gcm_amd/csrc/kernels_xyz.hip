@@ -390,12 +390,22 @@ __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 // read per lane from their LDS copy; where the two nodes of a lane differ in
 // material, their X stages run without the shared differences (pair_update per
 // node).
-template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET>
+//
+// ZS (z split, Z = nz * ZT > 512, uniform medium, no faces): a z row no longer
+// fits one block's register windows (two planes x 1024 z x 6 components x 5 rows
+// of fp64 = 94 % of a CU's register file), so each row is cut into nz parts of
+// ZT lanes, one block each.  A part's Z stage is exact except in the BS lanes
+// next to a cut, which need the other part's Y results: the lanes within 2*BS of
+// a cut write their nodes' Y results (all 9 components) to `seam`, those BS
+// lanes do not store, and k_zseam computes their Z stage from `seam` after the
+// launch ((nz - 1) * 4*BS columns per (x, y): 0.8 % of the layer at 1024^3).
+template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET, bool ZS = false>
 __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
     const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY_,
     IsoAxis AZ_, int x0, int chunk, int nplanes, int xb0, int nplanesb, FaceBC fb,
-    const IsoAxis* __restrict__ mtab, const uint8_t* __restrict__ mat) {
+    const IsoAxis* __restrict__ mtab, const uint8_t* __restrict__ mat, double* __restrict__ seam) {
 	static_assert(!HET || (KF0 && UNI), "heterogeneous step: floor(q) = 0, Z == ZT, equal axes");
+	static_assert(!ZS || (UNI && !FACES && !HET), "z split: uniform medium, no faces");
 	const IsoAxis& AY = UNI ? AX : AY_;
 	const IsoAxis& AZ = UNI ? AX : AZ_;
 	constexpr unsigned WMX = iso_window(0);
@@ -437,6 +447,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const int Y = g.sizes[1], Z = g.sizes[2];
 	int x, yb, xbeg, xend;
 	bool rev;  // this block marches its rows downwards (odd chunks, GCMX_TX2_ALT)
+	int zp = 0;                                    // ZS: this block's part of the z row
+	const int nz = ZS ? g.sizes[2] / ZT : 1;
 	{  // XCD-aware chunk-major block order (see k_fused_xyz) over the plane pairs of
 	   // range A [x0, x0 + nplanes), then range B [xb0, xb0 + nplanesb) (may be empty).
 	   // Pairs are GLOBAL: (2k, 2k+1) in the global x index g.gx0 + x, so a range
@@ -448,7 +460,11 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		const int npa = (nplanes + pa + 1) / 2;
 		const int npair = npa + (nplanesb > 0 ? (nplanesb + pb + 1) / 2 : 0);
 		const int T = (int)gridDim.x, b = (int)blockIdx.x;
-		const int p = xcd_order(b, T);
+		int p = xcd_order(b, T);
+		if constexpr (ZS) {  // the parts of one (pair, chunk) are neighbours in the order
+			zp = p % nz;
+			p /= nz;
+		}
 		const int q = p % npair;
 		x = q < npa ? x0 - pa + 2 * q : xb0 - pb + 2 * (q - npa);
 		xbeg = q < npa ? x0 : xb0;
@@ -474,7 +490,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #if GCMX_TX2_BUF
 	const Planes src(in + pbase, g.cs);
 	const PlanesW out_p(outl + pbase, g.cs);
-	const unsigned lv = (unsigned)zc * 8u, sv = zo * 8u;  // per-lane byte offsets
+	const unsigned zpart = ZS ? (unsigned)(zp * ZT) : 0u;      // ZS: first column of this part
+	const unsigned lv = (zpart + (unsigned)zc) * 8u, sv = (zpart + zo) * 8u;  // per-lane byte offsets
 	const unsigned pxm = plane - (unsigned)BS * stx;      // plane x - BS, row 0, column 0
 	auto ldx = [&](int j, int k, int r) {
 #if GCMX_TX2_PROBE_NOX  // timing probe only (wrong results): x-neighbour loads re-read the own planes
@@ -556,6 +573,12 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 
 	const int wv = z >> 6, ln = z & 63;  // wave in block, lane
+	// ZS: lanes whose Z stage needs the neighbouring part (k_zseam stores them), and
+	// the lanes within 2*BS of a cut, which hand their Y results over in `seam`
+	// (buffer ((s*9 + j)*X + x)*Y + y)*4BS + column, column 0 = z (s+1)*ZT - 2*BS)
+	const bool seam_own = ZS && ((zp > 0 && z < BS) || (zp < nz - 1 && z >= ZT - BS));
+	const int seam_s = ZS ? (z < 2 * BS && zp > 0 ? zp - 1 : (z >= ZT - 2 * BS && zp < nz - 1 ? zp : -1)) : -1;
+	const int seam_col = seam_s < 0 ? 0 : (seam_s == zp ? z - (ZT - 2 * BS) : z + 2 * BS);
 	if constexpr (NB) {  // zero halos (z ghosts stay zero without a z face); counters
 		if (ln < BS || ln >= 64 - BS) {
 			const int hs = ln < BS ? ln : ln + 2 * BS;
@@ -942,7 +965,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll
 			for (int c = 3; c < 9; c++) zv[c] = zv[c] * f;
 		}
-		if (t == 0 ? one : two) {
+		if ((t == 0 ? one : two) && !(ZS && seam_own)) {
 #pragma unroll
 			for (int c = 0; c < 9; c++) stz(c, t, y, live ? zv[c] : 0.0);
 		}
@@ -982,6 +1005,17 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		if constexpr (HET) kn = key_of(rn);
 		y_stage(y, yv);
 		TX2_T(0);
+		if constexpr (ZS) {
+			if (seam_s >= 0) {
+				const long long Xl = g.sizes[0];
+#pragma unroll
+				for (int t = 0; t < 2; t++)
+					if (t == 0 ? one : two)
+#pragma unroll
+						for (int j = 0; j < 9; j++)
+							seam[((((long long)seam_s * 9 + j) * Xl + (x + t)) * Y + y) * (4 * BS) + seam_col] = yv[t][j];
+			}
+		}
 		publish(it, y, yv);
 		TX2_T(2);
 		if constexpr (ZS2) {
@@ -1026,6 +1060,41 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	else run(std::false_type{});
 }
 
+// The Z stage of the nodes next to the cuts of a z-split step (k_step_tx2<...,
+// ZS>): one thread per (plane of the launch's ranges, y, cut, node), window and
+// node values from the Y results the parts left in `seam`, node_update<2> as in
+// the kernel (same operations, same build), the folded ODE factor, 9 stores.
+template <int BS, bool KF0>
+__global__ __launch_bounds__(256) void k_zseam(const double* __restrict__ seam, double* __restrict__ outl, Geo g,
+                                                IsoAxis A, int x0, int nplanes, int xb0, int nplanesb, int zt,
+                                                unsigned ode_on, double ode) {
+	constexpr int NC = 4 * BS;
+	const int X = g.sizes[0], Y = g.sizes[1], ncut = g.sizes[2] / zt - 1;
+	const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+	if (i >= (long long)(nplanes + nplanesb) * Y * ncut * (2 * BS)) return;
+	const int c = (int)(i % (2 * BS));
+	long long r = i / (2 * BS);
+	const int y = (int)(r % Y);
+	r /= Y;
+	const int s = (int)(r % ncut);
+	const int xi = (int)(r / ncut);
+	const int x = xi < nplanes ? x0 + xi : xb0 + (xi - nplanes);
+	const double* b = seam + (((long long)s * 9 * X + x) * Y + y) * NC;  // component j: + j * X * Y * NC
+	const long long cstride = (long long)X * Y * NC;
+	const int col = BS + c;  // z = (s + 1) * zt - BS + c
+	double zv[9];
+	node_update<2, BS, KF0>(
+	    A, [&](int j, int o) { return b[j * cstride + col + o]; }, [&](int j) { return b[j * cstride + col]; }, zv);
+	if (ode_on) {
+#pragma unroll
+		for (int k = 3; k < 9; k++) zv[k] = zv[k] * ode;
+	}
+	const long long off = g.origin + (long long)x * g.stride[0] + (long long)y * g.stride[1] +
+	                      (long long)((s + 1) * zt - BS + c) * g.stride[2];
+#pragma unroll
+	for (int k = 0; k < 9; k++) __builtin_nontemporal_store(zv[k], outl + k * g.cs + off);
+}
+
 // ------------------------------------------------------------- launchers --
 
 static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
@@ -1034,11 +1103,12 @@ static bool same_axis(const IsoAxis& p, const IsoAxis& q) {  // bitwise
 }
 
 // The instance a launch runs, as a readable symbol (gcmx_profile_kernel).
-template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET>
+template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET, bool ZS = false>
 static const char* tx2_name() {
 	static const std::string s = "k_step_tx2<" + std::to_string(BS) + ", " + std::to_string(ZT) + ", " +
 	                             (KF0 ? "KF0" : "!KF0") + ", " + (UNI ? "UNI" : "!UNI") + ", " +
-	                             (FACES ? "FACES" : "!FACES") + (HET ? ", HET" : "") + GCMX_FP_TAG + ">";
+	                             (FACES ? "FACES" : "!FACES") + (HET ? ", HET" : "") + (ZS ? ", ZS" : "") +
+	                             GCMX_FP_TAG + ">";
 	return s.c_str();
 }
 template <int BS, int ZT, bool KF0, bool UNI>
@@ -1090,10 +1160,31 @@ static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                          int x1, int xb0, int xb1, hipStream_t st, int req_chunk, const FaceBC* fb,
-                         const char** kname, const HetMaterials* het) {
+                         const char** kname, const HetMaterials* het, double* seam) {
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
 	const bool uni = kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
+	if constexpr (BS <= 2 && ZT > 512) {
+		// z split (k_step_tx2<BS, 512, ..., ZS> + k_zseam): Z a multiple of 512, uniform
+		// medium (equal axes, floor(q) = 0), no y/z faces, the caller's seam buffer
+		if (seam && !het && !(fb && fb->on) && g.sizes[2] % 512 == 0 && kf0 && same_axis(a[0], a[1]) &&
+		    same_axis(a[0], a[2])) {
+			const int nz = g.sizes[2] / 512, nb = xb1 > xb0 ? xb1 - xb0 : 0;
+			const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2 +
+			                  (nb > 0 ? (nb + ((g.gx0 + xb0) & 1) + 1) / 2 : 0);
+			const int chunk = tx2_chunk_for(g.sizes[1], npair * nz, req_chunk, device_cus());
+			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair * nz);
+			const FaceBC none{};
+			const FaceBC& f = fb ? *fb : none;
+			hipLaunchKernelGGL((k_step_tx2<BS, 512, true, true, false, false, true>), grid, dim3(512), 0, st, in, out,
+			                   g, a[0], a[1], a[2], x0, chunk, x1 - x0, xb0, nb, f, nullptr, nullptr, seam);
+			const long long n = (long long)((x1 - x0) + nb) * g.sizes[1] * (nz - 1) * (2 * BS);
+			hipLaunchKernelGGL((k_zseam<BS, true>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seam, out, g,
+			                   a[2], x0, x1 - x0, xb0, nb, 512, f.ode_on, f.ode);
+			*kname = tx2_name<BS, 512, true, true, false, false, true>();
+			return;
+		}
+	}
 	if constexpr (BS <= 2 && ZT <= 512) {
 		if (GCMX_XYZ_TX2 || fb) {
 			const int nb = xb1 > xb0 ? xb1 - xb0 : 0;
@@ -1110,7 +1201,7 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 			const uint8_t* mi = het ? het->ids : nullptr;
 			auto go = [&](auto K, const char* name) {
 				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, xb0,
-				                   nb, f, mt, mi);
+				                   nb, f, mt, mi, nullptr);
 				*kname = name;
 			};
 			if (het) {  // the caller checked Z == ZT, KF0 and equal axes per material
@@ -1131,7 +1222,7 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 		}
 	}
 	if (xb1 > xb0) {  // k_fused_xyz has no second range: two launches
-		launch_xyz_t<BS, ZT>(in, out, g, a, x0, x1, 0, 0, st, req_chunk, fb, kname, het);
+		launch_xyz_t<BS, ZT>(in, out, g, a, x0, x1, 0, 0, st, req_chunk, fb, kname, het, seam);
 		x0 = xb0;
 		x1 = xb1;
 	}
@@ -1155,13 +1246,13 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 template <int BS>
 static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                           int x1, int xb0, int xb1, hipStream_t st, int ch, const FaceBC* fb,
-                          const char** kn, const HetMaterials* het) {
+                          const char** kn, const HetMaterials* het, double* seam) {
 	const int Z = g.sizes[2];
-	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
-	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
-	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
-	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
-	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
 	return true;
 }
 
@@ -1175,7 +1266,7 @@ extern "C" int gcmx_diag_tx2(unsigned long long* out) {  // 16 x 8 counters, the
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk, const FaceBC* faces, const char** kname,
-                      const HetMaterials* het, int xb0, int xb1) {
+                      const HetMaterials* het, int xb0, int xb1, double* seam) {
 	const char* dummy = nullptr;
 	const char** kn = kname ? kname : &dummy;
 	if (!fused_supported(g) || x1 <= x0) return false;
@@ -1184,9 +1275,9 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	if (faces && faces->on && !fused_faces_supported(g)) return false;
 	if (faces && faces->ode_on && !(g.bs <= 2 && g.sizes[2] <= 512)) return false;  // k_fused_xyz has no epilogue
 	switch (g.bs) {
-	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
-	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
-	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
 	default: return false;
 	}
 }
@@ -1207,6 +1298,11 @@ int step_free_cus(const Geo& g, int x0, int x1, int req_chunk, int cus_in) {
 	const long long blocks = (long long)((g.sizes[1] + chunk - 1) / chunk) * npair;
 	const long long slots = (long long)cus * per_cu;
 	return blocks >= slots ? 0 : (int)((slots - blocks) / per_cu);
+}
+
+long long seam_doubles(const Geo& g) {
+	if (g.D != 3 || g.bs > 2 || g.sizes[2] <= 512 || g.sizes[2] % 512) return 0;
+	return (long long)(g.sizes[2] / 512 - 1) * 9 * g.sizes[0] * g.sizes[1] * 4 * g.bs;
 }
 
 bool het_supported(const Geo& g) {

@@ -58,7 +58,7 @@ def test_padding_reaches_the_geometry(G):
     c = G.Context(3, 2, [6, 20, 64], device=0)
     g = c.geometry()
     c.close()
-    row = 80 + int(os.environ["GCMX_ROW_PAD"])  # 2 lead + 2 + 64 + 2 -> 80, + pad
+    row = 96 + int(os.environ["GCMX_ROW_PAD"])  # 14 lead + 2 + 64 + 2 -> 96 (16-aligned), + pad
     assert g["stride"][1] == row
     assert g["stride"][0] == row * 24 + int(os.environ["GCMX_PLANE_PAD"])
     assert g["cs"] >= g["stride"][0] * 10 + int(os.environ["GCMX_CS_PAD"])

@@ -71,6 +71,40 @@ def test_fused_step_3d(G, bs, sizes):
         assert_same(ctx, b, f"fused bs={bs} sizes={sizes} step {step}")
 
 
+@pytest.mark.parametrize("bs,sizes", [(2, [5, 9, 1024]), (1, [4, 6, 1024]), (2, [3, 130, 1024])])
+def test_zsplit_step_matches_oracle(G, bs, sizes):
+    """Rows longer than 512: the z-split one-pass step -- two
+    512-lane parts per row, the Z stage of the nodes next to the cut from the
+    parts' Y results (k_zseam) -- == three oracle stages, bitwise, odd X included."""
+    b = oracle_body(3, bs, sizes)
+    random_state(b, seed=sum(sizes) + bs, ghosts=False)
+    ctx = context_for(b, path=G.PATH_AUTO)
+    ctx.profile(True)
+    for step in range(3):
+        for s in range(3):
+            b.stage(s, 0.9)
+        ctx.step(0.9)
+        assert_same(ctx, b, f"z split bs={bs} sizes={sizes} step {step}")
+    k = ctx.profile_read()["fused_xyz"]["kernel"]
+    assert k.startswith("k_step_tx2<") and "ZS" in k, k
+    ctx.close()
+
+
+def test_zsplit_not_taken_above_courant_one(G):
+    """floor(q) > 0 (Courant 1.5) keeps rows of 1024 on the one-plane k_fused_xyz,
+    which still equals the oracle."""
+    b = oracle_body(3, 2, [4, 6, 1024])
+    random_state(b, seed=11, ghosts=False)
+    ctx = context_for(b, path=G.PATH_AUTO)
+    ctx.profile(True)
+    for s in range(3):
+        b.stage(s, 1.5)
+    ctx.step(1.5)
+    assert_same(ctx, b, "Courant 1.5, Z = 1024")
+    assert ctx.profile_read()["fused_xyz"]["kernel"].startswith("k_fused_xyz<")
+    ctx.close()
+
+
 def test_fused_disabled_by_nonzero_ghosts(G):
     b = oracle_body(3, 2, [6, 6, 6])
     random_state(b, seed=1, ghosts=True)

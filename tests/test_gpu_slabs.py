@@ -114,6 +114,27 @@ def test_local_group_fused_equals_whole(G, sched, xs):
         c.close()
 
 
+@pytest.mark.parametrize("sched", ["xslab", "bfirst"])
+def test_local_group_zsplit_rows_equal_whole(G, sched):
+    """Rows of 1024 nodes (the z-split step, k_step_tx2<..., ZS> + k_zseam, on
+    plane ranges and the boundary-first two-range launch) in a ragged slab group
+    == one context, bitwise."""
+    xs, Y, Z, seed, steps = [9, 6, 7], 10, 1024, 0x5EED, 3
+    sc = {"xslab": G.SCHED_XSLAB, "bfirst": G.SCHED_BFIRST}[sched]
+    slabs = _group(G, xs, Y, Z, seed, sched=sc)
+    whole = _whole(G, sum(xs), Y, Z, seed)
+    for c in slabs + [whole]:
+        c.profile(True)
+    G.local_group_steps(slabs, 0.9, steps)
+    for _ in range(steps):
+        whole.step(0.9)
+    assert all(c.last_path == "fused" for c in slabs)
+    assert "ZS" in whole.profile_read()["fused_xyz"]["kernel"]
+    assert np.array_equal(_concat(slabs), _inner(whole, whole.download()))
+    for c in slabs + [whole]:
+        c.close()
+
+
 def test_local_group_split_path_per_stage_exchange(G):
     """Split path (gcmx_stage per axis): the X stage's halo is exchanged inside
     stage(0) (halo_ensure), per stage, as gcmx_stage with a communicator does."""
