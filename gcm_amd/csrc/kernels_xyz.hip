@@ -1172,7 +1172,10 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 			const int nz = g.sizes[2] / 512, nb = xb1 > xb0 ? xb1 - xb0 : 0;
 			const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2 +
 			                  (nb > 0 ? (nb + ((g.gx0 + xb0) & 1) + 1) / 2 : 0);
-			const int chunk = tx2_chunk_for(g.sizes[1], npair * nz, req_chunk, device_cus());
+			// 128 rows per block unless asked: 1024^3 35.2 ms against 36.3 (256 rows),
+			// 36.6 (64) and 39.0 (1024, the one-round rule of the Z <= 512 step),
+			// profiles/r6/e
+			const int chunk = req_chunk > 0 ? std::min(req_chunk, g.sizes[1]) : std::min(128, g.sizes[1]);
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair * nz);
 			const FaceBC none{};
 			const FaceBC& f = fb ? *fb : none;
