@@ -225,13 +225,14 @@ def lib_sha256() -> str:
 
 
 def pmc_traffic(n, ranks, bucket, symbol):
-    """HBM bytes per launch from profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes, tools/pmc_traffic.py), used only when that profile was
+    """HBM bytes per launch from profiles/pmc_traffic.json (512^3; other grids
+    profiles/pmc_traffic_<n>.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
+    tools/pmc_traffic.py), used only when that profile was
     taken of THIS library build (sha256), the same grid, rank count and kernel
     instance; otherwise (None, reason)."""
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if n == 512 else f"pmc_traffic_{n}.json")
     if not os.path.exists(pmc):
-        return None, "no PMC profile"
+        return None, f"no PMC profile ({os.path.basename(pmc)})"
     try:
         rec = json.load(open(pmc))
     except Exception as e:

@@ -1157,6 +1157,28 @@ static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK
 	return Y <= chunk ? Y : chunk;
 }
 
+// z split (k_step_tx2<BS, P, ..., ZS> + k_zseam): parts of P lanes, uniform
+// medium (equal axes, floor(q) = 0), no y/z faces, the caller's seam buffer.
+template <int BS, int P>
+static void launch_zs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0, int x1, int xb0, int xb1,
+                      hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname, double* seam) {
+	const int nz = g.sizes[2] / P, nb = xb1 > xb0 ? xb1 - xb0 : 0;
+	const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2 + (nb > 0 ? (nb + ((g.gx0 + xb0) & 1) + 1) / 2 : 0);
+	// 128 rows per block unless asked: 1024^3 35.2 ms against 36.3 (256 rows),
+	// 36.6 (64) and 39.0 (1024, the one-round rule of the Z <= 512 step),
+	// profiles/r6/e
+	const int chunk = req_chunk > 0 ? std::min(req_chunk, g.sizes[1]) : std::min(128, g.sizes[1]);
+	const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair * nz);
+	const FaceBC none{};
+	const FaceBC& f = fb ? *fb : none;
+	hipLaunchKernelGGL((k_step_tx2<BS, P, true, true, false, false, true>), grid, dim3(P), 0, st, in, out, g, a[0],
+	                   a[1], a[2], x0, chunk, x1 - x0, xb0, nb, f, nullptr, nullptr, seam);
+	const long long n = (long long)((x1 - x0) + nb) * g.sizes[1] * (nz - 1) * (2 * BS);
+	hipLaunchKernelGGL((k_zseam<BS, true>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seam, out, g, a[2],
+	                   x0, x1 - x0, xb0, nb, P, f.ode_on, f.ode);
+	*kname = tx2_name<BS, P, true, true, false, false, true>();
+}
+
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                          int x1, int xb0, int xb1, hipStream_t st, int req_chunk, const FaceBC* fb,
@@ -1164,30 +1186,6 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
 	const bool uni = kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
-	if constexpr (BS <= 2 && ZT > 512) {
-		// z split (k_step_tx2<BS, 512, ..., ZS> + k_zseam): Z a multiple of 512, uniform
-		// medium (equal axes, floor(q) = 0), no y/z faces, the caller's seam buffer
-		if (seam && !het && !(fb && fb->on) && g.sizes[2] % 512 == 0 && kf0 && same_axis(a[0], a[1]) &&
-		    same_axis(a[0], a[2])) {
-			const int nz = g.sizes[2] / 512, nb = xb1 > xb0 ? xb1 - xb0 : 0;
-			const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2 +
-			                  (nb > 0 ? (nb + ((g.gx0 + xb0) & 1) + 1) / 2 : 0);
-			// 128 rows per block unless asked: 1024^3 35.2 ms against 36.3 (256 rows),
-			// 36.6 (64) and 39.0 (1024, the one-round rule of the Z <= 512 step),
-			// profiles/r6/e
-			const int chunk = req_chunk > 0 ? std::min(req_chunk, g.sizes[1]) : std::min(128, g.sizes[1]);
-			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair * nz);
-			const FaceBC none{};
-			const FaceBC& f = fb ? *fb : none;
-			hipLaunchKernelGGL((k_step_tx2<BS, 512, true, true, false, false, true>), grid, dim3(512), 0, st, in, out,
-			                   g, a[0], a[1], a[2], x0, chunk, x1 - x0, xb0, nb, f, nullptr, nullptr, seam);
-			const long long n = (long long)((x1 - x0) + nb) * g.sizes[1] * (nz - 1) * (2 * BS);
-			hipLaunchKernelGGL((k_zseam<BS, true>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seam, out, g,
-			                   a[2], x0, x1 - x0, xb0, nb, 512, f.ode_on, f.ode);
-			*kname = tx2_name<BS, 512, true, true, false, false, true>();
-			return;
-		}
-	}
 	if constexpr (BS <= 2 && ZT <= 512) {
 		if (GCMX_XYZ_TX2 || fb) {
 			const int nb = xb1 > xb0 ? xb1 - xb0 : 0;
@@ -1277,6 +1275,17 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	if (het && !het_supported(g)) return false;
 	if (faces && faces->on && !fused_faces_supported(g)) return false;
 	if (faces && faces->ode_on && !(g.bs <= 2 && g.sizes[2] <= 512)) return false;  // k_fused_xyz has no epilogue
+	if (const int P = zs_part(g); P > 0 && seam && !het && !(faces && faces->on)) {
+		bool kf0 = true;
+		for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
+		if (kf0 && same_axis(a[0], a[1]) && same_axis(a[0], a[2])) {
+			if (g.bs == 1) P == 256 ? launch_zs<1, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam)
+			               : launch_zs<1, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam);
+			else P == 256 ? launch_zs<2, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam)
+			              : launch_zs<2, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam);
+			return true;
+		}
+	}
 	switch (g.bs) {
 	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
 	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
@@ -1303,9 +1312,21 @@ int step_free_cus(const Geo& g, int x0, int x1, int req_chunk, int cus_in) {
 	return blocks >= slots ? 0 : (int)((slots - blocks) / per_cu);
 }
 
+int zs_part(const Geo& g) {
+	// GCMX_ZS_PART=256 (tuning): rows of 512 and more cut into 256-lane parts
+	static const int env = [] {
+		const char* e = std::getenv("GCMX_ZS_PART");
+		return e ? std::atoi(e) : 0;
+	}();
+	const int Z = g.sizes[2];
+	if (g.D != 3 || g.bs > 2) return 0;
+	if (env == 256 && Z >= 512 && Z % 256 == 0) return 256;
+	return Z > 512 && Z % 512 == 0 ? 512 : 0;
+}
+
 long long seam_doubles(const Geo& g) {
-	if (g.D != 3 || g.bs > 2 || g.sizes[2] <= 512 || g.sizes[2] % 512) return 0;
-	return (long long)(g.sizes[2] / 512 - 1) * 9 * g.sizes[0] * g.sizes[1] * 4 * g.bs;
+	const int P = zs_part(g);
+	return P ? (long long)(g.sizes[2] / P - 1) * 9 * g.sizes[0] * g.sizes[1] * 4 * g.bs : 0;
 }
 
 bool het_supported(const Geo& g) {

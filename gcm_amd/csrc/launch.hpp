@@ -165,6 +165,7 @@ bool het_supported(const Geo& g);
 // of rows longer than 512 (k_step_tx2<..., ZS> + k_zseam); without it such rows
 // take the one-plane k_fused_xyz.
 long long seam_doubles(const Geo& g);
+int zs_part(const Geo& g);  // lanes per part of the z-split step, 0: rows are not split
 int step_free_cus(const Geo& g, int x0, int x1, int req_chunk, int cus = -1);  // cus <= 0: the device's
 // Two builds of the one-pass step kernels (kernels_xyz.hip): xyz_exact keeps the
 // reference's roundings (bitwise), xyz_fma contracts multiply-adds
