@@ -1005,17 +1005,6 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		if constexpr (HET) kn = key_of(rn);
 		y_stage(y, yv);
 		TX2_T(0);
-		if constexpr (ZS) {
-			if (seam_s >= 0) {
-				const long long Xl = g.sizes[0];
-#pragma unroll
-				for (int t = 0; t < 2; t++)
-					if (t == 0 ? one : two)
-#pragma unroll
-						for (int j = 0; j < 9; j++)
-							seam[((((long long)seam_s * 9 + j) * Xl + (x + t)) * Y + y) * (4 * BS) + seam_col] = yv[t][j];
-			}
-		}
 		publish(it, y, yv);
 		TX2_T(2);
 		if constexpr (ZS2) {
@@ -1040,6 +1029,18 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 				}
 			}
 			z_stage_store(t, y, yv);
+		}
+		if constexpr (ZS) {  // the cut lanes' Y results, with (after) the row's stores: a
+			                 // later vmcnt wait for the row-ahead loads never includes them
+			if (seam_s >= 0) {
+				const long long Xl = g.sizes[0];
+#pragma unroll
+				for (int t = 0; t < 2; t++)
+					if (t == 0 ? one : two)
+#pragma unroll
+						for (int j = 0; j < 9; j++)
+							seam[((((long long)seam_s * 9 + j) * Xl + (x + t)) * Y + y) * (4 * BS) + seam_col] = yv[t][j];
+			}
 		}
 		TX2_T(3);
 		x_enter(y, pre, kn);
