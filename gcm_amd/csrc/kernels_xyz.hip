@@ -311,6 +311,9 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_HET_AB
 #define GCMX_HET_AB 0
 #endif
+#ifndef GCMX_ZS_NOSEAM  // timing knob (wrong results): the z split without its hand-over stores
+#define GCMX_ZS_NOSEAM 0
+#endif
 #ifndef GCMX_TX2_UNROLL  // timing knob: row-loop unroll (5 = the window period: no window moves)
 #define GCMX_TX2_UNROLL 1
 #endif
@@ -1030,7 +1033,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			}
 			z_stage_store(t, y, yv);
 		}
-		if constexpr (ZS) {  // the cut lanes' Y results, with (after) the row's stores: a
+		if constexpr (ZS && !GCMX_ZS_NOSEAM) {  // the cut lanes' Y results, with (after) the row's stores: a
 			                 // later vmcnt wait for the row-ahead loads never includes them
 			if (seam_s >= 0) {
 				const long long Xl = g.sizes[0];
