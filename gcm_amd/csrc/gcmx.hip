@@ -139,7 +139,6 @@ struct gcmx_ctx {
 	int n_mat = 0;
 	std::vector<double> U, U1, L;  // [mat][D][M*M], [mat][D][M]
 	uint8_t* mat_d = nullptr;      // inner nodes, linear inner order; null = homogeneous
-	double* seam_d = nullptr;      // z-split step's hand-over buffer (seam_doubles), on first use
 	int max_mat_id = -1;           // largest id in mat_d (set_materials must cover it)
 	AxisTable* tabs_d = nullptr;   // [mat][D]
 	double tabs_tau = NAN;
@@ -1243,7 +1242,6 @@ void gcmx_destroy(gcmx_ctx* c) {
 	(void)hipFree(c->nodes_d);
 	(void)hipFree(c->ode_d);
 	(void)hipFree(c->het_d);
-	(void)hipFree(c->seam_d);
 	if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
 	if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
 	if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
@@ -1489,14 +1487,12 @@ gcmx_status fused_step(gcmx_ctx* c, const FaceBC* fb, bool final) {
 	const int X = g.sizes[0], bs = c->bs;
 	const double plane_bytes = node_stage_bytes(c) * (double)g.sizes[1] * g.sizes[2];
 	const bool halo = has_halo(c);
-	if (!c->seam_d && seam_doubles(g) > 0)  // rows longer than 512: the z-split step's buffer
-		HIP_TRY(hipMalloc(&c->seam_d, (size_t)seam_doubles(g) * sizeof(double)));
 	auto xyz = [&](const char* name, int x0, int x1, hipStream_t st, int rows, int xb0 = 0, int xb1 = 0) {
 		Timed t(c, name, plane_bytes * ((x1 - x0) + (xb1 - xb0)), st);
 		const HetMaterials het{c->het_d, c->mat_d};
 		auto launch = c->fp_mode == GCMX_FP_EXACT ? xyz_exact::launch_fused_xyz : xyz_fma::launch_fused_xyz;
 		return launch(c->cur, c->nxt, g, c->iso, x0, x1, st, rows, fb, &t.kname, c->iso_het ? &het : nullptr,
-		              xb0, xb1, c->seam_d);
+		              xb0, xb1);
 	};
 	const gcmx_schedule sched =
 	    c->sched == GCMX_SCHED_AUTO ? (halo ? GCMX_SCHED_BFIRST : GCMX_SCHED_SINGLE) : c->sched;

@@ -311,9 +311,7 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_HET_AB
 #define GCMX_HET_AB 0
 #endif
-#ifndef GCMX_ZS_NOSEAM  // timing knob (wrong results): the z split without its hand-over stores
-#define GCMX_ZS_NOSEAM 0
-#endif
+
 #ifndef GCMX_TX2_UNROLL  // timing knob: row-loop unroll (5 = the window period: no window moves)
 #define GCMX_TX2_UNROLL 1
 #endif
@@ -398,15 +396,17 @@ __host__ __device__ constexpr int wcomp(unsigned mask, int q) {
 // fits one block's register windows (two planes x 1024 z x 6 components x 5 rows
 // of fp64 = 94 % of a CU's register file), so each row is cut into nz parts of
 // ZT lanes, one block each.  A part's Z stage is exact except in the BS lanes
-// next to a cut, which need the other part's Y results: the lanes within 2*BS of
-// a cut write their nodes' Y results (all 9 components) to `seam`, those BS
-// lanes do not store, and k_zseam computes their Z stage from `seam` after the
-// launch ((nz - 1) * 4*BS columns per (x, y): 0.8 % of the layer at 1024^3).
+// next to a cut, which need the other part's Y results: those lanes do not
+// store, and k_zseam recomputes the X and Y stages of the 4*BS columns around
+// each cut and stores their Z stage after the launch (1024^3: 8 of 1024 columns).
+// (Handing the cut lanes' Y results over through memory instead cost 25 %: those
+// lanes' extra stores sit in the vmcnt queue the row-ahead loads are waited on
+// with, profiles/r6/h.)
 template <int BS, int ZT, bool KF0, bool UNI, bool FACES, bool HET, bool ZS = false>
 __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
     const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY_,
     IsoAxis AZ_, int x0, int chunk, int nplanes, int xb0, int nplanesb, FaceBC fb,
-    const IsoAxis* __restrict__ mtab, const uint8_t* __restrict__ mat, double* __restrict__ seam) {
+    const IsoAxis* __restrict__ mtab, const uint8_t* __restrict__ mat) {
 	static_assert(!HET || (KF0 && UNI), "heterogeneous step: floor(q) = 0, Z == ZT, equal axes");
 	static_assert(!ZS || (UNI && !FACES && !HET), "z split: uniform medium, no faces");
 	const IsoAxis& AY = UNI ? AX : AY_;
@@ -576,12 +576,8 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	};
 
 	const int wv = z >> 6, ln = z & 63;  // wave in block, lane
-	// ZS: lanes whose Z stage needs the neighbouring part (k_zseam stores them), and
-	// the lanes within 2*BS of a cut, which hand their Y results over in `seam`
-	// (buffer ((s*9 + j)*X + x)*Y + y)*4BS + column, column 0 = z (s+1)*ZT - 2*BS)
+	// ZS: lanes whose Z stage needs the neighbouring part (k_zseam stores them)
 	const bool seam_own = ZS && ((zp > 0 && z < BS) || (zp < nz - 1 && z >= ZT - BS));
-	const int seam_s = ZS ? (z < 2 * BS && zp > 0 ? zp - 1 : (z >= ZT - 2 * BS && zp < nz - 1 ? zp : -1)) : -1;
-	const int seam_col = seam_s < 0 ? 0 : (seam_s == zp ? z - (ZT - 2 * BS) : z + 2 * BS);
 	if constexpr (NB) {  // zero halos (z ghosts stay zero without a z face); counters
 		if (ln < BS || ln >= 64 - BS) {
 			const int hs = ln < BS ? ln : ln + 2 * BS;
@@ -1033,18 +1029,6 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			}
 			z_stage_store(t, y, yv);
 		}
-		if constexpr (ZS && !GCMX_ZS_NOSEAM) {  // the cut lanes' Y results, with (after) the row's stores: a
-			                 // later vmcnt wait for the row-ahead loads never includes them
-			if (seam_s >= 0) {
-				const long long Xl = g.sizes[0];
-#pragma unroll
-				for (int t = 0; t < 2; t++)
-					if (t == 0 ? one : two)
-#pragma unroll
-						for (int j = 0; j < 9; j++)
-							seam[((((long long)seam_s * 9 + j) * Xl + (x + t)) * Y + y) * (4 * BS) + seam_col] = yv[t][j];
-			}
-		}
 		TX2_T(3);
 		x_enter(y, pre, kn);
 		TX2_T(5);
@@ -1064,39 +1048,83 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	else run(std::false_type{});
 }
 
-// The Z stage of the nodes next to the cuts of a z-split step (k_step_tx2<...,
-// ZS>): one thread per (plane of the launch's ranges, y, cut, node), window and
-// node values from the Y results the parts left in `seam`, node_update<2> as in
-// the kernel (same operations, same build), the folded ODE factor, 9 stores.
+// The nodes next to the cuts of a z-split step (k_step_tx2<..., ZS>), after it:
+// lane (plane, column) of a group of 4*BS lanes holds one of the columns
+// cut - 2*BS ... cut + 2*BS - 1 of one x plane and marches y like k_fused_xyz --
+// the X stage of the entering row (node_update<0>: the same per-node operations
+// as the one-pass step's X stage), the Y stage from its register window -- then
+// the Z stage of the middle 2*BS columns from the group's Y results (lane
+// shuffles), the folded ODE factor, 9 stores.  Rows: `chunk` per block, the
+// 2*BS-row prologue recomputed.  Reads the 4*BS columns' neighbourhoods (mostly
+// L2), writes 2*BS columns per cut: at 1024^3 0.4 % of the step's bytes.
 template <int BS, bool KF0>
-__global__ __launch_bounds__(256) void k_zseam(const double* __restrict__ seam, double* __restrict__ outl, Geo g,
+__global__ __launch_bounds__(256) void k_zseam(const double* __restrict__ in, double* __restrict__ outl, Geo g,
                                                 IsoAxis A, int x0, int nplanes, int xb0, int nplanesb, int zt,
-                                                unsigned ode_on, double ode) {
-	constexpr int NC = 4 * BS;
-	const int X = g.sizes[0], Y = g.sizes[1], ncut = g.sizes[2] / zt - 1;
-	const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-	if (i >= (long long)(nplanes + nplanesb) * Y * ncut * (2 * BS)) return;
-	const int c = (int)(i % (2 * BS));
-	long long r = i / (2 * BS);
-	const int y = (int)(r % Y);
-	r /= Y;
-	const int s = (int)(r % ncut);
-	const int xi = (int)(r / ncut);
-	const int x = xi < nplanes ? x0 + xi : xb0 + (xi - nplanes);
-	const double* b = seam + (((long long)s * 9 * X + x) * Y + y) * NC;  // component j: + j * X * Y * NC
-	const long long cstride = (long long)X * Y * NC;
-	const int col = BS + c;  // z = (s + 1) * zt - BS + c
-	double zv[9];
-	node_update<2, BS, KF0>(
-	    A, [&](int j, int o) { return b[j * cstride + col + o]; }, [&](int j) { return b[j * cstride + col]; }, zv);
-	if (ode_on) {
+                                                int chunk, unsigned ode_on, double ode) {
+	constexpr int NC = 4 * BS, PB = 256 / NC, W = 2 * BS + 1;
+	const int Y = g.sizes[1], ncut = g.sizes[2] / zt - 1;
+	const int nch = (Y + chunk - 1) / chunk;
+	int b = (int)blockIdx.x;
+	const int ch = b % nch;
+	b /= nch;
+	const int cut = b % ncut;
+	const int pg = b / ncut;
+	const int c = (int)threadIdx.x % NC, xi = pg * PB + (int)threadIdx.x / NC;
+	const bool valid = xi < nplanes + nplanesb;
+	const int x = !valid ? x0 : xi < nplanes ? x0 + xi : xb0 + (xi - nplanes);
+	const int z = (cut + 1) * zt - 2 * BS + c;
+	const long long stx = g.stride[0], sty = g.stride[1], cs = g.cs;
+	const long long base = g.origin + (long long)x * stx + z;
+	const int yb = ch * chunk, ye = min(yb + chunk, Y);
+	// X result of row r (rows outside [0, Y): zero ghost rows; beyond them clamped)
+	auto xstage = [&](int r, double (&xr)[9]) {
+		const int rc = r < -BS ? -BS : (r > Y + BS - 1 ? Y + BS - 1 : r);
+		const long long o = base + (long long)rc * sty;
+		node_update<0, BS, KF0>(
+		    A, [&](int j, int oo) { return in[j * cs + o + oo * stx]; }, [&](int j) { return in[j * cs + o]; }, xr);
+	};
+	double win[9][W];
 #pragma unroll
-		for (int k = 3; k < 9; k++) zv[k] = zv[k] * ode;
+	for (int k = 0; k < W; k++) {
+		double xr[9];
+		const int r = yb - BS + k;
+		if (r >= 0 && r < Y) xstage(r, xr);
+		else
+#pragma unroll
+			for (int j = 0; j < 9; j++) xr[j] = 0.0;
+#pragma unroll
+		for (int j = 0; j < 9; j++) win[j][k] = xr[j];
 	}
-	const long long off = g.origin + (long long)x * g.stride[0] + (long long)y * g.stride[1] +
-	                      (long long)((s + 1) * zt - BS + c) * g.stride[2];
+	const bool mine = valid && c >= BS && c < 3 * BS;  // the columns whose Z stage the parts left
+	const int lane = (int)(threadIdx.x & 63);
+	for (int y = yb; y < ye; y++) {
+		double yv[9], zv[9];
+		node_update<1, BS, KF0>(A, [&](int j, int o) { return win[j][BS + o]; }, [&](int j) { return win[j][BS]; }, yv);
+		// z neighbours: lanes c +- o of the same group (the group never straddles a wave)
+		node_update<2, BS, KF0>(
+		    A, [&](int j, int o) { return __shfl(yv[j], lane + o, 64); }, [&](int j) { return yv[j]; }, zv);
+		if (mine) {
+			if (ode_on) {
 #pragma unroll
-	for (int k = 0; k < 9; k++) __builtin_nontemporal_store(zv[k], outl + k * g.cs + off);
+				for (int k = 3; k < 9; k++) zv[k] = zv[k] * ode;
+			}
+			const long long off = base + (long long)y * sty;
+#pragma unroll
+			for (int k = 0; k < 9; k++) __builtin_nontemporal_store(zv[k], outl + k * cs + off);
+		}
+#pragma unroll
+		for (int j = 0; j < 9; j++)
+#pragma unroll
+			for (int k = 0; k < W - 1; k++) win[j][k] = win[j][k + 1];
+		double xr[9];
+		const int r = y + BS + 1;
+		if (r < Y) xstage(r, xr);
+		else
+#pragma unroll
+			for (int j = 0; j < 9; j++) xr[j] = 0.0;
+#pragma unroll
+		for (int j = 0; j < 9; j++) win[j][W - 1] = xr[j];
+	}
 }
 
 // ------------------------------------------------------------- launchers --
@@ -1162,10 +1190,10 @@ static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK
 }
 
 // z split (k_step_tx2<BS, P, ..., ZS> + k_zseam): parts of P lanes, uniform
-// medium (equal axes, floor(q) = 0), no y/z faces, the caller's seam buffer.
+// medium (equal axes, floor(q) = 0), no y/z faces.
 template <int BS, int P>
 static void launch_zs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0, int x1, int xb0, int xb1,
-                      hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname, double* seam) {
+                      hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname) {
 	const int nz = g.sizes[2] / P, nb = xb1 > xb0 ? xb1 - xb0 : 0;
 	const int npair = (x1 - x0 + ((g.gx0 + x0) & 1) + 1) / 2 + (nb > 0 ? (nb + ((g.gx0 + xb0) & 1) + 1) / 2 : 0);
 	// 128 rows per block unless asked: 1024^3 35.2 ms against 36.3 (256 rows),
@@ -1176,17 +1204,19 @@ static void launch_zs(const double* in, double* out, const Geo& g, const IsoAxis
 	const FaceBC none{};
 	const FaceBC& f = fb ? *fb : none;
 	hipLaunchKernelGGL((k_step_tx2<BS, P, true, true, false, false, true>), grid, dim3(P), 0, st, in, out, g, a[0],
-	                   a[1], a[2], x0, chunk, x1 - x0, xb0, nb, f, nullptr, nullptr, seam);
-	const long long n = (long long)((x1 - x0) + nb) * g.sizes[1] * (nz - 1) * (2 * BS);
-	hipLaunchKernelGGL((k_zseam<BS, true>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seam, out, g, a[2],
-	                   x0, x1 - x0, xb0, nb, P, f.ode_on, f.ode);
+	                   a[1], a[2], x0, chunk, x1 - x0, xb0, nb, f, nullptr, nullptr);
+	// the cut columns: 256 / (4 BS) planes per block, 64-row chunks
+	const int np = (x1 - x0) + nb, pb = 256 / (4 * BS), sch = std::min(64, g.sizes[1]);
+	const long long nblk = (long long)((np + pb - 1) / pb) * (nz - 1) * ((g.sizes[1] + sch - 1) / sch);
+	hipLaunchKernelGGL((k_zseam<BS, true>), dim3((unsigned)nblk), dim3(256), 0, st, in, out, g, a[0], x0, x1 - x0, xb0,
+	                   nb, P, sch, f.ode_on, f.ode);
 	*kname = tx2_name<BS, P, true, true, false, false, true>();
 }
 
 template <int BS, int ZT>
 static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                          int x1, int xb0, int xb1, hipStream_t st, int req_chunk, const FaceBC* fb,
-                         const char** kname, const HetMaterials* het, double* seam) {
+                         const char** kname, const HetMaterials* het) {
 	bool kf0 = true;
 	for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
 	const bool uni = kf0 && g.sizes[2] == ZT && same_axis(a[0], a[1]) && same_axis(a[0], a[2]);
@@ -1206,7 +1236,7 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 			const uint8_t* mi = het ? het->ids : nullptr;
 			auto go = [&](auto K, const char* name) {
 				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, xb0,
-				                   nb, f, mt, mi, nullptr);
+				                   nb, f, mt, mi);
 				*kname = name;
 			};
 			if (het) {  // the caller checked Z == ZT, KF0 and equal axes per material
@@ -1227,7 +1257,7 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 		}
 	}
 	if (xb1 > xb0) {  // k_fused_xyz has no second range: two launches
-		launch_xyz_t<BS, ZT>(in, out, g, a, x0, x1, 0, 0, st, req_chunk, fb, kname, het, seam);
+		launch_xyz_t<BS, ZT>(in, out, g, a, x0, x1, 0, 0, st, req_chunk, fb, kname, het);
 		x0 = xb0;
 		x1 = xb1;
 	}
@@ -1251,13 +1281,13 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 template <int BS>
 static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                           int x1, int xb0, int xb1, hipStream_t st, int ch, const FaceBC* fb,
-                          const char** kn, const HetMaterials* het, double* seam) {
+                          const char** kn, const HetMaterials* het) {
 	const int Z = g.sizes[2];
-	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
-	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
-	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
-	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
-	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het, seam);
+	if (Z <= 64) launch_xyz_t<BS, 64>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else if (Z <= 128) launch_xyz_t<BS, 128>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else if (Z <= 256) launch_xyz_t<BS, 256>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else if (Z <= 512) launch_xyz_t<BS, 512>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
+	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
 	return true;
 }
 
@@ -1271,7 +1301,7 @@ extern "C" int gcmx_diag_tx2(unsigned long long* out) {  // 16 x 8 counters, the
 
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk, const FaceBC* faces, const char** kname,
-                      const HetMaterials* het, int xb0, int xb1, double* seam) {
+                      const HetMaterials* het, int xb0, int xb1) {
 	const char* dummy = nullptr;
 	const char** kn = kname ? kname : &dummy;
 	if (!fused_supported(g) || x1 <= x0) return false;
@@ -1279,21 +1309,21 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	if (het && !het_supported(g)) return false;
 	if (faces && faces->on && !fused_faces_supported(g)) return false;
 	if (faces && faces->ode_on && !(g.bs <= 2 && g.sizes[2] <= 512)) return false;  // k_fused_xyz has no epilogue
-	if (const int P = zs_part(g); P > 0 && seam && !het && !(faces && faces->on)) {
+	if (const int P = zs_part(g); P > 0 && !het && !(faces && faces->on)) {
 		bool kf0 = true;
 		for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
 		if (kf0 && same_axis(a[0], a[1]) && same_axis(a[0], a[2])) {
-			if (g.bs == 1) P == 256 ? launch_zs<1, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam)
-			               : launch_zs<1, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam);
-			else P == 256 ? launch_zs<2, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam)
-			              : launch_zs<2, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, seam);
+			if (g.bs == 1) P == 256 ? launch_zs<1, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn)
+			               : launch_zs<1, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn);
+			else P == 256 ? launch_zs<2, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn)
+			              : launch_zs<2, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn);
 			return true;
 		}
 	}
 	switch (g.bs) {
-	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
-	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
-	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het, seam);
+	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
+	case 2: return launch_xyz_bs<2>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
+	case 3: return launch_xyz_bs<3>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
 	default: return false;
 	}
 }
@@ -1328,10 +1358,6 @@ int zs_part(const Geo& g) {
 	return Z > 512 && Z % 512 == 0 ? 512 : 0;
 }
 
-long long seam_doubles(const Geo& g) {
-	const int P = zs_part(g);
-	return P ? (long long)(g.sizes[2] / P - 1) * 9 * g.sizes[0] * g.sizes[1] * 4 * g.bs : 0;
-}
 
 bool het_supported(const Geo& g) {
 	const int Z = g.sizes[2];

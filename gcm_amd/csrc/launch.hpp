@@ -161,10 +161,8 @@ bool het_supported(const Geo& g);
 // `kname`: set to the launched instance's symbol (a static string).
 // [xb0, xb1): an optional second plane range (xb0 >= x1) covered by the same
 // launch (the X-slab boundary sides; two launches on the k_fused_xyz path).
-// `seam`: scratch of seam_doubles(g) doubles (null: none) for the z-split step
-// of rows longer than 512 (k_step_tx2<..., ZS> + k_zseam); without it such rows
-// take the one-plane k_fused_xyz.
-long long seam_doubles(const Geo& g);
+// Rows longer than 512 (a multiple of 512), uniform medium, no y/z faces: the
+// z-split step (k_step_tx2<..., ZS> + k_zseam); else the one-plane k_fused_xyz.
 int zs_part(const Geo& g);  // lanes per part of the z-split step, 0: rows are not split
 int step_free_cus(const Geo& g, int x0, int x1, int req_chunk, int cus = -1);  // cus <= 0: the device's
 // Two builds of the one-pass step kernels (kernels_xyz.hip): xyz_exact keeps the
@@ -174,13 +172,13 @@ namespace xyz_exact {
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,
                       const char** kname = nullptr, const HetMaterials* het = nullptr, int xb0 = 0,
-                      int xb1 = 0, double* seam = nullptr);
+                      int xb1 = 0);
 }
 namespace xyz_fma {
 bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0,
                       int x1, hipStream_t st, int chunk = 0, const FaceBC* faces = nullptr,
                       const char** kname = nullptr, const HetMaterials* het = nullptr, int xb0 = 0,
-                      int xb1 = 0, double* seam = nullptr);
+                      int xb1 = 0);
 }
 
 }  // namespace gcmx
