@@ -24,7 +24,7 @@ from tests.test_gpu_parity import (test_adhesion_contact_two_contexts_bitwise, t
                                    test_fused_step_3d, test_generic_stages_random_with_ghosts,
                                    test_heterogeneous_materials, test_heterogeneous_one_pass_step_matches_oracle,
                                    test_heterogeneous_step_ode_fused_equals_step_then_ode, test_split_stages_3d,
-                                   test_x_slabs_with_copy_halo_equal_single)
+                                   test_x_slabs_with_copy_halo_equal_single, test_zsplit_step_matches_oracle)
 from tests.test_gpu_slabs import test_local_group_fused_equals_whole, test_rccl_self_exchange  # noqa: F401
 
 pytestmark = pytest.mark.gpu
