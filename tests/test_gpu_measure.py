@@ -45,3 +45,26 @@ def test_bench_prints_one_json_line_with_rccl_self():
     assert len(pr) == 1 and pr[0]["halo_ms"] > 0 and pr[0]["transport"] == "halo_rccl"
     assert pr[0]["halo_posts_per_step"] == 1.0 and pr[0]["bytes_per_direction"] > 0
     assert "box" in pr[0] and "process_state" in d
+
+
+@pytest.mark.timeout(120)
+def test_bench_refuses_more_ranks_than_gpus():
+    """`bench.py --gpus N` without a launcher starts N ranks itself -- and on a
+    box with fewer than N GPUs it must fail before touching one, not measure a
+    single rank.  Skipped where N GPUs exist: there the same
+    command would really run N ranks, which this test does not start."""
+    import os
+    import subprocess
+    import sys
+    import torch
+    n = torch.cuda.device_count() + 1
+    if n <= 2:
+        n = 2
+    if torch.cuda.device_count() >= n:
+        pytest.skip("enough GPUs for a real multi-rank run")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--n", "64", "--steps", "1"],
+                       capture_output=True, text=True, timeout=100, cwd=root, env=env)
+    assert r.returncode != 0 and not r.stdout.strip()
+    assert "refusing to run fewer ranks" in r.stderr
