@@ -51,17 +51,12 @@ def test_bench_prints_one_json_line_with_rccl_self():
 def test_bench_refuses_more_ranks_than_gpus():
     """`bench.py --gpus N` without a launcher starts N ranks itself -- and on a
     box with fewer than N GPUs it must fail before touching one, not measure a
-    single rank.  Skipped where N GPUs exist: there the same
-    command would really run N ranks, which this test does not start."""
+    single rank.  N = the visible GPUs + 1, so no rank starts."""
     import os
     import subprocess
     import sys
     import torch
-    n = torch.cuda.device_count() + 1
-    if n <= 2:
-        n = 2
-    if torch.cuda.device_count() >= n:
-        pytest.skip("enough GPUs for a real multi-rank run")
+    n = max(2, torch.cuda.device_count() + 1)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--n", "64", "--steps", "1"],
