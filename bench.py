@@ -123,7 +123,16 @@ def self_launch(a) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else sys.stderr))
     log(f"bench.py: started {a.gpus} ranks (pids {[p.pid for p in procs]}), MASTER_PORT {port}")
+    import signal
     import threading
+
+    def forward(signum, _frame):  # a terminated job takes its ranks with it
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        sys.exit(128 + signum)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
     out = []
     reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
     reader.start()
@@ -680,6 +689,10 @@ def main():
             "config": {"workload": f"3-D isotropic elastic CubicGrid {N}^3, borderSize 2, "
                                    f"Courant 0.9, tau 0.9, one full time step (3 stages)",
                        "global_nodes": total_nodes, "slabs": world, "path": ctx.effective_path,
+                       # who started the ranks: bench.py itself (--gpus N, no launcher), a
+                       # launcher (torch.distributed.run), or one process
+                       "launch": ("bench.py self-launch" if os.environ.get("GCM_BENCH_SELF_LAUNCHED")
+                                  else "launcher" if "WORLD_SIZE" in os.environ else "single process"),
                        "parallelism": f"x-slab{world}" if world > 1 else
                                       ("single, RCCL self-exchange (one-rank communicator)" if a.rccl_self else "single"),
                        **({"rccl_channels_per_peer": ctx.comm_channels_per_peer} if world > 1 or a.rccl_self else {}),

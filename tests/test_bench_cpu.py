@@ -77,6 +77,7 @@ def test_bench_starts_its_own_ranks_without_a_launcher(tmp_path):
     ranks itself (no silent one-rank run)."""
     d = _run([sys.executable, "bench.py"] + ARGS, _env(tmp_path))
     _check(d, tmp_path)
+    assert d["config"]["launch"] == "bench.py self-launch"
 
 
 def test_bench_under_torch_distributed_run(tmp_path):
@@ -88,6 +89,7 @@ def test_bench_under_torch_distributed_run(tmp_path):
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
               "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py"] + ARGS, _env(tmp_path))
     _check(d, tmp_path)
+    assert d["config"]["launch"] == "launcher"
 
 
 def test_bench_parity_check_sees_a_missing_exchange(tmp_path):
