@@ -26,7 +26,9 @@ def readable(rocprof_name):
         return rocprof_name
     a = [x.strip() for x in m.group(2).split(",")]
     flags = ["KF0", "UNI", "FACES"]
-    out = a[:2] + [(f if v == "true" else "!" + f) for f, v in zip(flags, a[2:])]
+    out = a[:2] + [(f if v == "true" else "!" + f) for f, v in zip(flags, a[2:5])]
+    # k_step_tx2's HET and ZS flags appear in the library's name only when set
+    out += [f for f, v in zip(["HET", "ZS"], a[5:7]) if v == "true"]
     if "xyz_fma::" in rocprof_name:  # the contracted build (gcmx_set_fp_mode), as the library names it
         out.append("FMA")
     return f"{m.group(1)}<{', '.join(out)}>"
@@ -55,15 +57,22 @@ def main(prof_dir, out, n=512, lib_path="gcm_amd/lib/libgcmx.so", calib_json=Non
                            "read8_fetch_bytes": r8, "fetch_factor": ff,
                            "write8_write_bytes": w8, "write_factor": wf},
            "kernels": {}}
-    # bench.py's bucket "fused_xyz" is the one-pass step: k_step_tx2 (default) or k_fused_xyz
-    for short, frag in (("march_x", "k_march<0, 2"), ("fused_yz", f"k_fused_yz<2, {z}"),
-                        ("fused_xyz", f"k_fused_xyz<2, {z}"), ("fused_xyz", f"k_step_tx2<2, {z}")):
+    # bench.py's bucket "fused_xyz" is the one-pass step: k_step_tx2 (default) or
+    # k_fused_xyz; rows longer than 512 run the z split, k_step_tx2<2, 512, ..., ZS>
+    # followed by k_zseam in the same bucket, so their bytes add up
+    zsplit = ("fused_xyz", "k_step_tx2<2, 512, true, true, false, false, true>", "k_zseam<2")
+    for short, frag, *extra in (("march_x", "k_march<0, 2"), ("fused_yz", f"k_fused_yz<2, {z}"),
+                                ("fused_xyz", f"k_fused_xyz<2, {z}"), ("fused_xyz", f"k_step_tx2<2, {z}"),
+                                *((zsplit,) if n > 512 else ())):
         fks = [v for k, v in f.items() if frag in k]
         wks = [v for k, v in w.items() if frag in k]
         if not fks or not wks:
             continue
         fk = fks[0] * 1024 * ff
         wk = wks[0] * 1024 * wf
+        for e in extra:  # the seam kernel's bytes, same launches
+            fk += sum(v for k, v in f.items() if e in k) * 1024 * ff
+            wk += sum(v for k, v in w.items() if e in k) * 1024 * wf
         full = [k for k in f if frag in k][0]
         res["kernels"][short] = {"symbol": readable(full), "rocprof_name": full,
                                  "fetch_bytes_per_launch": fk, "write_bytes_per_launch": wk,
