@@ -311,6 +311,9 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_HET_AB
 #define GCMX_HET_AB 0
 #endif
+#ifndef GCMX_ZS_PAIRS_FIRST  // z split: block order pairs fastest (1) or the parts of a pair adjacent (0)
+#define GCMX_ZS_PAIRS_FIRST 0
+#endif
 
 #ifndef GCMX_TX2_UNROLL  // timing knob: row-loop unroll (5 = the window period: no window moves)
 #define GCMX_TX2_UNROLL 1
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		const int npair = npa + (nplanesb > 0 ? (nplanesb + pb + 1) / 2 : 0);
 		const int T = (int)gridDim.x, b = (int)blockIdx.x;
 		int p = xcd_order(b, T);
-		if constexpr (ZS) {  // the parts of one (pair, chunk) are neighbours in the order
+		if constexpr (ZS && !GCMX_ZS_PAIRS_FIRST) {  // the parts of one (pair, chunk) are neighbours in the order
 			zp = p % nz;
 			p /= nz;
 		}
@@ -472,8 +475,13 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		x = q < npa ? x0 - pa + 2 * q : xb0 - pb + 2 * (q - npa);
 		xbeg = q < npa ? x0 : xb0;
 		xend = q < npa ? x0 + nplanes : xb0 + nplanesb;
-		yb = (p / npair) * chunk;
-		rev = GCMX_TX2_ALT && ((p / npair) & 1);
+		int cidx = p / npair;  // chunk index
+		if constexpr (ZS && GCMX_ZS_PAIRS_FIRST) {  // pairs fastest, then parts, then chunks
+			zp = cidx % nz;
+			cidx /= nz;
+		}
+		yb = cidx * chunk;
+		rev = GCMX_TX2_ALT && (cidx & 1);
 	}
 	const bool one = x >= xbeg;  // node x is ours (else only x + 1 is)
 	const bool two = x + 1 < xend;
