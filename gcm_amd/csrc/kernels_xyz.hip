@@ -312,7 +312,7 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #define GCMX_HET_AB 0
 #endif
 #ifndef GCMX_ZS_PAIRS_FIRST  // z split: block order pairs fastest (1) or the parts of a pair adjacent (0)
-#define GCMX_ZS_PAIRS_FIRST 0
+#define GCMX_ZS_PAIRS_FIRST 1  // an XCD's concurrent blocks then cover twice the consecutive pairs: 1024^3 -1.2 % (profiles/r6/n)
 #endif
 
 #ifndef GCMX_TX2_UNROLL  // timing knob: row-loop unroll (5 = the window period: no window moves)
