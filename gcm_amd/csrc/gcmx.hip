@@ -1617,7 +1617,9 @@ gcmx_status ode_upload(gcmx_ctx* c, const std::vector<double>& f);
 // materials on the heterogeneous one-pass step (per-material factors, each
 // node's own read from LDS).  Call after build_tables (het_ok is per tau).
 bool ode_foldable(const gcmx_ctx* c, const StepOde& ode) {
-	if (!ode.on || c->bs > 2 || c->geo.sizes[2] > 512) return false;
+	// rows longer than 512: only the z split has the store epilogue (uniform medium)
+	if (!ode.on || c->bs > 2 || (c->geo.sizes[2] > 512 && !(!c->mat_d && zs_admissible(c->geo, c->iso))))
+		return false;
 	if (!c->mat_d) return ode.f.size() == 1;
 	return c->iso_het && c->het_ok && (int)ode.f.size() <= kHetMaxMaterials;
 }
@@ -1783,6 +1785,7 @@ gcmx_status step_faces_body(gcmx_ctx* c, double tau, const gcmx_face* faces, con
 	// free of PRESSURE (its trace needs components the fused ghosts do not form)
 	// and no face may hold ghosts written earlier but not refreshed now.
 	bool fused = D == 3 && effective_path(c) == GCMX_PATH_FUSED && fused_faces_supported(c->geo) &&
+	             (c->geo.sizes[2] <= 512 || (!c->mat_d && zs_admissible(c->geo, c->iso))) &&
 	             (c->faces_written & ~on) == 0 && (!c->iso_het || c->het_ok);
 	FaceBC fb{};
 	for (int f = 2; f < 6 && fused; f++) {
@@ -1928,6 +1931,7 @@ static gcmx_status step_face_map_body(gcmx_ctx* c, double tau, const gcmx_face_m
 	HIP_TRY(hipGetLastError());
 	c->last_ode_fused = false;
 	bool fused = D == 3 && effective_path(c) == GCMX_PATH_FUSED && fused_faces_supported(c->geo) &&
+	             (c->geo.sizes[2] <= 512 || (!c->mat_d && zs_admissible(c->geo, c->iso))) &&
 	             (c->faces_written & ~on) == 0 && (!c->iso_het || c->het_ok);
 	for (int f = 2; f < 2 * D && fused; f++)
 		if (m->used[f] & pressure) fused = false;

@@ -411,7 +411,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
     IsoAxis AZ_, int x0, int chunk, int nplanes, int xb0, int nplanesb, FaceBC fb,
     const IsoAxis* __restrict__ mtab, const uint8_t* __restrict__ mat) {
 	static_assert(!HET || (KF0 && UNI), "heterogeneous step: floor(q) = 0, Z == ZT, equal axes");
-	static_assert(!ZS || (UNI && !FACES && !HET), "z split: uniform medium, no faces");
+	static_assert(!ZS || (UNI && !HET), "z split: uniform medium");
 	const IsoAxis& AY = UNI ? AX : AY_;
 	const IsoAxis& AZ = UNI ? AX : AZ_;
 	constexpr unsigned WMX = iso_window(0);
@@ -502,6 +502,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const Planes src(in + pbase, g.cs);
 	const PlanesW out_p(outl + pbase, g.cs);
 	const unsigned zpart = ZS ? (unsigned)(zp * ZT) : 0u;      // ZS: first column of this part
+	const int zg = (int)zpart + zc;                            // the lane's column in the row
 	const unsigned lv = (zpart + (unsigned)zc) * 8u, sv = (zpart + zo) * 8u;  // per-lane byte offsets
 	const unsigned pxm = plane - (unsigned)BS * stx;      // plane x - BS, row 0, column 0
 	auto ldx = [&](int j, int k, int r) {
@@ -785,7 +786,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	auto mirror_slot = [&](int k, int ks, int f) {
 #pragma unroll
 		for (int t = 0; t < 2; t++) {
-			const GhostRule gr = ghost_rule(f, t, zc, WMY);
+			const GhostRule gr = ghost_rule(f, t, zg, WMY);
 #pragma unroll
 			for (int q = 0; q < NWY; q++) {
 				double v = 0.0;
@@ -861,7 +862,11 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 		const int wu = __builtin_amdgcn_readfirstlane(z >> 6);
 #pragma unroll
 		for (int side = 0; side < 2; side++) {
-			const int lo = side ? Z - 1 - BS : 1, hi = side ? Z - 2 : BS;
+			// ZS: the z- face lies in the first part, the z+ face in the last, at
+			// lanes of that part (Zl: the part's row length)
+			const int Zl = ZS ? ZT : Z;
+			if (ZS && (side ? zp != nz - 1 : zp != 0)) continue;
+			const int lo = side ? Zl - 1 - BS : 1, hi = side ? Zl - 2 : BS;
 			if (!((fb.on >> (2 + side)) & 1u) || wu * 64 > hi || wu * 64 + 63 < lo) continue;
 			if (z < lo || z > hi) continue;
 #pragma unroll
@@ -895,7 +900,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			if constexpr (FACES)  // z ghosts: wave 0's left halo, the last wave's right halo
 				z_ghosts(y, yv, [&](int side, int t, int q, double v) {
 					if (side == 0) rg[0][t][q][BS - z] = v;
-					else rg[NW - 1][t][q][BS + 2 * (Z - 1) - z - 64 * (NW - 1)] = v;
+					else rg[NW - 1][t][q][BS + 2 * ((ZS ? ZT : Z) - 1) - z - 64 * (NW - 1)] = v;
 				});
 			// edges in LDS before the counter says so (LDS only: global memory keeps flowing)
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1065,10 +1070,16 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 // shuffles), the folded ODE factor, 9 stores.  Rows: `chunk` per block, the
 // 2*BS-row prologue recomputed.  Reads the 4*BS columns' neighbourhoods (mostly
 // L2), writes 2*BS columns per cut: at 1024^3 0.4 % of the step's bytes.
-template <int BS, bool KF0>
+//
+// FACES: y-face conditions as the one-pass step forms them (FaceBC, uniform or a
+// per-node map): a window row outside [0, Y) is the mirrored inner row with the
+// condition's components set to -inner + 2 f(t) (BorderConditions.hpp:94-114).
+template <int BS, bool KF0, bool FACES>
 __global__ __launch_bounds__(256) void k_zseam(const double* __restrict__ in, double* __restrict__ outl, Geo g,
                                                 IsoAxis A, int x0, int nplanes, int xb0, int nplanesb, int zt,
-                                                int chunk, unsigned ode_on, double ode) {
+                                                int chunk, FaceBC fb) {
+	const unsigned ode_on = fb.ode_on;
+	const double ode = fb.ode;
 	constexpr int NC = 4 * BS, PB = 256 / NC, W = 2 * BS + 1;
 	const int Y = g.sizes[1], ncut = g.sizes[2] / zt - 1;
 	const int nch = (Y + chunk - 1) / chunk;
@@ -1092,6 +1103,36 @@ __global__ __launch_bounds__(256) void k_zseam(const double* __restrict__ in, do
 		    A, [&](int j, int oo) { return in[j * cs + o + oo * stx]; }, [&](int j) { return in[j * cs + o]; }, xr);
 	};
 	double win[9][W];
+	// window slot k := the ghost of y face f mirrored from slot ks (runtime slot
+	// indices resolved by compile-time selects, as k_step_tx2's mirror_slot)
+	auto mirror = [&](int k, int ks, int f) {
+		unsigned mask;
+		bool none = false;
+		double two[9];
+		if (fb.map[f]) {
+			const unsigned cnd = fb.map[f][(size_t)x * g.sizes[2] + z];
+			none = cnd == kNoFaceCond;
+			const FaceCond& fc = fb.conds[none ? 0u : cnd];
+			mask = none ? 0u : fc.mask;
+#pragma unroll
+			for (int j = 0; j < 9; j++) two[j] = none ? 0.0 : fc.two_v[j];
+		} else {
+			mask = fb.mask[f];
+#pragma unroll
+			for (int j = 0; j < 9; j++) two[j] = fb.two_v[f][j];
+		}
+#pragma unroll
+		for (int j = 0; j < 9; j++) {
+			double v = 0.0;
+#pragma unroll
+			for (int kk = 0; kk < W; kk++)
+				if (kk == ks) v = win[j][kk];
+			const double gv = none ? 0.0 : ((mask >> j) & 1u) ? -v + two[j] : v;
+#pragma unroll
+			for (int kk = 0; kk < W; kk++)
+				if (kk == k) win[j][kk] = gv;
+		}
+	};
 #pragma unroll
 	for (int k = 0; k < W; k++) {
 		double xr[9];
@@ -1102,6 +1143,16 @@ __global__ __launch_bounds__(256) void k_zseam(const double* __restrict__ in, do
 			for (int j = 0; j < 9; j++) xr[j] = 0.0;
 #pragma unroll
 		for (int j = 0; j < 9; j++) win[j][k] = xr[j];
+	}
+	if constexpr (FACES) {  // ghost rows of the prologue window: mirrors of inner rows
+		if (fb.on & 3u) {
+#pragma unroll
+			for (int k = 0; k < W; k++) {
+				const int r = yb - BS + k;
+				const int f = r < 0 ? 0 : 1, ks = BS + ((r < 0 ? -r : 2 * (Y - 1) - r) - yb);
+				if ((r < 0 || r >= Y) && ((fb.on >> f) & 1u) && ks >= 0 && ks < W) mirror(k, ks, f);
+			}
+		}
 	}
 	const bool mine = valid && c >= BS && c < 3 * BS;  // the columns whose Z stage the parts left
 	const int lane = (int)(threadIdx.x & 63);
@@ -1132,6 +1183,12 @@ __global__ __launch_bounds__(256) void k_zseam(const double* __restrict__ in, do
 			for (int j = 0; j < 9; j++) xr[j] = 0.0;
 #pragma unroll
 		for (int j = 0; j < 9; j++) win[j][W - 1] = xr[j];
+		if constexpr (FACES) {  // the entering row is a y+ ghost row: the mirror of an inner row
+			if (r >= Y && ((fb.on >> 1) & 1u)) {
+				const int ks = BS + (2 * (Y - 1) - r) - (y + 1);
+				if (ks >= 0 && ks < W) mirror(W - 1, ks, 1);
+			}
+		}
 	}
 }
 
@@ -1198,8 +1255,8 @@ static int xyz_chunk_for(int Y, int nplanes, int req, int start = GCMX_XYZ_CHUNK
 }
 
 // z split (k_step_tx2<BS, P, ..., ZS> + k_zseam): parts of P lanes, uniform
-// medium (equal axes, floor(q) = 0), no y/z faces.
-template <int BS, int P>
+// medium (equal axes, floor(q) = 0); FACES: the y/z face conditions.
+template <int BS, int P, bool FACES>
 static void launch_zs(const double* in, double* out, const Geo& g, const IsoAxis* a, int x0, int x1, int xb0, int xb1,
                       hipStream_t st, int req_chunk, const FaceBC* fb, const char** kname) {
 	const int nz = g.sizes[2] / P, nb = xb1 > xb0 ? xb1 - xb0 : 0;
@@ -1211,14 +1268,14 @@ static void launch_zs(const double* in, double* out, const Geo& g, const IsoAxis
 	const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair * nz);
 	const FaceBC none{};
 	const FaceBC& f = fb ? *fb : none;
-	hipLaunchKernelGGL((k_step_tx2<BS, P, true, true, false, false, true>), grid, dim3(P), 0, st, in, out, g, a[0],
+	hipLaunchKernelGGL((k_step_tx2<BS, P, true, true, FACES, false, true>), grid, dim3(P), 0, st, in, out, g, a[0],
 	                   a[1], a[2], x0, chunk, x1 - x0, xb0, nb, f, nullptr, nullptr);
 	// the cut columns: 256 / (4 BS) planes per block, 64-row chunks
 	const int np = (x1 - x0) + nb, pb = 256 / (4 * BS), sch = std::min(64, g.sizes[1]);
 	const long long nblk = (long long)((np + pb - 1) / pb) * (nz - 1) * ((g.sizes[1] + sch - 1) / sch);
-	hipLaunchKernelGGL((k_zseam<BS, true>), dim3((unsigned)nblk), dim3(256), 0, st, in, out, g, a[0], x0, x1 - x0, xb0,
-	                   nb, P, sch, f.ode_on, f.ode);
-	*kname = tx2_name<BS, P, true, true, false, false, true>();
+	hipLaunchKernelGGL((k_zseam<BS, true, FACES>), dim3((unsigned)nblk), dim3(256), 0, st, in, out, g, a[0], x0,
+	                   x1 - x0, xb0, nb, P, sch, f);
+	*kname = tx2_name<BS, P, true, true, FACES, false, true>();
 }
 
 template <int BS, int ZT>
@@ -1315,18 +1372,24 @@ bool launch_fused_xyz(const double* in, double* out, const Geo& g, const IsoAxis
 	if (!fused_supported(g) || x1 <= x0) return false;
 	if (xb1 > xb0 && (xb0 < x1 || xb1 > g.sizes[0])) return false;  // range B after range A
 	if (het && !het_supported(g)) return false;
-	if (faces && faces->on && !fused_faces_supported(g)) return false;
-	if (faces && faces->ode_on && !(g.bs <= 2 && g.sizes[2] <= 512)) return false;  // k_fused_xyz has no epilogue
-	if (const int P = zs_part(g); P > 0 && !het && !(faces && faces->on)) {
-		bool kf0 = true;
-		for (int s = 0; s < 3; s++) kf0 = kf0 && a[s].kf1 == 0 && a[s].kf2 == 0;
-		if (kf0 && same_axis(a[0], a[1]) && same_axis(a[0], a[2])) {
-			if (g.bs == 1) P == 256 ? launch_zs<1, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn)
-			               : launch_zs<1, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn);
-			else P == 256 ? launch_zs<2, 256>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn)
-			              : launch_zs<2, 512>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn);
-			return true;
-		}
+	// the z split takes rows longer than 512 (and GCMX_ZS_PART's): uniform medium,
+	// floor(q) = 0 -- then with face conditions and the folded ODE too
+	const bool zs = !het && zs_admissible(g, a);
+	if (faces && faces->on && !(fused_faces_supported(g) && (g.sizes[2] <= 512 || zs))) return false;
+	if (faces && faces->ode_on && !(g.bs <= 2 && (g.sizes[2] <= 512 || zs))) return false;  // k_fused_xyz has no epilogue
+	if (zs) {
+		const int P = zs_part(g);
+		const bool fc = faces && faces->on;
+		auto go = [&](auto F) {
+			constexpr bool FC = decltype(F)::value;
+			if (g.bs == 1) P == 256 ? launch_zs<1, 256, FC>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn)
+			               : launch_zs<1, 512, FC>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn);
+			else P == 256 ? launch_zs<2, 256, FC>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn)
+			              : launch_zs<2, 512, FC>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn);
+		};
+		if (fc) go(std::true_type{});
+		else go(std::false_type{});
+		return true;
 	}
 	switch (g.bs) {
 	case 1: return launch_xyz_bs<1>(in, out, g, a, x0, x1, xb0, xb1, st, chunk, faces, kn, het);
@@ -1373,8 +1436,15 @@ bool het_supported(const Geo& g) {
 }
 
 bool fused_faces_supported(const Geo& g) {
-	return fused_supported(g) && g.bs <= 2 && g.sizes[2] <= 512 && g.sizes[1] >= 2 * g.bs + 2 &&
+	return fused_supported(g) && g.bs <= 2 && (g.sizes[2] <= 512 || zs_part(g) > 0) && g.sizes[1] >= 2 * g.bs + 2 &&
 	       g.sizes[2] >= 2 * g.bs + 2;
+}
+
+bool zs_admissible(const Geo& g, const IsoAxis* a) {
+	if (zs_part(g) <= 0) return false;
+	for (int s = 0; s < 3; s++)
+		if (a[s].kf1 != 0 || a[s].kf2 != 0) return false;
+	return GCMX_XYZ_NS::same_axis(a[0], a[1]) && GCMX_XYZ_NS::same_axis(a[0], a[2]);
 }
 
 #endif

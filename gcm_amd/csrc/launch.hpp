@@ -143,7 +143,8 @@ struct FaceTables {
 };
 void launch_set_face_tables(BorderQ* bq_d, FaceCond* fc_d, const FaceTables& t, hipStream_t st);
 // The one-pass step with FaceBC face conditions (on != 0) needs bs <= 2, Z <= 512
-// and Y, Z >= 2*bs + 2; a FaceBC with on == 0 carries only the ODE factor.
+// or the z split (then also zs_admissible) and Y, Z >= 2*bs + 2; a FaceBC with
+// on == 0 carries only the ODE factor.
 bool fused_faces_supported(const Geo& g);
 // One pass per time step: X, Y, Z stages of planes [x0, x1), `a` = the three axes.
 // `chunk`: y rows per block (0 = automatic, kernels_xyz.hip: xyz_chunk_for).
@@ -164,6 +165,9 @@ bool het_supported(const Geo& g);
 // Rows longer than 512 (a multiple of 512), uniform medium, no y/z faces: the
 // z-split step (k_step_tx2<..., ZS> + k_zseam); else the one-plane k_fused_xyz.
 int zs_part(const Geo& g);  // lanes per part of the z-split step, 0: rows are not split
+// The z split runs for these axis tables (uniform medium, floor(q) = 0): then the
+// one-pass step takes rows longer than 512 with face conditions and the folded ODE.
+bool zs_admissible(const Geo& g, const IsoAxis* a);
 int step_free_cus(const Geo& g, int x0, int x1, int req_chunk, int cus = -1);  // cus <= 0: the device's
 // Two builds of the one-pass step kernels (kernels_xyz.hip): xyz_exact keeps the
 // reference's roundings (bitwise), xyz_fma contracts multiply-adds

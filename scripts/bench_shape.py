@@ -9,6 +9,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import gcm_amd  # noqa: E402
@@ -19,7 +20,22 @@ ap.add_argument("shapes", nargs="+")
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--rows", type=int, default=0)
+ap.add_argument("--free", action="store_true", help="free surfaces on all six faces (gcmx_step_faces)")
 a = ap.parse_args()
+Q = gcm_amd.gcmx.QUANTITY_CODES if hasattr(gcm_amd.gcmx, "QUANTITY_CODES") else None
+FREE = None
+if a.free:  # ndi.hpp:30-55: the stress components on each face's normal set to zero
+    q = Q
+    FREE = [[(q["Sxx"], 0.0), (q["Sxy"], 0.0), (q["Sxz"], 0.0)]] * 2 + \
+           [[(q["Syy"], 0.0), (q["Sxy"], 0.0), (q["Syz"], 0.0)]] * 2 + \
+           [[(q["Szz"], 0.0), (q["Sxz"], 0.0), (q["Syz"], 0.0)]] * 2
+
+
+def step(c):
+    if FREE is not None:
+        c.step_faces(0.9, FREE)
+    else:
+        c.step(0.9)
 U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
 for sh in a.shapes:
     X, Y, Z = (int(v) for v in sh.split(","))
@@ -29,20 +45,24 @@ for sh in a.shapes:
         c.set_schedule(gcm_amd.SCHED_AUTO, a.rows)
     c.fill_random([X, Y, Z], 0x5EED)
     for _ in range(2):
-        c.step(0.9)
+        step(c)
     c.sync()
     c.profile(True)
-    avgs = []
+    avgs, walls = [], []
     for _ in range(a.reps):
         c.profile_reset()
+        t0 = time.perf_counter()
         for _ in range(a.steps):
-            c.step(0.9)
+            step(c)
         c.sync()
-        k = c.profile_read()["fused_xyz"]
+        walls.append((time.perf_counter() - t0) / a.steps * 1e3)
+        prof = c.profile_read()
+        k = prof["fused_xyz"] if "fused_xyz" in prof else max(prof.values(), key=lambda v: v["total_ms"])
         avgs.append(k["total_ms"] / k["launches"])
     ms = sorted(avgs)[len(avgs) // 2]
     n = X * Y * Z
-    print(json.dumps({"shape": [X, Y, Z], "kernel_ms": round(ms, 4), "frac": round(144 * n / (ms * 1e-3) / 8e12, 4),
+    print(json.dumps({"shape": [X, Y, Z], "free": a.free, "path": c.last_path,
+                      "step_ms": round(sorted(walls)[len(walls) // 2], 4), "kernel_ms": round(ms, 4), "frac": round(144 * n / (ms * 1e-3) / 8e12, 4),
                       "ns_per_node": round(ms * 1e6 / n, 4), "kernel": k["kernel"],
                       "alloc": c.layer_info()["alloc"]}), flush=True)
     c.close()

@@ -253,8 +253,8 @@ def test_step_ode_fused_equals_step_then_ode(G, faces):
     fc = [[(q["Sxx"], 0.0), (q["Sxy"], 0.0), (q["Sxz"], 0.0)], None,
           [(q["Syy"], -0.3), (q["Syz"], 0.0)], [(q["Vy"], 0.1)],
           [(q["Szz"], 0.0), (q["Sxz"], 0.0), (q["Syz"], 0.0)], None] if faces else None
-    for tau0, fused in ((3.0, True), (0.0, True)):
-        b = oracle_body(3, 2, [6, 20, 32])
+    for tau0, fused, sizes in ((3.0, True, [6, 20, 32]), (0.0, True, [6, 20, 32]), (3.0, True, [5, 12, 1024])):
+        b = oracle_body(3, 2, sizes)  # Z = 1024: the z split's epilogue (k_step_tx2 and k_zseam)
         random_state(b, seed=11, ghosts=False)
         a, c = context_for(b), context_for(b)
         for _ in range(3):

@@ -86,6 +86,16 @@ FACE_CASES = {
     "pressure_y": (2, [6, 20, 40], [(1, -1, {"PRESSURE": lambda t: 0.25}), (2, 0, free(2))], 0.9, "split"),
     # PRESSURE on an x face is filled in memory: still one pass
     "pressure_x": (2, [6, 20, 40], [(0, 1, {"PRESSURE": lambda t: 0.25}), (2, 0, free(2))], 0.9, "fused"),
+    # rows of 1024: the z split (two 512-lane parts, the cut columns by k_zseam)
+    # with the y faces in both kernels and the z faces in the first / last part
+    "z1024_free_all": (2, [5, 12, 1024], [(0, 0, free(0)), (1, 0, free(1)), (2, 0, free(2))], 0.9, "fused"),
+    "z1024_some": (2, [6, 10, 1024], [(1, 1, free(1, lambda t: 0.3 * math.sin(2 * t))),
+                                      (2, -1, free(2, lambda t: -0.2 + 0.1 * t)),
+                                      (1, -1, {"Vy": lambda t: 0.1, "Sxy": lambda t: 0.0}),
+                                      (0, -1, {"Vx": lambda t: 0.05})], 0.9, "fused"),
+    "z1024_bs1": (1, [4, 8, 1024], [(0, 0, free(0)), (1, 0, free(1)), (2, 0, free(2))], 0.9, "fused"),
+    # floor(q) = 1: no z split, so the per-stage path
+    "z1024_courant15": (2, [4, 8, 1024], [(1, 0, free(1)), (2, 0, free(2))], 1.5, "split"),
 }
 
 
@@ -345,6 +355,13 @@ PARTIAL_CASES = {
     "bs1": (1, [7, 12, 64], [
         (1, 0, ("box", (-1, -100, 10.5), (100, 100, 40.5)), free(1)),
         (2, 0, ("box", (2.5, 2.5, -100), (100, 100, 100)), free(2)),
+    ], 0.9, "fused"),
+    # rows of 1024 (z split): partial y faces across the cut columns (z 508-515)
+    # and on both parts, a partial z+ face in the last part
+    "z1024": (2, [6, 10, 1024], [
+        (1, -1, ("box", (-1, -1, 300.5), (100, 1, 700.5)), free(1)),
+        (1, 1, ("box", (2.5, 8, -1), (100, 100, 511.5)), free(1, lambda t: 0.2 + 0.1 * t)),
+        (2, 1, ("box", (-1, 3.5, -100), (100, 7.5, 2000)), {"Vz": lambda t: -0.1}),
     ], 0.9, "fused"),
 }
 
