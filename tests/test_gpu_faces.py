@@ -31,9 +31,10 @@ def G():
 
 
 def face_area(D, sizes, axis, side):
-    """An axis-aligned box holding exactly the nodes of one face (h = 1, start 0)."""
-    lo = [-1e3] * 3
-    hi = [1e3] * 3
+    """An axis-aligned box holding exactly the nodes of one face (h = 1, start 0;
+    the other axes unbounded for any grid here, rows of 1024 included)."""
+    lo = [-1e6] * 3
+    hi = [1e6] * 3
     c = 0.0 if side < 0 else float(sizes[axis] - 1)
     lo[axis], hi[axis] = c - 0.5, c + 0.5
     return ("box", tuple(lo), tuple(hi))
