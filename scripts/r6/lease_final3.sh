@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6, the end-of-round lease on the final build (final3: the z split with faces and the ODE fold;
+# Round 6, the end-of-round lease on the final build (final3: the z split with faces and the ODE fold):
 # box characterisation, the
 # full GPU suite, smoke, the default bench line, 256^3 and 1024^3 lines, the RCCL
 # self-exchange lines, simplex / 2-D / physics lines, and the rocprofv3 evidence
