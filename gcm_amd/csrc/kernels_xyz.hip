@@ -58,15 +58,20 @@ namespace GCMX_XYZ_NS {
 #ifndef GCMX_XYZ_UNROLL
 #define GCMX_XYZ_UNROLL 1
 #endif
+#ifndef GCMX_XYZ_MINWAVES_BS3  // borderSize 3 (tuning builds only: 4 was the round-5 value)
+#define GCMX_XYZ_MINWAVES_BS3 2
+#endif
 #ifndef GCMX_XYZ_TX2  // 1: k_step_tx2 (two x planes per thread) for borderSize <= 2, Z <= 512
 #define GCMX_XYZ_TX2 1
 #endif
 
+// borderSize 3 runs at 2 waves per SIMD: at 4 (128 VGPRs) its windows spill 97
+// VGPRs to scratch (profiles/r6/bs3_resource_usage.txt).
 // UNI: the launch has Z == ZT (no idle lanes) and the three axes' tables are
 // identical (isotropic medium, equal h): one IsoAxis in scalar registers for all
 // three stages and no idle-lane selects.
 template <int BS, int ZT, bool KF0, bool UNI>
-__global__ __launch_bounds__(ZT, GCMX_XYZ_MINWAVES) void k_fused_xyz(
+__global__ __launch_bounds__(ZT, BS >= 3 ? GCMX_XYZ_MINWAVES_BS3 : GCMX_XYZ_MINWAVES) void k_fused_xyz(
     const double* __restrict__ in, double* __restrict__ outl, Geo g, IsoAxis AX, IsoAxis AY_,
     IsoAxis AZ_, int x0, int chunk, int nplanes) {
 	const IsoAxis& AY = UNI ? AX : AY_;

@@ -20,6 +20,7 @@ ap.add_argument("shapes", nargs="+")
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--rows", type=int, default=0)
+ap.add_argument("--bs", type=int, default=2, help="borderSize (ghost depth)")
 ap.add_argument("--free", action="store_true", help="free surfaces on all six faces (gcmx_step_faces)")
 a = ap.parse_args()
 Q = gcm_amd.gcmx.QUANTITY_CODES if hasattr(gcm_amd.gcmx, "QUANTITY_CODES") else None
@@ -39,7 +40,7 @@ def step(c):
 U, U1, L = isotropic_elastic_matrices(3, 4.0, 2.0, 1.0)
 for sh in a.shapes:
     X, Y, Z = (int(v) for v in sh.split(","))
-    c = gcm_amd.Context(3, 2, [X, Y, Z], device=0)
+    c = gcm_amd.Context(3, a.bs, [X, Y, Z], device=0)
     c.set_materials(U[None], U1[None], L[None])
     if a.rows:
         c.set_schedule(gcm_amd.SCHED_AUTO, a.rows)
@@ -61,7 +62,7 @@ for sh in a.shapes:
         avgs.append(k["total_ms"] / k["launches"])
     ms = sorted(avgs)[len(avgs) // 2]
     n = X * Y * Z
-    print(json.dumps({"shape": [X, Y, Z], "free": a.free, "path": c.last_path,
+    print(json.dumps({"shape": [X, Y, Z], "bs": a.bs, "free": a.free, "path": c.last_path,
                       "step_ms": round(sorted(walls)[len(walls) // 2], 4), "kernel_ms": round(ms, 4), "frac": round(144 * n / (ms * 1e-3) / 8e12, 4),
                       "ns_per_node": round(ms * 1e6 / n, 4), "kernel": k["kernel"],
                       "alloc": c.layer_info()["alloc"]}), flush=True)
