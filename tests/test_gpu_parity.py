@@ -58,7 +58,7 @@ def test_split_stages_3d(G, bs, sizes):
 
 @pytest.mark.parametrize("bs,sizes", [(2, [12, 10, 70]), (2, [9, 150, 300]), (1, [4, 3, 64]),
                                       (3, [130, 7, 100]), (2, [5, 66, 520]), (3, [3, 5, 512]),
-                                      (3, [2, 4, 1024])])
+                                      (3, [3, 4, 1024])])
 def test_fused_step_3d(G, bs, sizes):
     """gcmx_step on the fused path (X march + fused Y/Z) == three oracle stages."""
     b = oracle_body(3, bs, sizes)
