@@ -290,6 +290,14 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	do {         \
 	} while (0)
 #endif
+#ifndef GCMX_TX2_BLKT  // tuning builds only: per-wave start / end times (s_memrealtime, 100 MHz) and the
+#define GCMX_TX2_BLKT 0  // CU of every block of the last k_step_tx2 launch (gcmx_diag_blk*)
+#endif
+#if GCMX_TX2_BLKT
+constexpr int kBlkMax = 8192;
+__device__ unsigned long long g_tx2_blk[kBlkMax][8][2];  // [block][wave][start, end]
+__device__ unsigned g_tx2_hw[kBlkMax];                   // HW_ID of the block's wave 0
+#endif
 
 // Timing knobs (A/B builds only; the defaults are the product): per-node face
 // maps compiled into the FACES ghosts; face values read from LDS instead of the
@@ -455,6 +463,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	__shared__ double flds[FACES && GCMX_TX2_FACE_LDS ? 4 : 1][9];  // 2 f(t) of the y/z faces
 
 	const int z = threadIdx.x;
+#if GCMX_TX2_BLKT
+	const unsigned long long blk_t0_ = __builtin_amdgcn_s_memrealtime();
+#endif
 	const int Y = g.sizes[1], Z = g.sizes[2];
 	int x, yb, xbeg, xend;
 	bool rev;  // this block marches its rows downwards (odd chunks, GCMX_TX2_ALT)
@@ -1055,6 +1066,14 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 #pragma unroll GCMX_TX2_UNROLL
 #endif
 	for (int it = 0; it < ye - yb; it++) row(REV ? ye - 1 - it : yb + it, it);
+#if GCMX_TX2_BLKT
+	if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)kBlkMax && threadIdx.x < 512) {
+		const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+		g_tx2_blk[blockIdx.x][threadIdx.x / 64][0] = blk_t0_;
+		g_tx2_blk[blockIdx.x][threadIdx.x / 64][1] = t1;
+		if (threadIdx.x == 0) g_tx2_hw[blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
+	}
+#endif
 #if GCMX_TX2_DIAG
 	if ((threadIdx.x & 63) == 0) {
 		const int wv = threadIdx.x / 64;
@@ -1360,6 +1379,21 @@ static bool launch_xyz_bs(const double* in, double* out, const Geo& g, const Iso
 	else launch_xyz_t<BS, 1024>(in, out, g, a, x0, x1, xb0, xb1, st, ch, fb, kn, het);
 	return true;
 }
+
+#if GCMX_TX2_BLKT
+// 8192 x 8 x 2 start / end times and 8192 HW_IDs of the last launch, then zeroed
+#if GCMX_FMA
+extern "C" int gcmx_diag_blk_fma(unsigned long long* t, unsigned* hw) {
+#else
+extern "C" int gcmx_diag_blk(unsigned long long* t, unsigned* hw) {
+#endif
+	if (hipDeviceSynchronize() != hipSuccess) return -1;
+	if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_tx2_blk), sizeof(g_tx2_blk)) != hipSuccess) return -1;
+	if (hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_tx2_hw), sizeof(g_tx2_hw)) != hipSuccess) return -1;
+	static unsigned long long zero[kBlkMax][8][2];
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_tx2_blk), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if GCMX_TX2_DIAG && !GCMX_FMA
 extern "C" int gcmx_diag_tx2(unsigned long long* out) {  // 16 x 8 counters, then reset
