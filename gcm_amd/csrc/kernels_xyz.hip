@@ -290,6 +290,9 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	do {         \
 	} while (0)
 #endif
+#ifndef GCMX_TX2_GEN2_DEFAULT  // old blocks' share of two generations' rows, percent (0: off; tx2_gen2)
+#define GCMX_TX2_GEN2_DEFAULT 0
+#endif
 #ifndef GCMX_TX2_BLKT  // tuning builds only: per-wave start / end times (s_memrealtime, 100 MHz) and the
 #define GCMX_TX2_BLKT 0  // CU of every block of the last k_step_tx2 launch (gcmx_diag_blk*)
 #endif
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	const unsigned long long blk_t0_ = __builtin_amdgcn_s_memrealtime();
 #endif
 	const int Y = g.sizes[1], Z = g.sizes[2];
-	int x, yb, xbeg, xend;
+	int x, yb, ye, xbeg, xend;
 	bool rev;  // this block marches its rows downwards (odd chunks, GCMX_TX2_ALT)
 	int zp = 0;                                    // ZS: this block's part of the z row
 	const int nz = ZS ? g.sizes[2] / ZT : 1;
@@ -487,21 +490,41 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			zp = p % nz;
 			p /= nz;
 		}
-		const int q = p % npair;
+		int q = p % npair;
+		int cidx = p / npair;  // chunk index
+		if (!ZS && chunk < 0) {
+			// Two generations (tx2_gen2): the launch is exactly two resident blocks per
+			// CU, and the first block dispatched to a CU (blocks [0, T/2)) runs ahead of
+			// its younger neighbour (oldest-first issue): old blocks take chunks of
+			// `co` rows, young ones `cy`.  Per generation, XCD k's blocks take the
+			// k-th contiguous run of (pair, chunk slot s) positions, pairs fastest;
+			// an old block runs chunk s, a young one chunk ncg + s.
+			const int co = (-chunk) & 0xFFFF, half = T >> 4;
+			const int j = b >> 3, gen = j >= half ? 1 : 0;
+			const int G = (b & 7) * half + (j - gen * half);
+			const int ncg = (T >> 1) / npair;  // chunks per generation
+			q = G % npair;
+			cidx = G / npair + gen * ncg;
+			const int cy = (-chunk) >> 16;
+			auto start = [&](int c) { return c <= ncg ? c * co : ncg * co + (c - ncg) * cy; };
+			yb = start(cidx);
+			ye = min(start(cidx + 1), Y);  // the host makes ncg (co + cy) == Y
+		}
 		x = q < npa ? x0 - pa + 2 * q : xb0 - pb + 2 * (q - npa);
 		xbeg = q < npa ? x0 : xb0;
 		xend = q < npa ? x0 + nplanes : xb0 + nplanesb;
-		int cidx = p / npair;  // chunk index
 		if constexpr (ZS && GCMX_ZS_PAIRS_FIRST) {  // pairs fastest, then parts, then chunks
 			zp = cidx % nz;
 			cidx /= nz;
 		}
-		yb = cidx * chunk;
+		if (ZS || chunk > 0) {
+			yb = cidx * chunk;
+			ye = min(yb + chunk, Y);
+		}
 		rev = GCMX_TX2_ALT && (cidx & 1);
 	}
 	const bool one = x >= xbeg;  // node x is ours (else only x + 1 is)
 	const bool two = x + 1 < xend;
-	const int ye = min(yb + chunk, Y);
 	const bool live = UNI || z < Z;
 	const int zc = live ? z : Z - 1;
 	const unsigned stx = (unsigned)g.stride[0];
@@ -1255,6 +1278,28 @@ static int tx2_chunk_for(int Y, int npair, int req, int slots) {
 	return Y < 16 ? Y : 16;
 }
 
+static int device_cus();
+// Two generations of rows (k_step_tx2's chunk < 0): when a launch is exactly two
+// resident blocks per CU, the block dispatched first to a CU finishes ~25 %
+// before its co-resident younger block (256^3: 0.40 against 0.51 ms,
+// profiles/r6/r), and the CU runs the rest at half occupancy.  Old blocks then
+// take `co` rows and young ones `cy` (co + cy = 2 Y / nchunk; GCMX_TX2_GEN2 =
+// the old share in percent, 0 = off).  Returns the kernel's chunk argument.
+static int tx2_gen2(int Y, int npair, int chunk, int T, int per_cu) {
+	static const int pct = [] {
+		const char* e = std::getenv("GCMX_TX2_GEN2");
+		return e ? std::atoi(e) : GCMX_TX2_GEN2_DEFAULT;
+	}();
+	if (pct <= 50 || pct >= 100 || per_cu != 2 || T != 2 * device_cus() || T % 16 || (T / 2) % npair) return chunk;
+	const int nchunk = T / npair;
+	if (Y % chunk || Y / chunk != nchunk) return chunk;
+	const int ncg = nchunk / 2, two = Y / ncg;  // rows of one old + one young chunk
+	if (two * ncg != Y) return chunk;
+	const int co = (two * pct + 50) / 100, cy = two - co;
+	if (cy < 2 * 2 + 1 || co > 0xFFFF) return chunk;
+	return -(co | (cy << 16));
+}
+
 static int device_cus() {
 	static int n = [] {
 		int dev = 0, v = 0;
@@ -1319,12 +1364,13 @@ static void launch_xyz_t(const double* in, double* out, const Geo& g, const IsoA
 			// resident blocks: 2 waves per SIMD (<= 256 VGPRs), i.e. 512 / ZT per CU
 			const int chunk = tx2_chunk_for(g.sizes[1], npair, req_chunk, device_cus() * (512 / ZT));
 			const dim3 grid(((g.sizes[1] + chunk - 1) / chunk) * npair);
+			const int cparam = req_chunk > 0 ? chunk : tx2_gen2(g.sizes[1], npair, chunk, (int)grid.x, 512 / ZT);
 			const FaceBC none{};
 			const FaceBC& f = fb ? *fb : none;
 			const IsoAxis* mt = het ? het->tab : nullptr;
 			const uint8_t* mi = het ? het->ids : nullptr;
 			auto go = [&](auto K, const char* name) {
-				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, chunk, x1 - x0, xb0,
+				hipLaunchKernelGGL(K, grid, dim3(ZT), 0, st, in, out, g, a[0], a[1], a[2], x0, cparam, x1 - x0, xb0,
 				                   nb, f, mt, mi);
 				*kname = name;
 			};
