@@ -291,7 +291,7 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	} while (0)
 #endif
 #ifndef GCMX_TX2_GEN2_DEFAULT  // old blocks' share of two generations' rows, percent (0: off; tx2_gen2)
-#define GCMX_TX2_GEN2_DEFAULT 0
+#define GCMX_TX2_GEN2_DEFAULT 64  // 256^3: 0.530-0.540 against 0.547-0.559 ms off, profiles/r6/s
 #endif
 #ifndef GCMX_TX2_BLKT  // tuning builds only: per-wave start / end times (s_memrealtime, 100 MHz) and the
 #define GCMX_TX2_BLKT 0  // CU of every block of the last k_step_tx2 launch (gcmx_diag_blk*)

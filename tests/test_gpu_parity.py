@@ -374,6 +374,35 @@ def test_full_size_256_paths_agree_and_match_oracle(G):
     assert np.array_equal(b.inner_view(outs[G.PATH_FUSED]), b.inner_view())
 
 
+@pytest.mark.parametrize("het", [False, True])
+def test_two_generation_rows_match_oracle(G, het):
+    """A launch of exactly two resident blocks per CU ([256, 64, 256]: 128 plane
+    pairs x 4 chunks of 16 rows = 512 blocks on 256 CUs) takes the two-generation
+    row split (old blocks 20 rows, young 12; kernels_xyz.hip tx2_gen2), uniform
+    and per-node media: 2 steps == the oracle, bitwise."""
+    import torch
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("the split is sized for 256 CUs")
+    sizes = [256, 64, 256]
+    mats = ((4.0, 2.0, 1.0), (1.0, 2.0, 0.8)) if het else None
+    b = oracle_body(3, 2, sizes, materials=mats, courant=0.9) if het else oracle_body(3, 2, sizes)
+    if het:
+        its = b.inner_indices()
+        b.mat_id[b.flat_index(its)] = np.where(its[:, 0] < sizes[0] // 2, 0, 1).astype(np.uint8)
+    random_state(b, seed=11, ghosts=False)
+    ctx = context_for(b)
+    assert ctx.effective_path == "fused"
+    tau = 0.9 / np.sqrt((3.0 + 6.0) / 2.5) if het else 0.9
+    ctx.profile(True)
+    for step in range(2):
+        for s in range(3):
+            b.stage(s, tau, 16)
+        ctx.step(tau)
+        assert_same(ctx, b, f"gen2 het={het} step {step}")
+    assert "k_step_tx2<2, 256" in ctx.profile_read()["fused_xyz"]["kernel"]
+    ctx.close()
+
+
 @pytest.mark.slow
 @pytest.mark.timeout(900)
 def test_full_size_512_step_matches_oracle(G):
