@@ -379,10 +379,8 @@ def test_two_generation_rows_match_oracle(G, het):
     """A launch of exactly two resident blocks per CU ([256, 64, 256]: 128 plane
     pairs x 4 chunks of 16 rows = 512 blocks on 256 CUs) takes the two-generation
     row split (old blocks 20 rows, young 12; kernels_xyz.hip tx2_gen2), uniform
-    and per-node media: 2 steps == the oracle, bitwise."""
-    import torch
-    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
-        pytest.skip("the split is sized for 256 CUs")
+    and per-node media: 2 steps == the oracle, bitwise.  (On a device with another
+    CU count the launch keeps equal chunks; the comparison holds either way.)"""
     sizes = [256, 64, 256]
     mats = ((4.0, 2.0, 1.0), (1.0, 2.0, 0.8)) if het else None
     b = oracle_body(3, 2, sizes, materials=mats, courant=0.9) if het else oracle_body(3, 2, sizes)
