@@ -4,6 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/r6/t
 mkdir -p $OUT
+for st in fresh after_import after_ctx torch_first; do timeout -k 10 120 python scripts/r6/probe_torch.py $st 2>&1 | tail -n 6; done
 timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_parity.py -k "two_generation or full_size_256 or heterogeneous_one_pass" > $OUT/pytest.txt 2>&1; rc=$?; echo "pytest rc=$rc"; tail -n 1 $OUT/pytest.txt
 [ $rc -eq 0 ] || exit $rc
