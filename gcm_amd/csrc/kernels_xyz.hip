@@ -293,6 +293,20 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 #ifndef GCMX_TX2_GEN2_DEFAULT  // old blocks' share of two generations' rows, percent (0: off; tx2_gen2)
 #define GCMX_TX2_GEN2_DEFAULT 64  // 256^3: 0.530-0.540 against 0.547-0.559 ms off, profiles/r6/s
 #endif
+#ifndef GCMX_TX2_PRIO  // tuning builds only: wave priority while a row's loads are issued (s_setprio)
+#define GCMX_TX2_PRIO 0
+#endif
+#if GCMX_TX2_PRIO
+#define TX2_PRIO_HI() __builtin_amdgcn_s_setprio(GCMX_TX2_PRIO)
+#define TX2_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define TX2_PRIO_HI() \
+	do {              \
+	} while (0)
+#define TX2_PRIO_LO() \
+	do {              \
+	} while (0)
+#endif
 #ifndef GCMX_TX2_BLKT  // tuning builds only: per-wave start / end times (s_memrealtime, 100 MHz) and the
 #define GCMX_TX2_BLKT 0  // CU of every block of the last k_step_tx2 launch (gcmx_diag_blk*)
 #endif
@@ -769,8 +783,10 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	auto x_stage = [&](const XPre& pre, int r, double (&xr)[2][9], unsigned key) {
 		PairWin wc;
 		double cv[2][9];
+		TX2_PRIO_HI();
 		pair_load(P2{}, wc, r);
 		cv_load(cv, r);
+		TX2_PRIO_LO();
 		sched_fence();
 		if constexpr (HET) {
 			const unsigned m0 = key & 255u, m1 = key >> 8;
@@ -1064,7 +1080,9 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 			sched_fence();
 		} else {  // loads older than this row's stores
 			sched_fence();
+			TX2_PRIO_HI();
 			x_load_ahead(pre, rn);
+			TX2_PRIO_LO();
 			sched_fence();
 		}
 		TX2_T(6);
