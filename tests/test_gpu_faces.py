@@ -97,6 +97,11 @@ FACE_CASES = {
     "z1024_bs1": (1, [4, 8, 1024], [(0, 0, free(0)), (1, 0, free(1)), (2, 0, free(2))], 0.9, "fused"),
     # floor(q) = 1: no z split, so the per-stage path
     "z1024_courant15": (2, [4, 8, 1024], [(1, 0, free(1)), (2, 0, free(2))], 1.5, "split"),
+    # 512 blocks on 256 CUs: the two-generation row split (old blocks 20 rows,
+    # young 12) with y faces on the first / last chunks
+    "gen2_some": (2, [256, 64, 256], [(1, 1, free(1, lambda t: 0.3 * math.sin(2 * t))),
+                                      (1, -1, {"Vy": lambda t: 0.1, "Sxy": lambda t: 0.0}),
+                                      (2, 0, free(2)), (0, -1, {"Vx": lambda t: 0.05})], 0.9, "fused"),
 }
 
 
