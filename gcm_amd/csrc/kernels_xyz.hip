@@ -307,9 +307,6 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	do {              \
 	} while (0)
 #endif
-#ifndef GCMX_ZSEAM_ROWS_DEFAULT  // rows per k_zseam block (env GCMX_ZSEAM_ROWS overrides, >= 8)
-#define GCMX_ZSEAM_ROWS_DEFAULT 64
-#endif
 #ifndef GCMX_TX2_BLKT  // tuning builds only: per-wave start / end times (s_memrealtime, 100 MHz) and the
 #define GCMX_TX2_BLKT 0  // CU of every block of the last k_step_tx2 launch (gcmx_diag_blk*)
 #endif
@@ -1360,13 +1357,8 @@ static void launch_zs(const double* in, double* out, const Geo& g, const IsoAxis
 	const FaceBC& f = fb ? *fb : none;
 	hipLaunchKernelGGL((k_step_tx2<BS, P, true, true, FACES, false, true>), grid, dim3(P), 0, st, in, out, g, a[0],
 	                   a[1], a[2], x0, chunk, x1 - x0, xb0, nb, f, nullptr, nullptr);
-	// the cut columns: 256 / (4 BS) planes per block, GCMX_ZSEAM_ROWS-row chunks
-	static const int zrows = [] {
-		const char* e = std::getenv("GCMX_ZSEAM_ROWS");
-		const int v = e ? std::atoi(e) : 0;
-		return v >= 8 ? v : GCMX_ZSEAM_ROWS_DEFAULT;
-	}();
-	const int np = (x1 - x0) + nb, pb = 256 / (4 * BS), sch = std::min(zrows, g.sizes[1]);
+	// the cut columns: 256 / (4 BS) planes per block, 64-row chunks
+	const int np = (x1 - x0) + nb, pb = 256 / (4 * BS), sch = std::min(64, g.sizes[1]);
 	const long long nblk = (long long)((np + pb - 1) / pb) * (nz - 1) * ((g.sizes[1] + sch - 1) / sch);
 	hipLaunchKernelGGL((k_zseam<BS, true, FACES>), dim3((unsigned)nblk), dim3(256), 0, st, in, out, g, a[0], x0,
 	                   x1 - x0, xb0, nb, P, sch, f);
