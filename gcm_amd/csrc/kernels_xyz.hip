@@ -307,6 +307,9 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	do {              \
 	} while (0)
 #endif
+#ifndef GCMX_TX2_ZPERM  // tuning builds only: SIMD partners hold neighbouring z blocks
+#define GCMX_TX2_ZPERM 0
+#endif
 #ifndef GCMX_TX2_BLKT  // tuning builds only: per-wave start / end times (s_memrealtime, 100 MHz) and the
 #define GCMX_TX2_BLKT 0  // CU of every block of the last k_step_tx2 launch (gcmx_diag_blk*)
 #endif
@@ -479,7 +482,17 @@ __global__ __launch_bounds__(ZT, GCMX_TX2_MINWAVES) void k_step_tx2(
 	__shared__ double hode[HET ? kHetMaxMaterials : 1];  // HET: folded ODE factor per material
 	__shared__ double flds[FACES && GCMX_TX2_FACE_LDS ? 4 : 1][9];  // 2 f(t) of the y/z faces
 
+#if GCMX_TX2_ZPERM
+	// z blocks of 64 columns dealt so that the two waves sharing a SIMD (w and
+	// w + 4 of a 512-lane block) hold neighbouring z blocks 2w and 2w + 1
+	const int z = [] {
+		int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+		if constexpr (ZT == 512) w = w < 4 ? 2 * w : 2 * (w - 4) + 1;
+		return w * 64 + (int)(threadIdx.x & 63);
+	}();
+#else
 	const int z = threadIdx.x;
+#endif
 #if GCMX_TX2_BLKT
 	const unsigned long long blk_t0_ = __builtin_amdgcn_s_memrealtime();
 #endif
