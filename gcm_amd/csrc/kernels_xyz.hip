@@ -307,8 +307,8 @@ __device__ unsigned long long g_tx2_diag[16][8];  // [wave in block][phase]: cyc
 	do {              \
 	} while (0)
 #endif
-#ifndef GCMX_TX2_ZPERM  // tuning builds only: SIMD partners hold neighbouring z blocks
-#define GCMX_TX2_ZPERM 0
+#ifndef GCMX_TX2_ZPERM  // SIMD partners hold neighbouring z blocks (512^3: 3.548-3.570 against 3.572-3.589 ms, profiles/r6/w)
+#define GCMX_TX2_ZPERM 1
 #endif
 #ifndef GCMX_TX2_BLKT  // tuning builds only: per-wave start / end times (s_memrealtime, 100 MHz) and the
 #define GCMX_TX2_BLKT 0  // CU of every block of the last k_step_tx2 launch (gcmx_diag_blk*)
